@@ -1,0 +1,232 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Mrays/s at 3840x2160, 100k spheres, octree depth 8 (BASELINE.json).
+
+One step = one frame of primary rays (numSamples=1, maxDepth=1 -> one traversal per pixel)
+over the seeded synthetic sphere cloud, rendered by the gfx950 kernel with the scene
+already resident in HBM.  With N GPUs (one process per GPU, torchrun) the frame is
+partitioned into 16-row bands dealt round-robin to the ranks; each rank renders its bands
+into device memory and the bands are gathered to rank 0 over RCCL and de-interleaved into
+the final frame -- the gather is inside the timed region.  Total work per step is one
+frame whatever N is ("scaling": "strong").
+
+Prints ONE JSON line on rank 0 (contract in the task description).  Extra keys:
+  roofline      -- dominant kernel (ort_trace_kernel) against the HBM roof, algorithmic
+                   bytes = reference-layout record bytes per SURVEY.md 8(d), counted on the
+                   GPU by the kernel's counting variant, / HIP-event kernel time.
+  cpu_baseline  -- the CPU oracle (line-by-line restatement of the reference shader; the
+                   reference itself has no CPU path) on a bounded row sample, rank 0, N=1.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+CONFIGS = {
+    # name: (width, height, spheres, depth, max_spheres_per_node, num_samples, bounce depth)
+    "c1": (256, 256, 100, 4, 0, 1, 1),
+    "c2": (1920, 1080, 10_000, 6, 0, 1, 1),
+    "c3": (3840, 2160, 100_000, 8, 0, 1, 1),
+    "c5": (7680, 4320, 1_000_000, 10, 1, 1, 4),
+}
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+BAND = 16
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"),
+                    help="PMC-measured HBM bytes per launch (written by tools/pmc_traffic.py)")
+    ap.add_argument("--save", default="", help="rank 0: save the assembled frame (.pfm/.png)")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    W, H, NSPH, DEPTH, MPN, NS, MAXD = CONFIGS[args.config]
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+
+    import torch
+    import torch.distributed as dist
+
+    import octreeraytracer_amd as ort
+
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    t0 = time.time()
+    spheres = ort.random_spheres(NSPH, args.seed)
+    tree = ort.build_octree(spheres, DEPTH, MPN)
+    t_build = time.time() - t0
+    r = ort.Renderer(local)
+    t0 = time.time()
+    r.upload(spheres, tree)
+    t_upload = time.time() - t0
+    info = r.info()
+    p = ort.FrameParams.default_camera(W, H, num_samples=NS, max_depth=MAXD)
+
+    # partition: 16-row bands dealt round-robin; every rank renders the same number of rows
+    nbands = -(-H // BAND)
+    per = -(-nbands // world)
+    if world == 1:
+        tile = ort.Tile(0, W, 0, H)
+    else:
+        tile = ort.Tile(0, W, rank * BAND, per * BAND, BAND, BAND * world)
+    out = torch.empty((tile.rows, W, 3), dtype=torch.float32, device="cuda")
+    gathered = None
+    frame = None
+    if world > 1 and rank == 0:
+        gathered = torch.empty((world, tile.rows, W, 3), dtype=torch.float32, device="cuda")
+        frame = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+    stream = torch.cuda.current_stream()
+
+    def step():
+        r.render(p, tile, out=out, stream=stream.cuda_stream)
+        if world > 1:
+            dist.gather(out, list(gathered.unbind(0)) if rank == 0 else None, dst=0)
+            if rank == 0:
+                # [rank][band][16 rows] -> global band b*world + rank
+                g = gathered.view(world, per, BAND, W, 3).permute(1, 0, 2, 3, 4).reshape(per * world * BAND, W, 3)
+                frame.copy_(g[:H])
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        evs[k][0].record(stream)
+        r.render(p, tile, out=out, stream=stream.cuda_stream)
+        evs[k][1].record(stream)
+        if world > 1:
+            dist.gather(out, list(gathered.unbind(0)) if rank == 0 else None, dst=0)
+            if rank == 0:
+                g = gathered.view(world, per, BAND, W, 3).permute(1, 0, 2, 3, 4).reshape(per * world * BAND, W, 3)
+                frame.copy_(g[:H])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = [a.elapsed_time(b) for a, b in evs]
+    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    # algorithmic traffic of this rank's launch (counting variant, untimed)
+    counts = r.count_traffic(p, tile)
+    alg_bytes = ort.algorithmic_bytes(counts)
+    kern_avg_ms = float(np.mean(kern_ms))
+    rays_per_frame = W * H * NS
+
+    result = None
+    if rank == 0:
+        ms_per_step = elapsed / args.steps * 1e3
+        value = rays_per_frame * args.steps / elapsed / 1e6
+        achieved = alg_bytes / (kern_avg_ms * 1e-3) / 1e9
+        traffic = None
+        tj = Path(args.traffic_json)
+        if tj.exists():
+            try:
+                tr = json.loads(tj.read_text())
+                if tr.get("config") == args.config and tr.get("tile_rows") == tile.rows:
+                    traffic = tr.get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        result = {
+            "metric": "Mrays/sec at 3840x2160, 100k spheres, depth 8; 1/2/4/8-GPU scaling",
+            "value": round(value, 2),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded generateRandomSpheres restatement, mt19937 seed %d)" % args.seed,
+            "config": {
+                "workload": f"{args.config}: {W}x{H} primary rays (spp={NS}, bounces={MAXD}), {NSPH} spheres, "
+                            f"octree depth {DEPTH}, maxSpheresPerNode {MPN}",
+                "width": W, "height": H, "spheres": NSPH, "octree_depth": DEPTH, "max_spheres_per_node": MPN,
+                "num_samples": NS, "max_bounces": MAXD, "nodes": info["n_nodes"], "indices": info["n_indices"],
+                "layout": info["layout"], "partition": "16-row bands round-robin + RCCL gather" if world > 1
+                else "full frame", "rays_per_step": rays_per_frame,
+            },
+            "kernel_ms_avg": round(kern_avg_ms, 4),
+            "kernel_ms_min": round(float(np.min(kern_ms)), 4),
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "algorithmic_bytes_per_launch": int(alg_bytes),
+                "bytes_per_ray": round(alg_bytes / max(1, counts["pixels"]), 1),
+                "counts": counts,
+                "kernel": "ort_trace_kernel<0,false>",
+            },
+            "setup_s": {"scene_build": round(t_build, 3), "upload": round(t_upload, 3)},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            result["cpu_baseline"] = cpu_baseline(spheres, tree, p, args.cpu_seconds)
+        if args.save:
+            img = (frame if world > 1 else out).cpu().numpy()
+            from octreeraytracer_amd import image
+            (image.write_png if args.save.endswith(".png") else image.write_pfm)(args.save, img)
+    r.close()
+    if world > 1:
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+
+
+def cpu_baseline(spheres, tree, p, budget_s):
+    """Oracle on the host cores over evenly spaced full rows, sized to ~budget_s of wall time."""
+    from oracle import oracle
+    threads = min(16, os.cpu_count() or 1)
+
+    def run(n):
+        stride = max(1, p.height // n)
+        t0 = time.perf_counter()
+        oracle.render(spheres, tree, p, 0, stride // 2, p.width, n, band_height=1, band_stride=stride, threads=threads)
+        return time.perf_counter() - t0, stride
+
+    n = 2 * threads
+    dt, _ = run(n)  # calibration sample
+    n = int(max(n, min(p.height, n * budget_s / max(dt, 1e-3))))
+    dt, stride = run(n)
+    rays = n * p.width * p.num_samples
+    return {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"{n} of {p.height} rows (every {stride}th), {rays} primary rays, {dt:.1f} s wall; "
+                      f"oracle/ort_oracle.c -O3, OpenMP dynamic over rows"}
+
+
+if __name__ == "__main__":
+    main()

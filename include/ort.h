@@ -1,0 +1,182 @@
+/*
+ * ort.h -- C ABI of the MI355X octree ray tracer (libort.so).
+ *
+ * This is the drop-in boundary that replaces the reference's OpenGL path:
+ *
+ *   reference (GL, Tiago27Cruz/OctreeRayTracer)                         this ABI
+ *   ---------------------------------------------------------------------------------------
+ *   Raytracer::initialize -> startGLFW/setupQuad/setupShader         ort_create
+ *     (src/raytracer.cpp:32-60, src/main.cpp:60-102)
+ *   Raytracer::setupBuffers: 7x glBufferData SSBOs + static uniforms ort_upload_scene /
+ *     (src/raytracer.cpp:74-152; SSBO bindings glsl:20-46)             ort_upload_octree
+ *   per-frame uniforms view/cameraPosition/cameraZoom + glDrawArrays ort_render
+ *     (src/raytracer.cpp:491-499; uniforms glsl:13-18, 48-53)
+ *   Raytracer::cleanupBuffers (src/raytracer.cpp:154-162)            ort_destroy
+ *   (GL errors never checked; shader errors printed, shader.cpp:52-78) ort_last_error
+ *
+ * Conventions: every call returns an int status (ORT_OK == 0); no C++ exception crosses
+ * the ABI.  The context owns all device memory; host arrays passed in are copied.  One
+ * context per device; calls on one context are not thread-safe, different contexts may
+ * be driven from different threads.  ort_render is synchronous when stream == NULL and
+ * stream-ordered (asynchronous) otherwise.
+ *
+ * Deliberate deviation: node offsets are int32, not float as in the
+ * reference's vec4.w packing (src/raytracer.cpp:98-99), which is exact only below 2^24.
+ */
+#ifndef ORT_H
+#define ORT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ORT_OK 0
+#define ORT_ERR_INVALID_ARG 1
+#define ORT_ERR_HIP 2
+#define ORT_ERR_NO_SCENE 3
+#define ORT_ERR_OUT_OF_MEMORY 4
+#define ORT_ERR_UNSUPPORTED 5
+#define ORT_ERR_INTERNAL 6
+
+typedef struct ort_ctx ort_ctx;
+
+/* The shader's uniforms (glsl:13-18, 48-53).  view is column-major like glm::mat4
+ * (view[4*col + row]); model/projection are unused by the reference shader. */
+typedef struct ort_params {
+    int32_t width, height;      /* iResolution.xy of the FULL frame (src/raytracer.cpp:150) */
+    int32_t num_samples;        /* numSamples (src/config.h:20) */
+    int32_t max_depth;          /* maxDepth: bounces per path (src/config.h:23, MAXRAYSDEPTH) */
+    int32_t use_octree;         /* useOctree: 1 octree traversal, 0 brute force (glsl:500-506) */
+    float view[16];             /* view matrix uniform */
+    float camera_position[3];   /* cameraPosition uniform */
+    float camera_zoom;          /* cameraZoom uniform: vertical field of view in degrees */
+} ort_params;
+
+/* Which pixels to render.  Output row j (0-based) is pixel row
+ *     y = y0 + (j / band_height) * band_stride + (j % band_height)
+ * (band_height <= 0 means one band: y = y0 + j).  Pixel rows are GL rows: y = 0 is the
+ * BOTTOM row of the image.  Columns are x0 .. x0+width-1.  Rows with y >= height are
+ * written as zeros.  The RNG seed and the camera always use the full-frame resolution,
+ * so any tiling produces the same pixels as a full-frame render. */
+typedef struct ort_tile {
+    int32_t x0, width;
+    int32_t y0, rows;
+    int32_t band_height;
+    int32_t band_stride;
+} ort_tile;
+
+/* Per-scene information after upload. */
+typedef struct ort_scene_info {
+    int32_t n_spheres;
+    int32_t n_nodes;
+    int64_t n_indices;
+    int32_t layout;            /* ORT_LAYOUT_* actually selected */
+    int32_t tree_depth;        /* deepest node level (root = 0) */
+    int64_t device_bytes;      /* device memory held for the scene */
+} ort_scene_info;
+
+#define ORT_LAYOUT_COMPACT 0   /* 8-byte node records, boxes re-derived from per-axis split planes */
+#define ORT_LAYOUT_EXPLICIT 1  /* reference record layout, boxes read from memory */
+
+/* Options (ort_set_option). */
+#define ORT_OPT_FORCE_LAYOUT 1 /* -1 auto (default), or ORT_LAYOUT_* */
+
+/* Traffic counters (ort_count_traffic), in the REFERENCE layout's terms. */
+#define ORT_COUNT_NODES_POPPED 0
+#define ORT_COUNT_CHILD_RECORDS 1
+#define ORT_COUNT_LEAF_OBJECTS 2
+#define ORT_COUNT_ACCEPTED_HITS 3
+#define ORT_COUNT_PIXELS 4
+#define ORT_COUNT_TRAVERSALS 5
+#define ORT_COUNT_N 6
+
+/* ---- device context ---------------------------------------------------------------- */
+int ort_create(int device, ort_ctx** out);
+int ort_destroy(ort_ctx* ctx);
+/* Last error message for ctx (or of the calling thread when ctx == NULL). Never NULL. */
+const char* ort_last_error(const ort_ctx* ctx);
+int ort_set_option(ort_ctx* ctx, int option, int value);
+
+/* Upload a scene in the reference's packing (src/raytracer.cpp:87-101), SoA:
+ *   sphere_center_radius[4*i]  = center.xyz, radius          (SSBO binding 0)
+ *   sphere_mat_albedo[4*i]     = float(materialType), albedo (SSBO binding 1)
+ *   sphere_fuzz_ri[4*i]        = fuzz, refractionIndex, 0, 0 (SSBO binding 2)
+ *   node_min[3*k], node_max[3*k], children_offset[k], objects_offset[k], object_count[k]
+ *                                                            (SSBO bindings 3, 4, 5)
+ *   object_indices[n_indices]                                (SSBO binding 6)
+ * Replaces any previous scene on the context. */
+int ort_upload_scene(ort_ctx* ctx,
+                     const float* sphere_center_radius, const float* sphere_mat_albedo,
+                     const float* sphere_fuzz_ri, int32_t n_spheres,
+                     const float* node_min, const float* node_max,
+                     const int32_t* children_offset, const int32_t* objects_offset,
+                     const int32_t* object_count, int32_t n_nodes,
+                     const int32_t* object_indices, int64_t n_indices);
+
+/* Same, taking Octree::flattenedTree.data() directly (36-byte GPUOctreeNode records). */
+int ort_upload_octree_nodes(ort_ctx* ctx,
+                            const float* sphere_center_radius, const float* sphere_mat_albedo,
+                            const float* sphere_fuzz_ri, int32_t n_spheres,
+                            const void* gpu_octree_nodes, int32_t n_nodes,
+                            const int32_t* object_indices, int64_t n_indices);
+
+int ort_scene_get_info(const ort_ctx* ctx, ort_scene_info* info);
+
+/* Render the tile; rgb_out receives tile->rows * tile->width RGB float triples, row-major,
+ * output row 0 first.  out_is_device != 0: rgb_out is a device pointer on ctx's device.
+ * stream: a hipStream_t on ctx's device, or NULL for the context's own stream (then the
+ * call returns after the frame is complete). */
+int ort_render(ort_ctx* ctx, const ort_params* params, const ort_tile* tile,
+               float* rgb_out, int out_is_device, void* stream);
+
+/* Duration in milliseconds of the last ort_render's kernel, from HIP events recorded
+ * around the launch on its stream.  Only valid once that stream has passed the frame. */
+int ort_last_kernel_ms(ort_ctx* ctx, float* ms);
+
+/* Run the counting variant of the kernel over the tile and return, summed over all
+ * pixels, the reference-layout work counters ORT_COUNT_* (counts[ORT_COUNT_N]). */
+int ort_count_traffic(ort_ctx* ctx, const ort_params* params, const ort_tile* tile, uint64_t* counts);
+
+/* ---- host scene-build stage (kept reference API, src/raytracer.cpp + src/octree.cpp) -- */
+
+/* Raytracer::generateRandomSpheres (src/raytracer.cpp:254-337) with std::mt19937(seed)
+ * in place of std::random_device.  Writes n records to each SoA array (4 floats each). */
+int ort_scene_random(int32_t n, uint32_t seed, float* sphere_center_radius,
+                     float* sphere_mat_albedo, float* sphere_fuzz_ri);
+/* Raytracer::generatePreBuiltSpheres (src/raytracer.cpp:164-252): 83 spheres.
+ * Pass NULL arrays to query *n_out only. */
+int ort_scene_prebuilt(float* sphere_center_radius, float* sphere_mat_albedo,
+                       float* sphere_fuzz_ri, int32_t* n_out);
+/* The DEBUG scene (src/raytracer.cpp:342-347): 3 spheres. */
+int ort_scene_debug(float* sphere_center_radius, float* sphere_mat_albedo,
+                    float* sphere_fuzz_ri, int32_t* n_out);
+
+typedef struct ort_octree ort_octree;
+/* Octree(max_depth, max_spheres_per_node).build(spheres) (src/octree.cpp:47-95). */
+int ort_octree_build(const float* sphere_center_radius, int32_t n_spheres, int32_t max_depth,
+                     int32_t max_spheres_per_node, ort_octree** out);
+int ort_octree_sizes(const ort_octree* tree, int64_t* n_nodes, int64_t* n_indices, double* build_seconds);
+/* Copy out in SoA form (any pointer may be NULL to skip that array). */
+int ort_octree_export(const ort_octree* tree, float* node_min, float* node_max,
+                      int32_t* children_offset, int32_t* objects_offset, int32_t* object_count,
+                      int32_t* object_indices);
+/* Zero-copy views: GPUOctreeNode[n_nodes] (36-byte records) and objectIndices. */
+const void* ort_octree_nodes(const ort_octree* tree);
+const int32_t* ort_octree_indices(const ort_octree* tree);
+void ort_octree_free(ort_octree* tree);
+
+/* Camera(position, world_up, yaw, pitch).GetViewMatrix() (src/opengl/camera.h:45-67,115-126):
+ * view_out[16] column-major. */
+int ort_camera_view(const float position[3], const float world_up[3], float yaw_deg, float pitch_deg,
+                    float view_out[16]);
+
+/* Library version string. */
+const char* ort_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ORT_H */

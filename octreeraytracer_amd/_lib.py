@@ -1,0 +1,132 @@
+"""ctypes binding of libort.so (include/ort.h).
+
+The library is built in-tree (``make lib`` / ``__graft_entry__.build()``) at
+``octreeraytracer_amd/lib/libort.so``.  There is no Python or CPU fallback for the render
+path: if the library (or a GPU) is missing, the calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+LIB_PATH = Path(__file__).resolve().parent / "lib" / "libort.so"
+
+ORT_OK = 0
+ORT_ERR_INVALID_ARG = 1
+ORT_ERR_HIP = 2
+ORT_ERR_NO_SCENE = 3
+ORT_ERR_OUT_OF_MEMORY = 4
+ORT_ERR_UNSUPPORTED = 5
+ORT_ERR_INTERNAL = 6
+
+ORT_LAYOUT_COMPACT = 0
+ORT_LAYOUT_EXPLICIT = 1
+ORT_OPT_FORCE_LAYOUT = 1
+ORT_COUNT_N = 6
+COUNT_NAMES = ("nodes_popped", "child_records", "leaf_objects", "accepted_hits", "pixels", "traversals")
+
+# Every symbol include/ort.h declares (checked by tests/test_abi.py).
+EXPORTED_SYMBOLS = (
+    "ort_create", "ort_destroy", "ort_last_error", "ort_set_option", "ort_upload_scene",
+    "ort_upload_octree_nodes", "ort_scene_get_info", "ort_render", "ort_last_kernel_ms",
+    "ort_count_traffic", "ort_scene_random", "ort_scene_prebuilt", "ort_scene_debug",
+    "ort_octree_build", "ort_octree_sizes", "ort_octree_export", "ort_octree_nodes",
+    "ort_octree_indices", "ort_octree_free", "ort_camera_view", "ort_version",
+)
+
+
+class OrtParams(C.Structure):
+    _fields_ = [
+        ("width", C.c_int32), ("height", C.c_int32), ("num_samples", C.c_int32),
+        ("max_depth", C.c_int32), ("use_octree", C.c_int32), ("view", C.c_float * 16),
+        ("camera_position", C.c_float * 3), ("camera_zoom", C.c_float),
+    ]
+
+
+class OrtTile(C.Structure):
+    _fields_ = [
+        ("x0", C.c_int32), ("width", C.c_int32), ("y0", C.c_int32), ("rows", C.c_int32),
+        ("band_height", C.c_int32), ("band_stride", C.c_int32),
+    ]
+
+
+class OrtSceneInfo(C.Structure):
+    _fields_ = [
+        ("n_spheres", C.c_int32), ("n_nodes", C.c_int32), ("n_indices", C.c_int64),
+        ("layout", C.c_int32), ("tree_depth", C.c_int32), ("device_bytes", C.c_int64),
+    ]
+
+
+class OrtError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"ort error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+
+_fp = C.POINTER(C.c_float)
+_ip = C.POINTER(C.c_int32)
+_u64p = C.POINTER(C.c_uint64)
+_vp = C.c_void_p
+
+
+def _declare(lib):
+    sig = {
+        "ort_create": (C.c_int, [C.c_int, C.POINTER(_vp)]),
+        "ort_destroy": (C.c_int, [_vp]),
+        "ort_last_error": (C.c_char_p, [_vp]),
+        "ort_set_option": (C.c_int, [_vp, C.c_int, C.c_int]),
+        "ort_upload_scene": (C.c_int, [_vp, _fp, _fp, _fp, C.c_int32, _fp, _fp, _ip, _ip, _ip, C.c_int32, _ip, C.c_int64]),
+        "ort_upload_octree_nodes": (C.c_int, [_vp, _fp, _fp, _fp, C.c_int32, _vp, C.c_int32, _ip, C.c_int64]),
+        "ort_scene_get_info": (C.c_int, [_vp, C.POINTER(OrtSceneInfo)]),
+        "ort_render": (C.c_int, [_vp, C.POINTER(OrtParams), C.POINTER(OrtTile), _vp, C.c_int, _vp]),
+        "ort_last_kernel_ms": (C.c_int, [_vp, _fp]),
+        "ort_count_traffic": (C.c_int, [_vp, C.POINTER(OrtParams), C.POINTER(OrtTile), _u64p]),
+        "ort_scene_random": (C.c_int, [C.c_int32, C.c_uint32, _fp, _fp, _fp]),
+        "ort_scene_prebuilt": (C.c_int, [_fp, _fp, _fp, _ip]),
+        "ort_scene_debug": (C.c_int, [_fp, _fp, _fp, _ip]),
+        "ort_octree_build": (C.c_int, [_fp, C.c_int32, C.c_int32, C.c_int32, C.POINTER(_vp)]),
+        "ort_octree_sizes": (C.c_int, [_vp, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.POINTER(C.c_double)]),
+        "ort_octree_export": (C.c_int, [_vp, _fp, _fp, _ip, _ip, _ip, _ip]),
+        "ort_octree_nodes": (_vp, [_vp]),
+        "ort_octree_indices": (_ip, [_vp]),
+        "ort_octree_free": (None, [_vp]),
+        "ort_camera_view": (C.c_int, [_fp, _fp, C.c_float, C.c_float, _fp]),
+        "ort_version": (C.c_char_p, []),
+        "ort_debug_emulate_render": (C.c_int, [_fp, _fp, _fp, C.c_int32, _fp, _fp, _ip, _ip, _ip, C.c_int32, _ip,
+                                               C.c_int64, C.c_int32, C.POINTER(OrtParams), C.POINTER(OrtTile),
+                                               _fp, _u64p]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+
+
+def lib():
+    """Load libort.so (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        path = os.environ.get("ORT_LIB", str(LIB_PATH))
+        if not Path(path).exists():
+            raise OSError(f"libort.so not found at {path}: run `make lib` or __graft_entry__.build()")
+        l = C.CDLL(path, mode=C.RTLD_GLOBAL)
+        _declare(l)
+        _lib = l
+    return _lib
+
+
+def check(rc: int, ctx=None):
+    if rc != ORT_OK:
+        msg = lib().ort_last_error(ctx)
+        raise OrtError(rc, msg.decode() if msg else "")
+
+
+def fptr(a):
+    return a.ctypes.data_as(_fp) if a is not None else None
+
+
+def iptr(a):
+    return a.ctypes.data_as(_ip) if a is not None else None

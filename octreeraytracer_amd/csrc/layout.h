@@ -1,0 +1,63 @@
+// layout.h -- host-side conversion of the reference buffer layout into the kernel's
+// compact layout (the "layout compiler" run once per ort_upload_*).
+//
+// Reference layout (src/raytracer.cpp:87-101): per node min.xyz/childrenOffset and
+// max.xyz/objectsOffset vec4s + objectCount; objectIndices; 36 B read per node popped plus
+// 32 B per child box examined (glsl:318-324, 459-462).
+//
+// Compact layout (MI355X):
+//   node[i] (8 B):  internal -> {childrenOffset, 0x80000000 | childMask}
+//                   leaf     -> {objectsOffset, objectCount}
+//     childMask bit k = child (childrenOffset + k) is in range and is not an empty leaf
+//     (the glsl:456 and glsl:467 skip tests, precomputed).
+//   leaf_sph[e] = spheres[objectIndices[e]] (16 B): one gather instead of index + sphere.
+//   leaf_idx[e] = objectIndices[e], read only for the final hit (material lookup).
+//   planes[a][k], k = 0..2^D: coordinate of the axis-a split plane at dyadic position
+//     k / 2^D.  The reference builder derives every child box from its parent by
+//     mid = (min+max)*0.5f and copies min/mid/max verbatim (src/octree.cpp:97-187, 197),
+//     so the box of the node at depth d, cell (cx,cy,cz) is exactly
+//     [planes[x][cx<<(D-d)], planes[x][(cx+1)<<(D-d)]] x ...; boxes are therefore
+//     re-derived bit-exactly in the kernel instead of being read (8 x 32 B per node).
+//     The conversion VERIFIES this for every reachable node; a tree that does not
+//     satisfy it (e.g. hand-made) is uploaded in the explicit reference layout instead.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace ort {
+
+struct SceneInput {
+    const float* sph_cr;
+    const float* sph_ma;
+    const float* sph_fr;
+    int32_t n_spheres;
+    const float* node_min;  // 3 per node
+    const float* node_max;
+    const int32_t* co;
+    const int32_t* oo;
+    const int32_t* cnt;
+    int32_t n_nodes;
+    const int32_t* indices;
+    int64_t n_indices;
+};
+
+struct CompactLayout {
+    int depth = 0;                 // D
+    std::vector<float> planes;     // 3 * (2^D + 1)
+    std::vector<uint32_t> node;    // 2 per node
+    std::vector<float> leaf_sph;   // 4 per index entry
+    std::vector<int32_t> leaf_idx; // 1 per index entry
+};
+
+// Validates the scene like the reference would need (index ranges); returns "" or a message.
+std::string validateScene(const SceneInput& in);
+
+// Builds the compact layout; returns false (with `why`) if the tree is not representable
+// (boxes not derivable by midpoint splits, node reachable twice, depth > maxDepth).
+bool buildCompactLayout(const SceneInput& in, int maxDepth, CompactLayout& out, std::string& why);
+
+// Maximum node depth reachable from the root (BFS), or -1 if a node is reached twice.
+int treeDepth(const SceneInput& in);
+
+}  // namespace ort

@@ -1,0 +1,23 @@
+// ort_internal.h -- internal declarations shared by the host .cpp files and the .hip file.
+#pragma once
+#include <cstdint>
+#include <string>
+
+#include "../../include/ort.h"
+
+namespace ort {
+void set_thread_error(const std::string& msg);
+const char* thread_error();
+}  // namespace ort
+
+extern "C" {
+// TEST-ONLY: run the kernel's per-pixel code (render_core.h, compact or explicit layout)
+// on the host CPU, single-threaded, for CPU-side validation of the traversal logic
+// against the independent oracle.  Never called by ort_render (which has no CPU path).
+int ort_debug_emulate_render(const float* sphere_center_radius, const float* sphere_mat_albedo,
+                             const float* sphere_fuzz_ri, int32_t n_spheres, const float* node_min,
+                             const float* node_max, const int32_t* children_offset,
+                             const int32_t* objects_offset, const int32_t* object_count, int32_t n_nodes,
+                             const int32_t* object_indices, int64_t n_indices, int32_t layout,
+                             const ort_params* params, const ort_tile* tile, float* rgb_out, uint64_t* counts);
+}

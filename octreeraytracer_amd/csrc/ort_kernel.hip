@@ -1,0 +1,574 @@
+// ort_kernel.hip -- gfx950 primary/secondary-ray kernel and the device half of the C ABI.
+//
+// Replaces the reference's GL dispatch: setupBuffers' SSBO uploads
+// (src/raytracer.cpp:74-152) become ort_upload_*; the per-frame uniform update +
+// glDrawArrays (src/raytracer.cpp:491-499) becomes ort_render, which launches
+// ort_trace_kernel: one pixel per lane, a 64-lane wave = an 8x8 pixel block, a 256-lane
+// workgroup = a 16x16 tile.  The fragment shader body (glsl:636-664) runs per lane from
+// render_core.h.  The octree walk keeps one frame per tree level in LDS (columns indexed
+// by lane: conflict-free), per-level child masks in registers, and the split-plane table
+// of the tree in LDS (3 x (2^D+1) floats, loaded once per workgroup).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "camera.h"
+#include "layout.h"
+#include "ort_internal.h"
+#include "render_core.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+constexpr int kBlock = 256;  // 4 waves, 16x16 pixels
+
+struct TileMap {
+    int x0, tw, y0, th, bh, bs;
+};
+
+struct LaunchArgs {
+    ort::PixelParams pp;
+    ort::KScene S;
+    TileMap tm;
+    int tilesX;
+    float* out;
+    unsigned long long* counters;
+};
+
+__host__ __device__ inline int tile_row_to_y(const TileMap& t, int j) {
+    return t.bh > 0 ? t.y0 + (j / t.bh) * t.bs + (j % t.bh) : t.y0 + j;
+}
+
+__host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+size_t lds_bytes(int mode, int depth) {
+    if (mode != 0) return 0;
+    const size_t planes = align16(sizeof(float) * 3 * (((size_t)1 << depth) + 1));
+    const size_t levels = (size_t)std::max(depth, 1);
+    return planes + 2 * levels * kBlock * sizeof(int);
+}
+
+template <int MODE, bool COUNT>
+__global__ void __launch_bounds__(kBlock) ort_trace_kernel(LaunchArgs A) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int tid = threadIdx.x;
+    const float* planes = nullptr;
+    ort::LdsFrames fr;
+    fr.co = nullptr;
+    fr.tm = nullptr;
+    fr.stride = kBlock;
+    fr.lane = tid;
+    if constexpr (MODE == 0) {
+        const int D = A.S.depth;
+        const int np = 3 * ((1 << D) + 1);
+        float* lp = reinterpret_cast<float*>(smem);
+        for (int i = tid; i < np; i += kBlock) lp[i] = A.S.planes[i];
+        const size_t poff = align16(sizeof(float) * (size_t)np);
+        fr.co = reinterpret_cast<int*>(smem + poff);
+        fr.tm = reinterpret_cast<float*>(smem + poff + (size_t)(D > 0 ? D : 1) * kBlock * sizeof(int));
+        planes = lp;
+        __syncthreads();
+    }
+    const int wave = tid >> 6, lane = tid & 63;
+    const int bx = blockIdx.x % A.tilesX, by = blockIdx.x / A.tilesX;
+    const int col = bx * 16 + (wave & 1) * 8 + (lane & 7);
+    const int row = by * 16 + (wave >> 1) * 8 + (lane >> 3);
+    if (col >= A.tm.tw || row >= A.tm.th) return;
+    const int y = tile_row_to_y(A.tm, row);
+    float* o = A.out + 3 * ((size_t)row * (size_t)A.tm.tw + (size_t)col);
+    if (y >= A.pp.H) {
+        o[0] = 0.0f; o[1] = 0.0f; o[2] = 0.0f;
+        return;
+    }
+    ort::Counters cnt;
+    for (int k = 0; k < 6; ++k) cnt.v[k] = 0;
+    ort::V3 c;
+    if constexpr (MODE == 1) {
+        int snode[ORT_MAX_STACK];
+        float stmin[ORT_MAX_STACK];
+        c = ort::shade_pixel<MODE, COUNT>(A.pp, A.S, planes, fr, snode, stmin, A.tm.x0 + col, y, cnt);
+    } else {
+        c = ort::shade_pixel<MODE, COUNT>(A.pp, A.S, planes, fr, nullptr, nullptr, A.tm.x0 + col, y, cnt);
+    }
+    o[0] = c.x;
+    o[1] = c.y;
+    o[2] = c.z;
+    if constexpr (COUNT) {
+        cnt.v[4] = 1;
+        for (int k = 0; k < 6; ++k)
+            if (cnt.v[k]) atomicAdd(A.counters + k, cnt.v[k]);
+    }
+}
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+
+}  // namespace
+
+struct ort_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool timed = false;
+    std::string err;
+    int force_layout = -1;
+    bool has_scene = false;
+    int layout = ORT_LAYOUT_EXPLICIT;
+    int depth = 0;
+    int32_t n_spheres = 0, n_nodes = 0;
+    int64_t n_indices = 0;
+    DevBuf sph_cr, sph_ma, sph_fr;
+    DevBuf node, leaf_sph, leaf_idx, planes;    // compact
+    DevBuf nodeA, nodeB, cnt, indices;           // explicit
+    DevBuf scratch_out, counters;
+};
+
+namespace {
+
+int fail(ort_ctx* ctx, int code, const std::string& msg) {
+    if (ctx) ctx->err = msg;
+    ort::set_thread_error(msg);
+    return code;
+}
+
+int hip_fail(ort_ctx* ctx, hipError_t e, const char* what) {
+    return fail(ctx, e == hipErrorOutOfMemory ? ORT_ERR_OUT_OF_MEMORY : ORT_ERR_HIP,
+                std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HIPCHK(ctx, expr)                                  \
+    do {                                                   \
+        hipError_t _e = (expr);                            \
+        if (_e != hipSuccess) return hip_fail(ctx, _e, #expr); \
+    } while (0)
+
+void free_buf(DevBuf& b) {
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
+}
+
+void free_scene(ort_ctx* c) {
+    DevBuf* all[] = {&c->sph_cr, &c->sph_ma, &c->sph_fr, &c->node, &c->leaf_sph, &c->leaf_idx,
+                     &c->planes, &c->nodeA, &c->nodeB, &c->cnt, &c->indices};
+    for (DevBuf* b : all) free_buf(*b);
+    c->has_scene = false;
+}
+
+int upload(ort_ctx* ctx, DevBuf& b, const void* src, size_t bytes) {
+    free_buf(b);
+    if (bytes == 0) bytes = 16;  // keep a valid pointer for empty arrays
+    HIPCHK(ctx, hipMalloc(&b.p, bytes));
+    b.bytes = bytes;
+    if (src) HIPCHK(ctx, hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+    return ORT_OK;
+}
+
+int upload_impl(ort_ctx* ctx, const ort::SceneInput& in) {
+    const std::string bad = ort::validateScene(in);
+    if (!bad.empty()) return fail(ctx, ORT_ERR_INVALID_ARG, "ort_upload_scene: " + bad);
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    free_scene(ctx);
+    // spheres: binding 0, 1 and the .xy of binding 2
+    std::vector<float> fr2((size_t)in.n_spheres * 2);
+    for (int32_t i = 0; i < in.n_spheres; ++i) {
+        fr2[2 * (size_t)i] = in.sph_fr[4 * (size_t)i];
+        fr2[2 * (size_t)i + 1] = in.sph_fr[4 * (size_t)i + 1];
+    }
+    int rc;
+    if ((rc = upload(ctx, ctx->sph_cr, in.sph_cr, 16 * (size_t)in.n_spheres))) return rc;
+    if ((rc = upload(ctx, ctx->sph_ma, in.sph_ma, 16 * (size_t)in.n_spheres))) return rc;
+    if ((rc = upload(ctx, ctx->sph_fr, fr2.data(), 8 * (size_t)in.n_spheres))) return rc;
+    ctx->n_spheres = in.n_spheres;
+    ctx->n_nodes = in.n_nodes;
+    ctx->n_indices = in.n_indices;
+    ctx->layout = ORT_LAYOUT_EXPLICIT;
+    ctx->depth = 0;
+    if (in.n_nodes > 0) {
+        ort::CompactLayout cl;
+        std::string why;
+        const bool want_compact = ctx->force_layout != ORT_LAYOUT_EXPLICIT;
+        const bool compact_ok = want_compact && ort::buildCompactLayout(in, ORT_COMPACT_MAX_DEPTH, cl, why);
+        if (ctx->force_layout == ORT_LAYOUT_COMPACT && !compact_ok)
+            return fail(ctx, ORT_ERR_UNSUPPORTED, "compact layout forced but not possible: " + why);
+        if (compact_ok) {
+            ctx->layout = ORT_LAYOUT_COMPACT;
+            ctx->depth = cl.depth;
+            if ((rc = upload(ctx, ctx->node, cl.node.data(), 4 * cl.node.size()))) return rc;
+            if ((rc = upload(ctx, ctx->leaf_sph, cl.leaf_sph.data(), 4 * cl.leaf_sph.size()))) return rc;
+            if ((rc = upload(ctx, ctx->leaf_idx, cl.leaf_idx.data(), 4 * cl.leaf_idx.size()))) return rc;
+            if ((rc = upload(ctx, ctx->planes, cl.planes.data(), 4 * cl.planes.size()))) return rc;
+            HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        } else {
+            const int d = ort::treeDepth(in);
+            ctx->depth = d < 0 ? 0 : d;
+            std::vector<float> A(4 * (size_t)in.n_nodes), B(4 * (size_t)in.n_nodes);
+            for (int32_t i = 0; i < in.n_nodes; ++i) {
+                for (int k = 0; k < 3; ++k) {
+                    A[4 * (size_t)i + k] = in.node_min[3 * (size_t)i + k];
+                    B[4 * (size_t)i + k] = in.node_max[3 * (size_t)i + k];
+                }
+                std::memcpy(&A[4 * (size_t)i + 3], &in.co[i], 4);
+                std::memcpy(&B[4 * (size_t)i + 3], &in.oo[i], 4);
+            }
+            if ((rc = upload(ctx, ctx->nodeA, A.data(), 4 * A.size()))) return rc;
+            if ((rc = upload(ctx, ctx->nodeB, B.data(), 4 * B.size()))) return rc;
+            if ((rc = upload(ctx, ctx->cnt, in.cnt, 4 * (size_t)in.n_nodes))) return rc;
+            if ((rc = upload(ctx, ctx->indices, in.indices, 4 * (size_t)in.n_indices))) return rc;
+            HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        }
+    } else {
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    }
+    ctx->has_scene = true;
+    return ORT_OK;
+}
+
+ort::KScene device_scene(const ort_ctx* c) {
+    ort::KScene S;
+    std::memset(&S, 0, sizeof(S));
+    S.sph_cr = (const float4*)c->sph_cr.p;
+    S.sph_ma = (const float4*)c->sph_ma.p;
+    S.sph_fr = (const float2*)c->sph_fr.p;
+    S.n_spheres = c->n_spheres;
+    S.n_nodes = c->n_nodes;
+    S.node = (const uint2*)c->node.p;
+    S.leaf_sph = (const float4*)c->leaf_sph.p;
+    S.leaf_idx = (const int*)c->leaf_idx.p;
+    S.planes = (const float*)c->planes.p;
+    S.depth = c->depth;
+    S.nodeA = (const float4*)c->nodeA.p;
+    S.nodeB = (const float4*)c->nodeB.p;
+    S.count = (const int*)c->cnt.p;
+    S.indices = (const int*)c->indices.p;
+    return S;
+}
+
+ort::KCamera to_kcamera(const ort::CameraFrame& f) {
+    ort::KCamera k;
+    k.origin = ort::mk(f.origin[0], f.origin[1], f.origin[2]);
+    k.lowerLeft = ort::mk(f.lowerLeft[0], f.lowerLeft[1], f.lowerLeft[2]);
+    k.horizontal = ort::mk(f.horizontal[0], f.horizontal[1], f.horizontal[2]);
+    k.vertical = ort::mk(f.vertical[0], f.vertical[1], f.vertical[2]);
+    k.u = ort::mk(f.u[0], f.u[1], f.u[2]);
+    k.v = ort::mk(f.v[0], f.v[1], f.v[2]);
+    k.w = ort::mk(f.w[0], f.w[1], f.w[2]);
+    k.lensRadius = f.lensRadius;
+    return k;
+}
+
+std::string check_params(const ort_params* p, const ort_tile* t) {
+    if (!p || !t) return "null params or tile";
+    if (p->width <= 0 || p->height <= 0) return "width/height must be positive";
+    if (t->width < 0 || t->rows < 0) return "negative tile size";
+    if (t->x0 < 0 || (int64_t)t->x0 + t->width > p->width) return "tile columns outside the frame";
+    if (t->y0 < 0) return "negative y0";
+    if (t->band_height > 0 && t->band_stride < t->band_height) return "band_stride < band_height";
+    return "";
+}
+
+ort::PixelParams pixel_params(const ort_params* p) {
+    ort::PixelParams pp;
+    const ort::CameraFrame f = ort::cameraFrameFromView(p->view, p->camera_position, p->camera_zoom,
+                                                        (float)p->width / (float)p->height);
+    pp.cam = to_kcamera(f);
+    pp.W = p->width;
+    pp.H = p->height;
+    pp.ns = p->num_samples;
+    pp.maxDepth = p->max_depth;
+    return pp;
+}
+
+template <bool COUNT>
+hipError_t launch(int mode, const LaunchArgs& a, int blocks, size_t lds, hipStream_t s) {
+    if (mode == 0) hipLaunchKernelGGL((ort_trace_kernel<0, COUNT>), dim3(blocks), dim3(kBlock), lds, s, a);
+    else if (mode == 1) hipLaunchKernelGGL((ort_trace_kernel<1, COUNT>), dim3(blocks), dim3(kBlock), lds, s, a);
+    else hipLaunchKernelGGL((ort_trace_kernel<2, COUNT>), dim3(blocks), dim3(kBlock), lds, s, a);
+    return hipGetLastError();
+}
+
+int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out, int out_is_device,
+                void* stream, unsigned long long* dcounters) {
+    const std::string bad = check_params(p, t);
+    if (!bad.empty()) return fail(ctx, ORT_ERR_INVALID_ARG, "ort_render: " + bad);
+    if (!ctx->has_scene) return fail(ctx, ORT_ERR_NO_SCENE, "ort_render: no scene uploaded");
+    const int mode = (p->use_octree == 1) ? (ctx->layout == ORT_LAYOUT_COMPACT ? 0 : 1) : 2;
+    if (mode != 2 && ctx->n_nodes <= 0) return fail(ctx, ORT_ERR_NO_SCENE, "ort_render: scene has no octree");
+    if (!out && (size_t)t->width * (size_t)t->rows > 0) return fail(ctx, ORT_ERR_INVALID_ARG, "ort_render: null output");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    const size_t pix = (size_t)t->width * (size_t)t->rows;
+    float* dout = out;
+    if (!out_is_device && pix > 0) {
+        if (ctx->scratch_out.bytes < 12 * pix) {
+            free_buf(ctx->scratch_out);
+            HIPCHK(ctx, hipMalloc(&ctx->scratch_out.p, 12 * pix));
+            ctx->scratch_out.bytes = 12 * pix;
+        }
+        dout = (float*)ctx->scratch_out.p;
+    }
+    LaunchArgs a;
+    a.pp = pixel_params(p);
+    a.S = device_scene(ctx);
+    a.tm = {t->x0, t->width, t->y0, t->rows, t->band_height, t->band_stride};
+    a.tilesX = (t->width + 15) / 16;
+    a.out = dout;
+    a.counters = dcounters;
+    const int tilesY = (t->rows + 15) / 16;
+    const long long blocks = (long long)a.tilesX * tilesY;
+    if (blocks > 0) {
+        if (blocks > 0x7fffffffLL) return fail(ctx, ORT_ERR_INVALID_ARG, "ort_render: tile too large");
+        const size_t lds = lds_bytes(mode, ctx->depth);
+        HIPCHK(ctx, hipEventRecord(ctx->ev0, s));
+        hipError_t e = dcounters ? launch<true>(mode, a, (int)blocks, lds, s) : launch<false>(mode, a, (int)blocks, lds, s);
+        if (e != hipSuccess) return hip_fail(ctx, e, "ort_trace_kernel launch");
+        HIPCHK(ctx, hipEventRecord(ctx->ev1, s));
+        ctx->timed = true;
+    }
+    if (!out_is_device && pix > 0) {
+        HIPCHK(ctx, hipMemcpyAsync(out, dout, 12 * pix, hipMemcpyDeviceToHost, s));
+        HIPCHK(ctx, hipStreamSynchronize(s));
+    } else if (!stream) {
+        HIPCHK(ctx, hipStreamSynchronize(s));
+    }
+    return ORT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ort_create(int device, ort_ctx** out) {
+    if (!out) return fail(nullptr, ORT_ERR_INVALID_ARG, "ort_create: null out");
+    *out = nullptr;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) return hip_fail(nullptr, e, "hipGetDeviceCount");
+    if (device < 0 || device >= n)
+        return fail(nullptr, ORT_ERR_INVALID_ARG, "ort_create: device " + std::to_string(device) + " not present (" +
+                                                      std::to_string(n) + " visible)");
+    ort_ctx* c = new (std::nothrow) ort_ctx();
+    if (!c) return fail(nullptr, ORT_ERR_OUT_OF_MEMORY, "ort_create: out of host memory");
+    c->device = device;
+    if ((e = hipSetDevice(device)) != hipSuccess || (e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipEventCreate(&c->ev0)) != hipSuccess || (e = hipEventCreate(&c->ev1)) != hipSuccess) {
+        const int rc = hip_fail(nullptr, e, "ort_create");
+        delete c;
+        return rc;
+    }
+    *out = c;
+    return ORT_OK;
+}
+
+int ort_destroy(ort_ctx* ctx) {
+    if (!ctx) return ORT_OK;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    free_scene(ctx);
+    free_buf(ctx->scratch_out);
+    free_buf(ctx->counters);
+    if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
+    if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return ORT_OK;
+}
+
+const char* ort_last_error(const ort_ctx* ctx) { return ctx ? ctx->err.c_str() : ort::thread_error(); }
+
+int ort_set_option(ort_ctx* ctx, int option, int value) {
+    if (!ctx) return fail(nullptr, ORT_ERR_INVALID_ARG, "ort_set_option: null ctx");
+    if (option == ORT_OPT_FORCE_LAYOUT) {
+        if (value < -1 || value > ORT_LAYOUT_EXPLICIT) return fail(ctx, ORT_ERR_INVALID_ARG, "bad layout");
+        ctx->force_layout = value;
+        return ORT_OK;
+    }
+    return fail(ctx, ORT_ERR_INVALID_ARG, "unknown option");
+}
+
+int ort_upload_scene(ort_ctx* ctx, const float* cr, const float* ma, const float* fr, int32_t n_spheres,
+                     const float* node_min, const float* node_max, const int32_t* co, const int32_t* oo,
+                     const int32_t* cnt, int32_t n_nodes, const int32_t* idx, int64_t n_indices) {
+    if (!ctx) return fail(nullptr, ORT_ERR_INVALID_ARG, "ort_upload_scene: null ctx");
+    try {
+        ort::SceneInput in{cr, ma, fr, n_spheres, node_min, node_max, co, oo, cnt, n_nodes, idx, n_indices};
+        return upload_impl(ctx, in);
+    } catch (const std::bad_alloc&) {
+        return fail(ctx, ORT_ERR_OUT_OF_MEMORY, "ort_upload_scene: out of host memory");
+    } catch (const std::exception& ex) {
+        return fail(ctx, ORT_ERR_INTERNAL, std::string("ort_upload_scene: ") + ex.what());
+    }
+}
+
+int ort_upload_octree_nodes(ort_ctx* ctx, const float* cr, const float* ma, const float* fr, int32_t n_spheres,
+                            const void* nodes, int32_t n_nodes, const int32_t* idx, int64_t n_indices) {
+    if (!ctx) return fail(nullptr, ORT_ERR_INVALID_ARG, "ort_upload_octree_nodes: null ctx");
+    if (n_nodes < 0 || (n_nodes > 0 && !nodes)) return fail(ctx, ORT_ERR_INVALID_ARG, "ort_upload_octree_nodes: bad nodes");
+    try {
+        struct Rec { float mn[3], mx[3]; int32_t co, oo, cnt; };
+        static_assert(sizeof(Rec) == 36, "GPUOctreeNode layout");
+        const Rec* r = (const Rec*)nodes;
+        std::vector<float> mn(3 * (size_t)n_nodes), mx(3 * (size_t)n_nodes);
+        std::vector<int32_t> co((size_t)n_nodes), oo((size_t)n_nodes), cn((size_t)n_nodes);
+        for (int32_t i = 0; i < n_nodes; ++i) {
+            std::memcpy(&mn[3 * (size_t)i], r[i].mn, 12);
+            std::memcpy(&mx[3 * (size_t)i], r[i].mx, 12);
+            co[i] = r[i].co;
+            oo[i] = r[i].oo;
+            cn[i] = r[i].cnt;
+        }
+        ort::SceneInput in{cr, ma, fr, n_spheres, mn.data(), mx.data(), co.data(), oo.data(), cn.data(), n_nodes, idx, n_indices};
+        return upload_impl(ctx, in);
+    } catch (const std::bad_alloc&) {
+        return fail(ctx, ORT_ERR_OUT_OF_MEMORY, "ort_upload_octree_nodes: out of host memory");
+    } catch (const std::exception& ex) {
+        return fail(ctx, ORT_ERR_INTERNAL, std::string("ort_upload_octree_nodes: ") + ex.what());
+    }
+}
+
+int ort_scene_get_info(const ort_ctx* ctx, ort_scene_info* info) {
+    if (!ctx || !info) return fail(nullptr, ORT_ERR_INVALID_ARG, "ort_scene_get_info: null argument");
+    if (!ctx->has_scene) return fail(const_cast<ort_ctx*>(ctx), ORT_ERR_NO_SCENE, "no scene uploaded");
+    info->n_spheres = ctx->n_spheres;
+    info->n_nodes = ctx->n_nodes;
+    info->n_indices = ctx->n_indices;
+    info->layout = ctx->layout;
+    info->tree_depth = ctx->depth;
+    const DevBuf* all[] = {&ctx->sph_cr, &ctx->sph_ma, &ctx->sph_fr, &ctx->node, &ctx->leaf_sph, &ctx->leaf_idx,
+                           &ctx->planes, &ctx->nodeA, &ctx->nodeB, &ctx->cnt, &ctx->indices};
+    int64_t b = 0;
+    for (const DevBuf* d : all) b += (int64_t)d->bytes;
+    info->device_bytes = b;
+    return ORT_OK;
+}
+
+int ort_render(ort_ctx* ctx, const ort_params* params, const ort_tile* tile, float* rgb_out, int out_is_device,
+               void* stream) {
+    if (!ctx) return fail(nullptr, ORT_ERR_INVALID_ARG, "ort_render: null ctx");
+    return render_impl(ctx, params, tile, rgb_out, out_is_device, stream, nullptr);
+}
+
+int ort_last_kernel_ms(ort_ctx* ctx, float* ms) {
+    if (!ctx || !ms) return fail(nullptr, ORT_ERR_INVALID_ARG, "ort_last_kernel_ms: null argument");
+    if (!ctx->timed) return fail(ctx, ORT_ERR_NO_SCENE, "no kernel launched yet");
+    HIPCHK(ctx, hipEventSynchronize(ctx->ev1));
+    HIPCHK(ctx, hipEventElapsedTime(ms, ctx->ev0, ctx->ev1));
+    return ORT_OK;
+}
+
+int ort_count_traffic(ort_ctx* ctx, const ort_params* params, const ort_tile* tile, uint64_t* counts) {
+    if (!ctx || !counts) return fail(nullptr, ORT_ERR_INVALID_ARG, "ort_count_traffic: null argument");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    if (!ctx->counters.p) {
+        HIPCHK(ctx, hipMalloc(&ctx->counters.p, 64));
+        ctx->counters.bytes = 64;
+    }
+    HIPCHK(ctx, hipMemsetAsync(ctx->counters.p, 0, 64, ctx->stream));
+    const size_t pix = tile ? (size_t)tile->width * (size_t)tile->rows : 0;
+    DevBuf tmp;
+    if (pix) HIPCHK(ctx, hipMalloc(&tmp.p, 12 * pix));
+    const int rc = render_impl(ctx, params, tile, (float*)tmp.p, 1, nullptr, (unsigned long long*)ctx->counters.p);
+    if (rc == ORT_OK) {
+        unsigned long long h[8] = {0};
+        hipError_t e = hipMemcpy(h, ctx->counters.p, 64, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) { free_buf(tmp); return hip_fail(ctx, e, "ort_count_traffic: copy counters"); }
+        for (int k = 0; k < ORT_COUNT_N; ++k) counts[k] = h[k];
+    }
+    free_buf(tmp);
+    return rc;
+}
+
+// ---- TEST-ONLY host emulation (see ort_internal.h) ----------------------------------
+int ort_debug_emulate_render(const float* cr, const float* ma, const float* fr, int32_t n_spheres,
+                             const float* node_min, const float* node_max, const int32_t* co, const int32_t* oo,
+                             const int32_t* cnt, int32_t n_nodes, const int32_t* idx, int64_t n_indices,
+                             int32_t layout, const ort_params* p, const ort_tile* t, float* out, uint64_t* counts) {
+    try {
+        const std::string bad = check_params(p, t);
+        if (!bad.empty()) return fail(nullptr, ORT_ERR_INVALID_ARG, bad);
+        ort::SceneInput in{cr, ma, fr, n_spheres, node_min, node_max, co, oo, cnt, n_nodes, idx, n_indices};
+        const std::string vbad = ort::validateScene(in);
+        if (!vbad.empty()) return fail(nullptr, ORT_ERR_INVALID_ARG, vbad);
+        ort::KScene S;
+        std::memset(&S, 0, sizeof(S));
+        std::vector<float> fr2((size_t)n_spheres * 2);
+        for (int32_t i = 0; i < n_spheres; ++i) {
+            fr2[2 * (size_t)i] = fr[4 * (size_t)i];
+            fr2[2 * (size_t)i + 1] = fr[4 * (size_t)i + 1];
+        }
+        S.sph_cr = (const float4*)cr;
+        S.sph_ma = (const float4*)ma;
+        S.sph_fr = (const float2*)fr2.data();
+        S.n_spheres = n_spheres;
+        S.n_nodes = n_nodes;
+        ort::CompactLayout cl;
+        std::vector<float> A, B;
+        int mode = 2;
+        if (p->use_octree == 1) {
+            if (n_nodes <= 0) return fail(nullptr, ORT_ERR_NO_SCENE, "no octree");
+            std::string why;
+            if (layout == ORT_LAYOUT_COMPACT) {
+                if (!ort::buildCompactLayout(in, ORT_COMPACT_MAX_DEPTH, cl, why))
+                    return fail(nullptr, ORT_ERR_UNSUPPORTED, why);
+                mode = 0;
+                S.node = (const uint2*)cl.node.data();
+                S.leaf_sph = (const float4*)cl.leaf_sph.data();
+                S.leaf_idx = cl.leaf_idx.data();
+                S.planes = cl.planes.data();
+                S.depth = cl.depth;
+            } else {
+                mode = 1;
+                A.resize(4 * (size_t)n_nodes);
+                B.resize(4 * (size_t)n_nodes);
+                for (int32_t i = 0; i < n_nodes; ++i) {
+                    for (int k = 0; k < 3; ++k) {
+                        A[4 * (size_t)i + k] = node_min[3 * (size_t)i + k];
+                        B[4 * (size_t)i + k] = node_max[3 * (size_t)i + k];
+                    }
+                    std::memcpy(&A[4 * (size_t)i + 3], &co[i], 4);
+                    std::memcpy(&B[4 * (size_t)i + 3], &oo[i], 4);
+                }
+                S.nodeA = (const float4*)A.data();
+                S.nodeB = (const float4*)B.data();
+                S.count = cnt;
+                S.indices = idx;
+            }
+        }
+        const ort::PixelParams pp = pixel_params(p);
+        const TileMap tm = {t->x0, t->width, t->y0, t->rows, t->band_height, t->band_stride};
+        ort::Counters total;
+        for (int k = 0; k < 6; ++k) total.v[k] = 0;
+        std::vector<int> snode(ORT_MAX_STACK);
+        std::vector<float> stmin(ORT_MAX_STACK);
+        ort::LocalFrames lf;
+        for (int row = 0; row < t->rows; ++row) {
+            const int y = tile_row_to_y(tm, row);
+            for (int c = 0; c < t->width; ++c) {
+                float* o = out + 3 * ((size_t)row * t->width + c);
+                if (y >= p->height) { o[0] = o[1] = o[2] = 0.0f; continue; }
+                ort::Counters cc;
+                for (int k = 0; k < 6; ++k) cc.v[k] = 0;
+                ort::V3 v;
+                if (mode == 0) v = ort::shade_pixel<0, true>(pp, S, S.planes, lf, nullptr, nullptr, t->x0 + c, y, cc);
+                else if (mode == 1) v = ort::shade_pixel<1, true>(pp, S, nullptr, lf, snode.data(), stmin.data(), t->x0 + c, y, cc);
+                else v = ort::shade_pixel<2, true>(pp, S, nullptr, lf, nullptr, nullptr, t->x0 + c, y, cc);
+                o[0] = v.x; o[1] = v.y; o[2] = v.z;
+                cc.v[4] = 1;
+                for (int k = 0; k < 6; ++k) total.v[k] += cc.v[k];
+            }
+        }
+        if (counts) for (int k = 0; k < 6; ++k) counts[k] = total.v[k];
+        return ORT_OK;
+    } catch (const std::exception& ex) {
+        return fail(nullptr, ORT_ERR_INTERNAL, ex.what());
+    }
+}
+
+}  // extern "C"

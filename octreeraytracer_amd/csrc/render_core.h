@@ -1,0 +1,661 @@
+// render_core.h -- per-pixel path of the MI355X kernel (__host__ __device__).
+//
+// Restates shaders/octree_fragment_shader.glsl for one pixel:
+//   main()                    glsl:636-664   -> shade_pixel
+//   radiance()                glsl:597-633   -> radiance
+//   Material_bsdf/refract/    glsl:508-589   -> bsdf
+//     schlick
+//   skyColor                  glsl:592-595
+//   Camera_getRay             glsl:205-221   -> camera_ray
+//   random_in_unit_*/cosine   glsl:104-173
+//   Sphere_hit                glsl:224-273   -> sphere_hit_t
+//   traverseOctree            glsl:290-481   -> traverse_compact (fast layout) /
+//                                               traverse_explicit (reference layout)
+//   bruteForceIntersect       glsl:484-498   -> traverse_brute
+//
+// traverse_compact reproduces the reference's stack DFS exactly but stores it as one
+// FRAME per tree level (children offset, parent tmin, and an 8-bit mask of the children
+// still to visit, in traversal-order rank), and re-derives every box from per-axis split
+// planes (see layout.h).  The reference pushes the surviving children of a node in
+// reverse traversal order and always pops the top, so its stack is exactly "for every
+// ancestor level, the not-yet-visited surviving siblings in traversal order": popping
+// the lowest rank bit of the deepest non-empty frame pops the same node with the same
+// tmin.  A hit ends the walk after its leaf (glsl:336), so `closest` is still t_max at
+// every push, and the 200-entry cap (glsl:471) cannot bind for depth <= 28 (<= 7d+1
+// entries); the compact layout is only used for depth <= ORT_COMPACT_MAX_DEPTH.
+#pragma once
+
+#include <stdint.h>
+
+#include "../../include/ort_math.h"
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define ORT_FN __host__ __device__ __forceinline__
+#else
+#define ORT_FN static inline
+#endif
+
+#if defined(__clang__)
+#pragma clang fp contract(off)
+#endif
+
+#define ORT_COMPACT_MAX_DEPTH 10
+#define ORT_MAX_STACK 200
+#define ORT_INTERNAL_FLAG 0x80000000u
+#define ORT_MAXFLOAT 3.402823466e+38f
+
+namespace ort {
+
+struct V3 {
+    float x, y, z;
+};
+ORT_FN int f2i(float f) { int i; __builtin_memcpy(&i, &f, 4); return i; }
+ORT_FN V3 mk(float x, float y, float z) { V3 r; r.x = x; r.y = y; r.z = z; return r; }
+ORT_FN V3 add(V3 a, V3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+ORT_FN V3 sub(V3 a, V3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+ORT_FN V3 mul(V3 a, V3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+ORT_FN V3 scl(float s, V3 a) { return mk(s * a.x, s * a.y, s * a.z); }
+ORT_FN float dot(V3 a, V3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+ORT_FN V3 normalize(V3 v) {
+    const float s = 1.0f / sqrtf(dot(v, v));
+    return mk(v.x * s, v.y * s, v.z * s);
+}
+ORT_FN float length(V3 v) { return sqrtf(dot(v, v)); }
+ORT_FN V3 cross(V3 a, V3 b) { return mk(a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y); }
+// GLSL reflect(I, N) = I - 2.0 * dot(N, I) * N
+ORT_FN V3 reflect(V3 I, V3 N) {
+    const float k = 2.0f * dot(N, I);
+    return mk(I.x - k * N.x, I.y - k * N.y, I.z - k * N.z);
+}
+
+struct KCamera {
+    V3 origin, lowerLeft, horizontal, vertical, u, v, w;
+    float lensRadius;
+};
+
+struct Ray {
+    V3 o, d;
+};
+
+// Device view of an uploaded scene (pointers into one context's buffers).
+struct KScene {
+    const float4* sph_cr;    // center.xyz, radius          (binding 0)
+    const float4* sph_ma;    // float(material), albedo     (binding 1)
+    const float2* sph_fr;    // fuzz, refraction index      (binding 2 .xy)
+    int n_spheres;
+    int n_nodes;
+    // compact layout
+    const uint2* node;       // internal: {childrenOffset, FLAG|childMask}; leaf: {objectsOffset, objectCount}
+    const float4* leaf_sph;  // per objectIndices entry: the sphere's center.xyz, radius
+    const int* leaf_idx;     // per entry: sphere index (= objectIndices)
+    const float* planes;     // 3 x (2^depth + 1) split-plane coordinates (global copy)
+    int depth;               // tree depth D (root = 0)
+    // explicit (reference) layout
+    const float4* nodeA;     // min.xyz, int bits of childrenOffset (binding 3)
+    const float4* nodeB;     // max.xyz, int bits of objectsOffset  (binding 4)
+    const int* count;        // objectCount                         (binding 5)
+    const int* indices;      // objectIndices                       (binding 6)
+};
+
+struct Counters {
+    unsigned long long v[6];
+};
+
+// Sign-vector -> octant traversal order, glsl:341-447, as 8 x 3-bit codes (rank r at bits 3r).
+// Index = (sx+1)*9 + (sy+1)*3 + (sz+1), s in {-1,0,1}.  (0,0,0) cannot occur for a normalised
+// direction; the reference leaves traversalOrder uninitialised there, we use the identity.
+ORT_FN uint32_t pack_order(int a, int b, int c, int d, int e, int f, int g, int h) {
+    return (uint32_t)a | ((uint32_t)b << 3) | ((uint32_t)c << 6) | ((uint32_t)d << 9) | ((uint32_t)e << 12) |
+           ((uint32_t)f << 15) | ((uint32_t)g << 18) | ((uint32_t)h << 21);
+}
+ORT_FN uint32_t order_code(V3 d) {
+    const int sx = (d.x < 0.0f) ? -1 : ((d.x > 0.0f) ? 1 : 0);
+    const int sy = (d.y < 0.0f) ? -1 : ((d.y > 0.0f) ? 1 : 0);
+    const int sz = (d.z < 0.0f) ? -1 : ((d.z > 0.0f) ? 1 : 0);
+    const uint32_t CYAN = pack_order(0, 1, 2, 3, 4, 5, 6, 7);
+    const uint32_t YELLOW = pack_order(2, 0, 3, 1, 6, 4, 7, 5);
+    const uint32_t RED = pack_order(3, 1, 2, 0, 7, 5, 6, 4);
+    const uint32_t DPURPLE = pack_order(1, 0, 3, 2, 5, 4, 7, 6);
+    const uint32_t BLUE = pack_order(4, 5, 6, 7, 0, 1, 2, 3);
+    const uint32_t PURPLE = pack_order(6, 4, 7, 5, 2, 0, 3, 1);
+    const uint32_t GREEN = pack_order(7, 5, 6, 4, 3, 1, 2, 0);
+    const uint32_t BLACK = pack_order(5, 4, 7, 6, 1, 0, 3, 2);
+    // the if/else-if chain of glsl:352-447, in the same order
+    if (sx == 1 && sy == 1 && sz == 1) return CYAN;
+    if ((sx == -1 && sy == 1 && sz == 1) || (sx == -1 && sy == 1 && sz == 0) || (sx == 0 && sy == 1 && sz == 0) ||
+        (sx == 0 && sy == 1 && sz == 1))
+        return YELLOW;
+    if ((sx == -1 && sy == -1 && sz == 1) || (sx == -1 && sy == 0 && sz == 1) || (sx == 0 && sy == 0 && sz == 1) ||
+        (sx == 0 && sy == -1 && sz == 1) || (sx == -1 && sy == -1 && sz == 0) || (sx == 0 && sy == -1 && sz == 0) ||
+        (sx == -1 && sy == 0 && sz == 0))
+        return RED;
+    if ((sx == 1 && sy == -1 && sz == 1) || (sx == 1 && sy == 0 && sz == 1) || (sx == 1 && sy == -1 && sz == 0) ||
+        (sx == 1 && sy == 0 && sz == 0))
+        return DPURPLE;
+    if ((sx == 1 && sy == 1 && sz == -1) || (sx == 1 && sy == 0 && sz == -1) || (sx == 0 && sy == 1 && sz == -1) ||
+        (sx == 1 && sy == 1 && sz == 0))
+        return BLUE;
+    if (sx == -1 && sy == 1 && sz == -1) return PURPLE;
+    if ((sx == -1 && sy == -1 && sz == -1) || (sx == -1 && sy == 0 && sz == -1) || (sx == 0 && sy == -1 && sz == -1) ||
+        (sx == 0 && sy == 0 && sz == -1))
+        return GREEN;
+    if (sx == 1 && sy == -1 && sz == -1) return BLACK;
+    return CYAN;
+}
+
+// rayBoxIntersection (glsl:276-288) on one axis: GLSL min/max semantics, bot/top order kept.
+ORT_FN void slab(float tbot, float ttop, float& tmin, float& tmax) {
+    tmin = ort_minf(tbot, ttop);
+    tmax = ort_maxf(tbot, ttop);
+}
+ORT_FN bool ray_box(const Ray& r, V3 inv, V3 bmin, V3 bmax, float& tmin, float& tmax) {
+    const float bx = inv.x * (bmin.x - r.o.x), by = inv.y * (bmin.y - r.o.y), bz = inv.z * (bmin.z - r.o.z);
+    const float ux = inv.x * (bmax.x - r.o.x), uy = inv.y * (bmax.y - r.o.y), uz = inv.z * (bmax.z - r.o.z);
+    float x0, x1, y0, y1, z0, z1;
+    slab(bx, ux, x0, x1);
+    slab(by, uy, y0, y1);
+    slab(bz, uz, z0, z1);
+    tmin = ort_maxf(ort_maxf(x0, y0), z0);
+    tmax = ort_minf(ort_minf(x1, y1), z1);
+    return tmax >= tmin;
+}
+
+// Sphere_hit (glsl:224-273) returning only the accepted t; a = dot(d,d) precomputed.
+ORT_FN bool sphere_hit_t(const Ray& r, float a, float4 sp, float t_min, float t_max, float& t) {
+    const V3 oc = mk(r.o.x - sp.x, r.o.y - sp.y, r.o.z - sp.z);
+    const float half_b = dot(oc, r.d);
+    const float c = dot(oc, oc) - sp.w * sp.w;
+    const float disc = half_b * half_b - a * c;
+    if (disc > 0.0f) {
+        const float sq = sqrtf(disc);
+        float temp = (-half_b - sq) / a;
+        if (temp < t_max && temp > t_min) { t = temp; return true; }
+        temp = (-half_b + sq) / a;
+        if (temp < t_max && temp > t_min) { t = temp; return true; }
+    }
+    return false;
+}
+
+// Frame storage for traverse_compact: device = LDS columns, host = local arrays.
+struct LdsFrames {
+    int* co;     // co[level * stride + lane]
+    float* tm;
+    int stride;
+    int lane;
+    ORT_FN void set(int L, int c, float t) { co[L * stride + lane] = c; tm[L * stride + lane] = t; }
+    ORT_FN int getCo(int L) const { return co[L * stride + lane]; }
+    ORT_FN float getTm(int L) const { return tm[L * stride + lane]; }
+};
+struct LocalFrames {
+    int co[ORT_COMPACT_MAX_DEPTH + 1];
+    float tm[ORT_COMPACT_MAX_DEPTH + 1];
+    ORT_FN void set(int L, int c, float t) { co[L] = c; tm[L] = t; }
+    ORT_FN int getCo(int L) const { return co[L]; }
+    ORT_FN float getTm(int L) const { return tm[L]; }
+};
+
+// Per-level masks of remaining children (rank space), levels 0..11 in 96 bits.
+struct LevelMasks {
+    uint64_t lo;  // levels 0..7, one byte each
+    uint32_t hi;  // levels 8..11
+    ORT_FN void clear() { lo = 0; hi = 0; }
+    ORT_FN void put(int L, uint32_t m) {
+        if (L < 8) lo |= (uint64_t)m << (8 * L);
+        else hi |= m << (8 * (L - 8));
+    }
+    ORT_FN int top() const {
+        if (hi) return 8 + ((31 - __builtin_clz(hi)) >> 3);
+        if (lo) return (63 - __builtin_clzll(lo)) >> 3;
+        return -1;
+    }
+    // pops the lowest rank of level L; returns the rank
+    ORT_FN int pop(int L) {
+        if (L < 8) {
+            const uint32_t m = (uint32_t)(lo >> (8 * L)) & 0xffu;
+            const int r = __builtin_ctz(m);
+            lo &= ~((uint64_t)1 << (8 * L + r));
+            return r;
+        }
+        const uint32_t m = (hi >> (8 * (L - 8))) & 0xffu;
+        const int r = __builtin_ctz(m);
+        hi &= ~(1u << (8 * (L - 8) + r));
+        return r;
+    }
+};
+
+// Child-box entry t of octant `oct` for a node at depth `dep` with cell (cx,cy,cz):
+// recomputes the reference's rayBoxIntersection for that child (tmin only + hit flag).
+ORT_FN float plane_t(float inv, float p, float o) { return inv * (p - o); }
+
+template <bool COUNT, class Frames>
+ORT_FN bool traverse_compact(const KScene& S, const float* planes, const Ray& r, float t_min, float t_max,
+                             int& hitEntry, float& hitT, Frames& fr, Counters& cnt) {
+    const int D = S.depth;
+    const int P1 = (1 << D) + 1;
+    const float* PX = planes;
+    const float* PY = planes + P1;
+    const float* PZ = planes + 2 * P1;
+    const V3 inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+    const float a = dot(r.d, r.d);
+    {
+        float t0, t1;
+        const V3 bmin = mk(PX[0], PY[0], PZ[0]);
+        const V3 bmax = mk(PX[1 << D], PY[1 << D], PZ[1 << D]);
+        if (!ray_box(r, inv, bmin, bmax, t0, t1)) return false;
+    }
+    const uint32_t ocode = order_code(r.d);
+    int node = 0, depth = 0;
+    uint32_t cx = 0, cy = 0, cz = 0;
+    float ntmin = t_min;
+    const float closest0 = t_max;
+    float closest = t_max;
+    bool hit = false;
+    LevelMasks masks;
+    masks.clear();
+    for (;;) {
+        const uint2 rec = S.node[node];
+        if (COUNT) cnt.v[0] += 1;
+        if (rec.y & ORT_INTERNAL_FLAG) {
+            const int co = (int)rec.x;
+            const uint32_t cmask = rec.y & 0xffu;
+            if (COUNT) {
+                const long long rem = (long long)S.n_nodes - (long long)co;
+                cnt.v[1] += (unsigned long long)(rem >= 8 ? 8 : (rem > 0 ? rem : 0));
+            }
+            const int s = D - depth;  // >= 1 for an internal node
+            const float tx0 = plane_t(inv.x, PX[cx << s], r.o.x);
+            const float tx1 = plane_t(inv.x, PX[(2 * cx + 1) << (s - 1)], r.o.x);
+            const float tx2 = plane_t(inv.x, PX[(cx + 1) << s], r.o.x);
+            const float ty0 = plane_t(inv.y, PY[cy << s], r.o.y);
+            const float ty1 = plane_t(inv.y, PY[(2 * cy + 1) << (s - 1)], r.o.y);
+            const float ty2 = plane_t(inv.y, PY[(cy + 1) << s], r.o.y);
+            const float tz0 = plane_t(inv.z, PZ[cz << s], r.o.z);
+            const float tz1 = plane_t(inv.z, PZ[(2 * cz + 1) << (s - 1)], r.o.z);
+            const float tz2 = plane_t(inv.z, PZ[(cz + 1) << s], r.o.z);
+            float xa0, xa1, xb0, xb1, ya0, ya1, yb0, yb1, za0, za1, zb0, zb1;
+            slab(tx0, tx1, xa0, xa1);  // lower x half: min = mid-split plane order bot/top
+            slab(tx1, tx2, xb0, xb1);
+            slab(ty0, ty1, ya0, ya1);
+            slab(ty1, ty2, yb0, yb1);
+            slab(tz0, tz1, za0, za1);
+            slab(tz1, tz2, zb0, zb1);
+            uint32_t rmask = 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int oct = (int)((ocode >> (3 * k)) & 7u);
+                if ((cmask >> oct) & 1u) {
+                    const bool xh = (oct >> 1) & 1, yh = oct & 1, zh = (oct >> 2) & 1;
+                    const float cmin = ort_maxf(ort_maxf(xh ? xb0 : xa0, yh ? yb0 : ya0), zh ? zb0 : za0);
+                    const float cmax = ort_minf(ort_minf(xh ? xb1 : xa1, yh ? yb1 : ya1), zh ? zb1 : za1);
+                    const bool keep = (cmax >= cmin) && !(cmax < ntmin) && !(cmin > closest0);
+                    if (keep) rmask |= 1u << k;
+                }
+            }
+            if (rmask) {
+                masks.put(depth, rmask);
+                fr.set(depth, co, ntmin);
+            }
+        } else {
+            const int off = (int)rec.x;
+            const int n = (int)rec.y;
+            for (int i = 0; i < n; ++i) {
+                const float4 sp = S.leaf_sph[off + i];
+                if (COUNT) cnt.v[2] += 1;
+                float t;
+                if (sphere_hit_t(r, a, sp, ntmin, closest, t)) {
+                    hit = true;
+                    closest = t;
+                    hitEntry = off + i;
+                    if (COUNT) cnt.v[3] += 1;
+                }
+            }
+            if (hit) break;  // glsl:336: the walk ends after the leaf that produced a hit
+        }
+        const int L = masks.top();
+        if (L < 0) break;
+        const int rk = masks.pop(L);
+        const int oct = (int)((ocode >> (3 * rk)) & 7u);
+        const int sh = depth - L;  // current node is at `depth`; its ancestor at level L
+        cx = ((cx >> sh) << 1) | (uint32_t)((oct >> 1) & 1);
+        cy = ((cy >> sh) << 1) | (uint32_t)(oct & 1);
+        cz = ((cz >> sh) << 1) | (uint32_t)((oct >> 2) & 1);
+        depth = L + 1;
+        node = fr.getCo(L) + oct;
+        // the tmin the reference pushed: max(childTMin, parent node_tmin) (glsl:474)
+        const int s = D - depth;
+        float xl, xu, yl, yu, zl, zu;
+        slab(plane_t(inv.x, PX[cx << s], r.o.x), plane_t(inv.x, PX[(cx + 1) << s], r.o.x), xl, xu);
+        slab(plane_t(inv.y, PY[cy << s], r.o.y), plane_t(inv.y, PY[(cy + 1) << s], r.o.y), yl, yu);
+        slab(plane_t(inv.z, PZ[cz << s], r.o.z), plane_t(inv.z, PZ[(cz + 1) << s], r.o.z), zl, zu);
+        const float cmin = ort_maxf(ort_maxf(xl, yl), zl);
+        ntmin = ort_maxf(cmin, fr.getTm(L));
+    }
+    hitT = closest;
+    return hit;
+}
+
+// Literal restatement of traverseOctree (glsl:290-481) over the reference record layout
+// (boxes read from memory, 200-entry stack).  Used for trees the compact layout cannot
+// represent.  `stack_node`/`stack_tmin` point at ORT_MAX_STACK entries owned by the lane.
+template <bool COUNT>
+ORT_FN bool traverse_explicit(const KScene& S, const Ray& r, float t_min, float t_max, int& hitEntry, float& hitT,
+                              int* stack_node, float* stack_tmin, Counters& cnt) {
+    const V3 inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+    const float a = dot(r.d, r.d);
+    int sp = 0;
+    stack_node[0] = 0;
+    stack_tmin[0] = t_min;
+    bool hit = false;
+    float closest = t_max;
+    {
+        const float4 A = S.nodeA[0], B = S.nodeB[0];
+        float t0, t1;
+        if (!ray_box(r, inv, mk(A.x, A.y, A.z), mk(B.x, B.y, B.z), t0, t1)) return false;
+    }
+    const uint32_t ocode = order_code(r.d);
+    // bounded so that a malformed (cyclic) upload cannot hang the GPU
+    for (long long guard = 0; sp >= 0 && guard < (1ll << 26); ++guard) {
+        const int nodeIdx = stack_node[sp];
+        const float ntmin = stack_tmin[sp];
+        --sp;
+        if (COUNT) cnt.v[0] += 1;
+        const float4 A = S.nodeA[nodeIdx], B = S.nodeB[nodeIdx];
+        const int co = f2i(A.w);
+        const int oo = f2i(B.w);
+        const int objectCount = S.count[nodeIdx];
+        if (co == -1) {
+            for (int i = 0; i < objectCount; ++i) {
+                const int e = oo + i;
+                const float4 spr = S.sph_cr[S.indices[e]];
+                if (COUNT) cnt.v[2] += 1;
+                float t;
+                if (sphere_hit_t(r, a, spr, ntmin, closest, t)) {
+                    hit = true;
+                    closest = t;
+                    hitEntry = e;
+                    sp = -1;
+                    if (COUNT) cnt.v[3] += 1;
+                }
+            }
+        } else {
+            for (int i = 7; i >= 0; --i) {
+                const int oct = (int)((ocode >> (3 * i)) & 7u);
+                const int childIdx = co + oct;
+                if (childIdx >= S.n_nodes) continue;
+                if (COUNT) cnt.v[1] += 1;
+                const float4 CA = S.nodeA[childIdx], CB = S.nodeB[childIdx];
+                float cmin, cmax;
+                const bool boxhit = ray_box(r, inv, mk(CA.x, CA.y, CA.z), mk(CB.x, CB.y, CB.z), cmin, cmax);
+                if (!boxhit || cmax < ntmin || cmin > closest ||
+                    (f2i(CA.w) == -1 && f2i(CB.w) == -1))
+                    continue;
+                if (sp < ORT_MAX_STACK - 1) {
+                    ++sp;
+                    stack_node[sp] = childIdx;
+                    stack_tmin[sp] = ort_maxf(cmin, ntmin);
+                }
+            }
+        }
+    }
+    hitT = closest;
+    return hit;
+}
+
+// bruteForceIntersect (glsl:484-498): exact closest hit over all spheres.
+template <bool COUNT>
+ORT_FN bool traverse_brute(const KScene& S, const Ray& r, float t_min, float t_max, int& hitSphere, float& hitT,
+                           Counters& cnt) {
+    const float a = dot(r.d, r.d);
+    bool hit = false;
+    float closest = t_max;
+    for (int i = 0; i < S.n_spheres; ++i) {
+        float t;
+        if (COUNT) cnt.v[2] += 1;
+        if (sphere_hit_t(r, a, S.sph_cr[i], t_min, closest, t)) {
+            hit = true;
+            closest = t;
+            hitSphere = i;
+            if (COUNT) cnt.v[3] += 1;
+        }
+    }
+    hitT = closest;
+    return hit;
+}
+
+struct HitRec {
+    float t;
+    V3 point, normal;
+    int mat;
+    V3 albedo;
+    float fuzz, ri;
+};
+
+// --- random directions (glsl:104-173) ---
+ORT_FN V3 random_in_unit_disk(ort_rng& st) {
+    const float PI_F = (float)3.14159265359;
+    const float spx = 2.0f * ort_rand2D(&st) - 1.0f;
+    const float spy = 2.0f * ort_rand2D(&st) - 1.0f;
+    float r, phi;
+    if (spx > -spy) {
+        if (spx > spy) {
+            r = spx;
+            phi = spy / spx;
+        } else {
+            r = spy;
+            phi = 2.0f - spx / spy;
+        }
+    } else {
+        if (spx < spy) {
+            r = -spx;
+            phi = 4.0f + spy / spx;
+        } else {
+            r = -spy;
+            if (spy != 0.0f) phi = 6.0f - spx / spy;
+            else phi = 0.0f;
+        }
+    }
+    phi *= PI_F / 4.0f;
+    return mk(r * ort_cosf(phi), r * ort_sinf(phi), 0.0f);
+}
+ORT_FN V3 random_in_unit_sphere(ort_rng& st) {
+    const float PI_F = (float)3.14159265359;
+    const float z = 2.0f * ort_rand2D(&st) - 1.0f;
+    const float phi = 2.0f * PI_F * ort_rand2D(&st);
+    const float r = ort_powf(ort_rand2D(&st), 1.0f / 3.0f);
+    const float s = sqrtf(1.0f - z * z);
+    return mk(r * s * ort_cosf(phi), r * s * ort_sinf(phi), r * z);
+}
+ORT_FN V3 random_cosine_direction(ort_rng& st) {
+    const float PI_F = (float)3.14159265359;
+    const float r1 = ort_rand2D(&st);
+    const float r2 = ort_rand2D(&st);
+    const float phi = 2.0f * PI_F * r1;
+    const float sr2 = sqrtf(r2);
+    return mk(ort_cosf(phi) * sr2, ort_sinf(phi) * sr2, sqrtf(1.0f - r2));
+}
+
+ORT_FN bool refract_vec(V3 v, V3 n, float ni_over_nt, V3& refracted) {
+    const V3 uv = normalize(v);
+    const float dt = dot(uv, n);
+    const float disc = 1.0f - ni_over_nt * ni_over_nt * (1.0f - dt * dt);
+    if (disc > 0.0f) {
+        const float sq = sqrtf(disc);
+        refracted = mk(ni_over_nt * (uv.x - n.x * dt) - n.x * sq, ni_over_nt * (uv.y - n.y * dt) - n.y * sq,
+                       ni_over_nt * (uv.z - n.z * dt) - n.z * sq);
+        return true;
+    }
+    return false;
+}
+ORT_FN float schlick(float cosine, float ri) {
+    float r0 = (1.0f - ri) / (1.0f + ri);
+    r0 = r0 * r0;
+    return r0 + (1.0f - r0) * ort_powf(1.0f - cosine, 5.0f);
+}
+
+// Material_bsdf (glsl:525-589)
+ORT_FN bool bsdf(const HitRec& h, const Ray& wo, Ray& wi, V3& att, ort_rng& st) {
+    wi.o = h.point;
+    switch (h.mat) {
+        case 0: {
+            const V3 ld = random_cosine_direction(st);
+            const V3 w = h.normal;
+            const V3 a = (fabsf(w.x) > 0.1f) ? mk(0.0f, 1.0f, 0.0f) : mk(1.0f, 0.0f, 0.0f);
+            const V3 u = normalize(cross(a, w));
+            const V3 v = cross(w, u);
+            wi.d = normalize(mk((ld.x * u.x + ld.y * v.x) + ld.z * w.x, (ld.x * u.y + ld.y * v.y) + ld.z * w.y,
+                                (ld.x * u.z + ld.y * v.z) + ld.z * w.z));
+            att = h.albedo;
+            return true;
+        }
+        case 1: {
+            const float fuzz = h.fuzz;
+            const V3 refl = reflect(normalize(wo.d), h.normal);
+            const V3 rs = random_in_unit_sphere(st);
+            wi.d = mk(refl.x + fuzz * rs.x, refl.y + fuzz * rs.y, refl.z + fuzz * rs.z);
+            att = h.albedo;
+            return dot(wi.d, h.normal) > 0.0f;
+        }
+        case 2: {
+            V3 outward;
+            float ni_over_nt, cosine;
+            const float ri = h.ri;
+            att = mk(1.0f, 1.0f, 1.0f);
+            if (dot(wo.d, h.normal) > 0.0f) {
+                outward = mk(-h.normal.x, -h.normal.y, -h.normal.z);
+                ni_over_nt = ri;
+                cosine = dot(wo.d, h.normal) / length(wo.d);
+                cosine = sqrtf(1.0f - ri * ri * (1.0f - cosine * cosine));
+            } else {
+                outward = h.normal;
+                ni_over_nt = 1.0f / ri;
+                cosine = -dot(wo.d, h.normal) / length(wo.d);
+            }
+            V3 refracted = mk(0.0f, 0.0f, 0.0f);
+            const bool can = refract_vec(wo.d, outward, ni_over_nt, refracted);
+            const float prob = can ? schlick(cosine, ri) : 1.0f;
+            if (ort_rand2D(&st) < prob) wi.d = reflect(wo.d, h.normal);
+            else wi.d = refracted;
+            return true;
+        }
+        default:
+            return false;
+    }
+}
+
+ORT_FN V3 sky_color(const Ray& r) {
+    const float t = 0.5f * (r.d.y + 1.0f);
+    return mk((1.0f - t) * 1.0f + t * 0.5f, (1.0f - t) * 1.0f + t * 0.7f, (1.0f - t) * 1.0f + t * 1.0f);
+}
+
+// Camera_getRay (glsl:205-221)
+ORT_FN Ray camera_ray(const KCamera& c, float s, float t, float W, float H, ort_rng& st) {
+    const float pixelRadius = 0.5f / ort_maxf(W, H);
+    const float jx = pixelRadius * (ort_rand2D(&st) - 0.5f);
+    const float jy = pixelRadius * (ort_rand2D(&st) - 0.5f);
+    const V3 rdd = random_in_unit_disk(st);
+    const V3 rd = mk(c.lensRadius * rdd.x, c.lensRadius * rdd.y, c.lensRadius * rdd.z);
+    const V3 off = mk(c.u.x * rd.x + c.v.x * rd.y, c.u.y * rd.x + c.v.y * rd.y, c.u.z * rd.x + c.v.z * rd.y);
+    Ray r;
+    r.o = add(c.origin, off);
+    const float a = s + jx, b = t + jy;
+    r.d = normalize(mk((((c.lowerLeft.x + a * c.horizontal.x) + b * c.vertical.x) - c.origin.x) - off.x,
+                       (((c.lowerLeft.y + a * c.horizontal.y) + b * c.vertical.y) - c.origin.y) - off.y,
+                       (((c.lowerLeft.z + a * c.horizontal.z) + b * c.vertical.z) - c.origin.z) - off.z));
+    return r;
+}
+
+// Intersection dispatch for one ray; fills the hit record like intersectScene (glsl:500-506).
+// MODE: 0 compact octree, 1 explicit octree, 2 brute force.
+template <int MODE, bool COUNT, class Frames>
+ORT_FN bool intersect(const KScene& S, const float* planes, const Ray& r, HitRec& h, Frames& fr, int* snode,
+                      float* stmin, Counters& cnt) {
+    int entry = -1;
+    float t = 0.0f;
+    bool hit;
+    if (COUNT) cnt.v[5] += 1;
+    if (MODE == 0) hit = traverse_compact<COUNT>(S, planes, r, 0.001f, ORT_MAXFLOAT, entry, t, fr, cnt);
+    else if (MODE == 1) hit = traverse_explicit<COUNT>(S, r, 0.001f, ORT_MAXFLOAT, entry, t, snode, stmin, cnt);
+    else hit = traverse_brute<COUNT>(S, r, 0.001f, ORT_MAXFLOAT, entry, t, cnt);
+    if (!hit) return false;
+    int sidx;
+    float4 sp;
+    if (MODE == 0) {
+        sidx = S.leaf_idx[entry];
+        sp = S.leaf_sph[entry];
+    } else if (MODE == 1) {
+        sidx = S.indices[entry];
+        sp = S.sph_cr[sidx];
+    } else {
+        sidx = entry;
+        sp = S.sph_cr[sidx];
+    }
+    h.t = t;
+    h.point = mk(r.o.x + t * r.d.x, r.o.y + t * r.d.y, r.o.z + t * r.d.z);
+    h.normal = mk((h.point.x - sp.x) / sp.w, (h.point.y - sp.y) / sp.w, (h.point.z - sp.z) / sp.w);
+    const float4 ma = S.sph_ma[sidx];
+    const float2 fr2 = S.sph_fr[sidx];
+    h.mat = (int)ma.x;
+    h.albedo = mk(ma.y, ma.z, ma.w);
+    h.fuzz = fr2.x;
+    h.ri = fr2.y;
+    return true;
+}
+
+struct PixelParams {
+    KCamera cam;
+    int W, H, ns, maxDepth;
+};
+
+// main() of the fragment shader (glsl:636-664) for pixel (px, py), py = 0 the bottom row.
+template <int MODE, bool COUNT, class Frames>
+ORT_FN V3 shade_pixel(const PixelParams& P, const KScene& S, const float* planes, Frames& fr, int* snode, float* stmin,
+                      int px, int py, Counters& cnt) {
+    const float W = (float)P.W, H = (float)P.H;
+    const float fx = (float)px + 0.5f, fy = (float)py + 0.5f;
+    ort_rng st;
+    st.x = fx / W;
+    st.y = fy / H;
+    V3 col = mk(0.0f, 0.0f, 0.0f);
+    for (int s = 0; s < P.ns; ++s) {
+        const int sqrt_ns = (int)sqrtf((float)P.ns);
+        const int i = s % sqrt_ns;
+        const int j = s / sqrt_ns;
+        const float u = (fx + ((float)i + ort_rand2D(&st)) / (float)sqrt_ns) / W;
+        const float v = (fy + ((float)j + ort_rand2D(&st)) / (float)sqrt_ns) / H;
+        Ray ray = camera_ray(P.cam, u, v, W, H, st);
+        // radiance (glsl:597-633)
+        V3 c = mk(1.0f, 1.0f, 1.0f);
+        float importance = 1.0f;
+        ray.d = normalize(ray.d);
+        for (int b = 0; b < P.maxDepth; ++b) {
+            if (importance < 0.01f) break;
+            HitRec h;
+            if (intersect<MODE, COUNT>(S, planes, ray, h, fr, snode, stmin, cnt)) {
+                Ray wi;
+                wi.d = ray.d;
+                V3 att = mk(0.0f, 0.0f, 0.0f);
+                const bool scattered = bsdf(h, ray, wi, att, st);
+                ray.o = wi.o;
+                ray.d = wi.d;
+                if (scattered) {
+                    c = mul(c, att);
+                } else {
+                    c = mul(c, mk(0.0f, 0.0f, 0.0f));
+                    break;
+                }
+                importance *= ort_maxf(att.x, ort_maxf(att.y, att.z));
+            } else {
+                c = mul(c, sky_color(ray));
+                break;
+            }
+        }
+        col = add(col, c);
+    }
+    const float fns = (float)P.ns;
+    col = mk(col.x / fns, col.y / fns, col.z / fns);
+    const float g = 1.0f / 2.2f;
+    return mk(ort_powf(col.x, g), ort_powf(col.y, g), ort_powf(col.z, g));
+}
+
+}  // namespace ort

@@ -1,0 +1,4 @@
+// render_core_flags.h -- constants shared by the host layout compiler and the kernel.
+#pragma once
+#define ORT_INTERNAL_FLAG_HOST 0x80000000u
+#define ORT_COMPACT_MAX_DEPTH_HOST 10

@@ -1,0 +1,205 @@
+"""Device renderer: the GL path of the reference replaced by the gfx950 kernel (libort.so).
+
+``Renderer`` owns one ort_ctx (one GPU).  ``upload`` = setupBuffers (src/raytracer.cpp:74-152),
+``render`` = the per-frame uniforms + glDrawArrays (src/raytracer.cpp:491-499) followed by a
+read of the frame (the reference never reads pixels back; this returns them).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib as L
+from .scene import (DEFAULT_CAMERA_POSITION, DEFAULT_PITCH, DEFAULT_YAW, DEFAULT_ZOOM, FlatOctree, SphereSet,
+                    camera_view)
+
+
+@dataclass
+class FrameParams:
+    """The shader uniforms (glsl:13-18, 48-53)."""
+
+    width: int
+    height: int
+    num_samples: int = 1
+    max_depth: int = 1
+    use_octree: int = 1
+    view: np.ndarray = field(default_factory=lambda: camera_view())
+    camera_position: tuple = DEFAULT_CAMERA_POSITION
+    camera_zoom: float = DEFAULT_ZOOM
+
+    def to_c(self) -> L.OrtParams:
+        p = L.OrtParams()
+        p.width, p.height = int(self.width), int(self.height)
+        p.num_samples, p.max_depth, p.use_octree = int(self.num_samples), int(self.max_depth), int(self.use_octree)
+        v = np.asarray(self.view, np.float32).reshape(16)
+        for i in range(16):
+            p.view[i] = float(v[i])
+        for i in range(3):
+            p.camera_position[i] = float(self.camera_position[i])
+        p.camera_zoom = float(self.camera_zoom)
+        return p
+
+    @staticmethod
+    def default_camera(width, height, num_samples=1, max_depth=1, use_octree=1, position=DEFAULT_CAMERA_POSITION,
+                       yaw=DEFAULT_YAW, pitch=DEFAULT_PITCH, zoom=DEFAULT_ZOOM) -> "FrameParams":
+        return FrameParams(width, height, num_samples, max_depth, use_octree, camera_view(position, yaw, pitch),
+                           tuple(position), zoom)
+
+
+@dataclass
+class Tile:
+    """Rows/columns to render; see ort_tile in include/ort.h.  Output row j is pixel row
+    y0 + (j // band_height) * band_stride + j % band_height (GL rows: y = 0 at the bottom)."""
+
+    x0: int
+    width: int
+    y0: int
+    rows: int
+    band_height: int = 0
+    band_stride: int = 0
+
+    @staticmethod
+    def full(p: FrameParams) -> "Tile":
+        return Tile(0, p.width, 0, p.height)
+
+    def to_c(self) -> L.OrtTile:
+        t = L.OrtTile()
+        t.x0, t.width, t.y0, t.rows = int(self.x0), int(self.width), int(self.y0), int(self.rows)
+        t.band_height, t.band_stride = int(self.band_height), int(self.band_stride)
+        return t
+
+    def pixel_rows(self, height: int) -> np.ndarray:
+        j = np.arange(self.rows)
+        y = self.y0 + (j // self.band_height) * self.band_stride + j % self.band_height if self.band_height > 0 \
+            else self.y0 + j
+        return y
+
+
+class Renderer:
+    def __init__(self, device: int = 0):
+        self._lib = L.lib()
+        self._ctx = C.c_void_p()
+        L.check(self._lib.ort_create(device, C.byref(self._ctx)))
+        self.device = device
+
+    # -- lifecycle -------------------------------------------------------------------
+    def close(self):
+        if self._ctx:
+            self._lib.ort_destroy(self._ctx)
+            self._ctx = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        L.check(rc, self._ctx)
+
+    # -- scene -----------------------------------------------------------------------
+    def set_layout(self, layout: int):
+        """Force ORT_LAYOUT_COMPACT / ORT_LAYOUT_EXPLICIT (-1 = auto) for the next upload."""
+        self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_FORCE_LAYOUT, int(layout)))
+
+    def upload(self, spheres: SphereSet, tree: FlatOctree | None):
+        cr = np.ascontiguousarray(spheres.center_radius, np.float32)
+        ma = np.ascontiguousarray(spheres.mat_albedo, np.float32)
+        fr = np.ascontiguousarray(spheres.fuzz_ri, np.float32)
+        if tree is None:
+            self._check(self._lib.ort_upload_scene(self._ctx, L.fptr(cr), L.fptr(ma), L.fptr(fr), spheres.n,
+                                                   None, None, None, None, None, 0, None, 0))
+            return
+        nmin = np.ascontiguousarray(tree.node_min, np.float32)
+        nmax = np.ascontiguousarray(tree.node_max, np.float32)
+        co = np.ascontiguousarray(tree.children_offset, np.int32)
+        oo = np.ascontiguousarray(tree.objects_offset, np.int32)
+        cnt = np.ascontiguousarray(tree.object_count, np.int32)
+        idx = np.ascontiguousarray(tree.object_indices, np.int32)
+        self._check(self._lib.ort_upload_scene(self._ctx, L.fptr(cr), L.fptr(ma), L.fptr(fr), spheres.n,
+                                               L.fptr(nmin), L.fptr(nmax), L.iptr(co), L.iptr(oo), L.iptr(cnt),
+                                               tree.n_nodes, L.iptr(idx), tree.n_indices))
+
+    def info(self) -> dict:
+        i = L.OrtSceneInfo()
+        self._check(self._lib.ort_scene_get_info(self._ctx, C.byref(i)))
+        return {"n_spheres": i.n_spheres, "n_nodes": i.n_nodes, "n_indices": i.n_indices,
+                "layout": "compact" if i.layout == L.ORT_LAYOUT_COMPACT else "explicit",
+                "tree_depth": i.tree_depth, "device_bytes": i.device_bytes}
+
+    # -- frames ----------------------------------------------------------------------
+    def render(self, params: FrameParams, tile: Tile | None = None, out=None, stream=None):
+        """Render a tile.  out: None (returns a new (rows, width, 3) float32 numpy array),
+        a numpy array, or a device pointer (int) / torch CUDA tensor on this device.
+        stream: None (synchronous) or a hipStream_t handle (int), e.g.
+        torch.cuda.current_stream().cuda_stream."""
+        tile = tile or Tile.full(params)
+        p, t = params.to_c(), tile.to_c()
+        s = C.c_void_p(int(stream)) if stream else None
+        if out is None:
+            out = np.empty((tile.rows, tile.width, 3), np.float32)
+        if isinstance(out, np.ndarray):
+            assert out.dtype == np.float32 and out.flags.c_contiguous and out.size >= tile.rows * tile.width * 3
+            self._check(self._lib.ort_render(self._ctx, C.byref(p), C.byref(t), out.ctypes.data_as(C.c_void_p), 0, s))
+            return out
+        ptr = out.data_ptr() if hasattr(out, "data_ptr") else int(out)
+        if hasattr(out, "numel"):
+            assert out.numel() >= tile.rows * tile.width * 3 and out.is_contiguous()
+        self._check(self._lib.ort_render(self._ctx, C.byref(p), C.byref(t), C.c_void_p(ptr), 1, s))
+        return out
+
+    def last_kernel_ms(self) -> float:
+        ms = C.c_float()
+        self._check(self._lib.ort_last_kernel_ms(self._ctx, C.byref(ms)))
+        return ms.value
+
+    def count_traffic(self, params: FrameParams, tile: Tile | None = None) -> dict:
+        tile = tile or Tile.full(params)
+        p, t = params.to_c(), tile.to_c()
+        counts = (C.c_uint64 * L.ORT_COUNT_N)()
+        self._check(self._lib.ort_count_traffic(self._ctx, C.byref(p), C.byref(t), counts))
+        return dict(zip(L.COUNT_NAMES, [int(v) for v in counts]))
+
+
+# Reference-layout record bytes touched, SURVEY.md 8(d): the algorithmic traffic model.
+BYTES_PER = {"nodes_popped": 36, "child_records": 32, "leaf_objects": 20, "accepted_hits": 32, "pixels": 12}
+
+
+def algorithmic_bytes(counts: dict) -> int:
+    return sum(BYTES_PER[k] * int(counts[k]) for k in BYTES_PER)
+
+
+def emulate_render_host(spheres: SphereSet, tree: FlatOctree | None, params: FrameParams, tile: Tile | None = None,
+                        layout: int = L.ORT_LAYOUT_COMPACT):
+    """TEST-ONLY: run the kernel's per-pixel code (render_core.h) on the host CPU.
+    Used by the CPU test suite to validate the kernel's traversal logic against the
+    independent oracle without a GPU.  ``Renderer.render`` never calls this."""
+    lib = L.lib()
+    tile = tile or Tile.full(params)
+    out = np.empty((tile.rows, tile.width, 3), np.float32)
+    counts = (C.c_uint64 * L.ORT_COUNT_N)()
+    p, t = params.to_c(), tile.to_c()
+    cr = np.ascontiguousarray(spheres.center_radius, np.float32)
+    ma = np.ascontiguousarray(spheres.mat_albedo, np.float32)
+    fr = np.ascontiguousarray(spheres.fuzz_ri, np.float32)
+    if tree is None:
+        keep = ()
+        args = (None, None, None, None, None, 0, None, 0)
+    else:
+        keep = tuple(np.ascontiguousarray(a, t) for a, t in (
+            (tree.node_min, np.float32), (tree.node_max, np.float32), (tree.children_offset, np.int32),
+            (tree.objects_offset, np.int32), (tree.object_count, np.int32), (tree.object_indices, np.int32)))
+        args = (L.fptr(keep[0]), L.fptr(keep[1]), L.iptr(keep[2]), L.iptr(keep[3]), L.iptr(keep[4]),
+                tree.n_nodes, L.iptr(keep[5]), tree.n_indices)
+    L.check(lib.ort_debug_emulate_render(L.fptr(cr), L.fptr(ma), L.fptr(fr), spheres.n, *args, layout,
+                                         C.byref(p), C.byref(t), L.fptr(out), counts))
+    del keep
+    return out, dict(zip(L.COUNT_NAMES, [int(v) for v in counts]))
