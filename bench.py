@@ -38,7 +38,6 @@ CONFIGS = {
     "c5": (7680, 4320, 1_000_000, 10, 1, 1, 4),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-BAND = 16
 
 
 def parse():
@@ -86,28 +85,15 @@ def main():
     p = ort.FrameParams.default_camera(W, H, num_samples=NS, max_depth=MAXD)
 
     # partition: 16-row bands dealt round-robin; every rank renders the same number of rows
-    nbands = -(-H // BAND)
-    per = -(-nbands // world)
-    if world == 1:
-        tile = ort.Tile(0, W, 0, H)
-    else:
-        tile = ort.Tile(0, W, rank * BAND, per * BAND, BAND, BAND * world)
+    from octreeraytracer_amd.distributed import FrameGather, rank_tile
+    tile = rank_tile(W, H, rank, world)
     out = torch.empty((tile.rows, W, 3), dtype=torch.float32, device="cuda")
-    gathered = None
-    frame = None
-    if world > 1 and rank == 0:
-        gathered = torch.empty((world, tile.rows, W, 3), dtype=torch.float32, device="cuda")
-        frame = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+    gather = FrameGather(dist, W, H, world, rank, "cuda")
     stream = torch.cuda.current_stream()
 
     def step():
         r.render(p, tile, out=out, stream=stream.cuda_stream)
-        if world > 1:
-            dist.gather(out, list(gathered.unbind(0)) if rank == 0 else None, dst=0)
-            if rank == 0:
-                # [rank][band][16 rows] -> global band b*world + rank
-                g = gathered.view(world, per, BAND, W, 3).permute(1, 0, 2, 3, 4).reshape(per * world * BAND, W, 3)
-                frame.copy_(g[:H])
+        return gather(out)
 
     for _ in range(args.warmup):
         step()
@@ -121,11 +107,7 @@ def main():
         evs[k][0].record(stream)
         r.render(p, tile, out=out, stream=stream.cuda_stream)
         evs[k][1].record(stream)
-        if world > 1:
-            dist.gather(out, list(gathered.unbind(0)) if rank == 0 else None, dst=0)
-            if rank == 0:
-                g = gathered.view(world, per, BAND, W, 3).permute(1, 0, 2, 3, 4).reshape(per * world * BAND, W, 3)
-                frame.copy_(g[:H])
+        frame = gather(out)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -197,7 +179,7 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(spheres, tree, p, args.cpu_seconds)
         if args.save:
-            img = (frame if world > 1 else out).cpu().numpy()
+            img = frame.cpu().numpy()
             from octreeraytracer_amd import image
             (image.write_png if args.save.endswith(".png") else image.write_pfm)(args.save, img)
     r.close()

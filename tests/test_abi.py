@@ -1,0 +1,57 @@
+"""The C-ABI library loads and exports every symbol include/ort.h declares (no GPU needed)."""
+import ctypes
+import re
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def declared_symbols():
+    text = (ROOT / "include" / "ort.h").read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(ort_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_lists_expected_entry_points():
+    names = declared_symbols()
+    for must in ("ort_create", "ort_destroy", "ort_upload_scene", "ort_render", "ort_last_error"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol(ort):
+    lib = ort.lib()
+    missing = [n for n in declared_symbols() if not hasattr(lib, n)]
+    assert not missing, missing
+    from octreeraytracer_amd import _lib
+    assert sorted(_lib.EXPORTED_SYMBOLS) == declared_symbols()
+
+
+def test_version_and_thread_error(ort):
+    lib = ort.lib()
+    assert b"gfx950" in lib.ort_version()
+    assert lib.ort_last_error(None) is not None
+
+
+def test_octree_build_errors_cross_the_abi_as_codes(ort):
+    import numpy as np
+    s = ort.SphereSet.empty(0)
+    with pytest.raises(ort.OrtError) as e:
+        ort.build_octree(s, 3, 0)
+    assert e.value.code == 1 and "Sphere list is empty" in str(e.value)  # src/octree.cpp:50-52
+
+
+def test_render_without_gpu_context_fails_loudly(ort):
+    """ort_create must fail with an error code (not fall back to a CPU path) when no device exists."""
+    torch = pytest.importorskip("torch")
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    with pytest.raises(ort.OrtError):
+        ort.Renderer(0)
+
+
+def test_struct_layouts_match_header(ort):
+    from octreeraytracer_amd import _lib
+    assert ctypes.sizeof(_lib.OrtParams) == 4 * (5 + 16 + 3 + 1)
+    assert ctypes.sizeof(_lib.OrtTile) == 24

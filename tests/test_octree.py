@@ -1,0 +1,128 @@
+"""This repo's octree builder (octreeraytracer_amd/csrc/octree.cpp) against the REFERENCE's
+src/octree.cpp: committed fixtures produced by the reference builder (tools/make_golden.py),
+plus a live comparison when oracle/_ref/ref_octree was built in this container."""
+import hashlib
+import json
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+G = Path(__file__).resolve().parent / "golden"
+MANIFEST = json.loads((G / "manifest.json").read_text())
+
+
+def sha(*arrays):
+    h = hashlib.sha256()
+    for a in arrays:
+        h.update(np.ascontiguousarray(a).tobytes())
+    return h.hexdigest()
+
+
+def scene(ort, name):
+    if name == "debug":
+        return ort.debug_spheres()
+    if name == "prebuilt":
+        return ort.prebuilt_spheres()
+    return ort.random_spheres(int(name.replace("rand", "").replace("k", "000")), 42)
+
+
+def parse_key(key):
+    name, d, m = key.split("_")
+    return name, int(d[1:]), int(m[1:])
+
+
+@pytest.mark.parametrize("key", sorted(k for k, v in MANIFEST["trees"].items() if "file" in v))
+def test_builder_matches_reference_fixture(ort, key):
+    name, d, m = parse_key(key)
+    fx = np.load(G / MANIFEST["trees"][key]["file"])
+    t = ort.build_octree(scene(ort, name), d, m)
+    assert np.array_equal(t.gpu_records(), fx["records"]), key
+    assert np.array_equal(t.object_indices, fx["indices"]), key
+
+
+@pytest.mark.parametrize("key", ["rand10k_d6_m0", "rand10k_d6_m1"])
+def test_builder_matches_reference_hash(ort, key):
+    name, d, m = parse_key(key)
+    t = ort.build_octree(scene(ort, name), d, m)
+    e = MANIFEST["trees"][key]
+    assert (t.n_nodes, t.n_indices) == (e["nodes"], e["indices"])
+    assert sha(t.gpu_records(), t.object_indices) == e["sha256"]
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("key", ["rand100k_d8_m0", "rand100k_d8_m1"])
+def test_builder_matches_reference_hash_c3(ort, key):
+    name, d, m = parse_key(key)
+    t = ort.build_octree(scene(ort, name), d, m)
+    e = MANIFEST["trees"][key]
+    assert (t.n_nodes, t.n_indices) == (e["nodes"], e["indices"])  # 10,953,681 / 5,472,144
+    assert sha(t.gpu_records(), t.object_indices) == e["sha256"]
+
+
+def test_sphere_generator_is_pinned(ort):
+    for name, e in MANIFEST["spheres"].items():
+        s = scene(ort, name)
+        assert s.n == e["n"]
+        assert sha(s.center_radius, s.mat_albedo, s.fuzz_ri) == e["sha256"], name
+    fx = np.load(G / "spheres_rand100_seed42.npz")
+    s = ort.random_spheres(100, 42)
+    assert np.array_equal(s.center_radius, fx["center_radius"]) and np.array_equal(s.mat_albedo, fx["mat_albedo"])
+
+
+def test_random_sphere_layout_rules(ort):
+    """generateRandomSpheres (src/raytracer.cpp:254-337): radius 0.2, 20/20/60 material split."""
+    s = ort.random_spheres(1000, 7)
+    assert np.all(s.center_radius[:, 3] == np.float32(0.2))
+    mats = s.mat_albedo[:, 0].astype(int)
+    assert (mats == 1).sum() == 200 and (mats == 2).sum() == 200 and (mats == 0).sum() == 600
+    assert np.all(s.fuzz_ri[mats == 1, 0] <= 0.5) and np.all(s.fuzz_ri[mats != 1, 0] == 0)
+    ri = s.fuzz_ri[mats == 2, 1]
+    assert np.all((ri >= 1.3) & (ri <= 1.7)) and np.all(s.fuzz_ri[mats != 2, 1] == 1)
+    assert np.all((s.mat_albedo[:, 1:] >= 0) & (s.mat_albedo[:, 1:] < 1))
+
+
+def test_debug_scene_known_answers(ort):
+    """Comments of the reference: src/octree.cpp:75-77, src/raytracer.cpp:343-345."""
+    t = ort.build_octree(ort.debug_spheres(), 3, 2)
+    assert t.n_nodes == 9 and t.n_indices == 3
+    assert np.array_equal(t.node_min[0], [-13, -13, -13]) and np.array_equal(t.node_max[0], [13, 13, 13])
+    assert t.children_offset[0] == 1 and np.all(t.children_offset[1:] == -1)
+    holders = {i: t.object_indices[t.objects_offset[i]] for i in range(9) if t.object_count[i] > 0}
+    assert holders == {1: 0, 2: 2, 8: 1}  # leaves 1, 2, 8 hold spheres 0, 2, 1
+
+
+def test_octant_numbering_and_child_boxes(ort):
+    """octant = (z<<2)|(x<<1)|y (src/octree.h:10-20); children copy min/mid/max verbatim."""
+    t = ort.build_octree(ort.random_spheres(300, 3), 2, 0)
+    mn, mx = t.node_min[0], t.node_max[0]
+    mid = (mn + mx) * np.float32(0.5)
+    co = t.children_offset[0]
+    for k in range(8):
+        z, x, y = (k >> 2) & 1, (k >> 1) & 1, k & 1
+        want_min = [mid[0] if x else mn[0], mid[1] if y else mn[1], mid[2] if z else mn[2]]
+        want_max = [mx[0] if x else mid[0], mx[1] if y else mid[1], mx[2] if z else mid[2]]
+        assert np.array_equal(t.node_min[co + k], want_min) and np.array_equal(t.node_max[co + k], want_max)
+
+
+def test_bfs_layout_invariants(ort):
+    t = ort.build_octree(ort.random_spheres(2000, 11), 5, 1)
+    co, oo, cnt = t.children_offset, t.objects_offset, t.object_count
+    internal = co != -1
+    assert np.all(co[internal] > np.nonzero(internal)[0])  # children after parent (BFS)
+    assert np.all(np.diff(co[internal]) == 8)              # children of consecutive parents are contiguous
+    assert np.all(cnt[internal] == 0) and np.all(oo[internal] == -1)
+    leaves = ~internal & (cnt > 0)
+    assert np.array_equal(np.cumsum(cnt[leaves])[:-1], oo[leaves][1:])  # offsets in BFS order
+    assert np.all(oo[~internal & (cnt == 0)] == -1)
+
+
+@pytest.mark.parametrize("n,d,m,seed", [(1, 3, 0, 1), (2, 4, 0, 2), (50, 0, 0, 3), (50, 6, 10, 4), (500, 4, -1, 5),
+                                        (3000, 6, 2, 6), (777, 7, 0, 8)])
+def test_builder_matches_live_reference(ort, oracle, n, d, m, seed):
+    if not oracle.ref_octree_available():
+        pytest.skip("oracle/_ref/ref_octree not built (no /root/reference)")
+    s = ort.random_spheres(n, seed)
+    rec, idx, _ = oracle.ref_build_octree(s.center_radius, d, m)
+    t = ort.build_octree(s, d, m)
+    assert np.array_equal(t.gpu_records(), rec) and np.array_equal(t.object_indices, idx)
