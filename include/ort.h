@@ -81,7 +81,8 @@ typedef struct ort_scene_info {
 #define ORT_LAYOUT_EXPLICIT 1  /* reference record layout, boxes read from memory */
 
 /* Options (ort_set_option). */
-#define ORT_OPT_FORCE_LAYOUT 1 /* -1 auto (default), or ORT_LAYOUT_* */
+#define ORT_OPT_FORCE_LAYOUT 1     /* -1 auto (default), or ORT_LAYOUT_* */
+#define ORT_OPT_EXACT_TRAVERSAL 2  /* 1: disable the sign-specialised fast walk (A/B testing; same pixels) */
 
 /* Traffic counters (ort_count_traffic), in the REFERENCE layout's terms. */
 #define ORT_COUNT_NODES_POPPED 0

@@ -38,6 +38,7 @@ struct LaunchArgs {
     int tilesX;
     float* out;
     unsigned long long* counters;
+    int exact_only;  // ORT_OPT_EXACT_TRAVERSAL: disable the fast path (A/B testing)
 };
 
 __host__ __device__ inline int tile_row_to_y(const TileMap& t, int j) {
@@ -46,11 +47,13 @@ __host__ __device__ inline int tile_row_to_y(const TileMap& t, int j) {
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
+constexpr size_t kRankLutBytes = 8 * 256;  // ort::rank_lut_entry table
+
 size_t lds_bytes(int mode, int depth) {
     if (mode != 0) return 0;
     const size_t planes = align16(sizeof(float) * 3 * (((size_t)1 << depth) + 1));
     const size_t levels = (size_t)std::max(depth, 1);
-    return planes + 2 * levels * kBlock * sizeof(int);
+    return planes + kRankLutBytes + 2 * levels * kBlock * sizeof(int);
 }
 
 template <int MODE, bool COUNT>
@@ -58,6 +61,7 @@ __global__ void __launch_bounds__(kBlock) ort_trace_kernel(LaunchArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tid = threadIdx.x;
     const float* planes = nullptr;
+    const uint8_t* rank_lut = nullptr;
     ort::LdsFrames fr;
     fr.co = nullptr;
     fr.tm = nullptr;
@@ -69,9 +73,13 @@ __global__ void __launch_bounds__(kBlock) ort_trace_kernel(LaunchArgs A) {
         float* lp = reinterpret_cast<float*>(smem);
         for (int i = tid; i < np; i += kBlock) lp[i] = A.S.planes[i];
         const size_t poff = align16(sizeof(float) * (size_t)np);
-        fr.co = reinterpret_cast<int*>(smem + poff);
-        fr.tm = reinterpret_cast<float*>(smem + poff + (size_t)(D > 0 ? D : 1) * kBlock * sizeof(int));
+        uint8_t* lut = smem + poff;
+        for (int i = tid; i < (int)kRankLutBytes; i += kBlock) lut[i] = ort::rank_lut_entry((uint32_t)i >> 8, (uint32_t)i & 255u);
+        const size_t foff = poff + kRankLutBytes;
+        fr.co = reinterpret_cast<int*>(smem + foff);
+        fr.tm = reinterpret_cast<float*>(smem + foff + (size_t)(D > 0 ? D : 1) * kBlock * sizeof(int));
         planes = lp;
+        if (!A.exact_only) rank_lut = lut;
         __syncthreads();
     }
     const int wave = tid >> 6, lane = tid & 63;
@@ -91,9 +99,9 @@ __global__ void __launch_bounds__(kBlock) ort_trace_kernel(LaunchArgs A) {
     if constexpr (MODE == 1) {
         int snode[ORT_MAX_STACK];
         float stmin[ORT_MAX_STACK];
-        c = ort::shade_pixel<MODE, COUNT>(A.pp, A.S, planes, fr, snode, stmin, A.tm.x0 + col, y, cnt);
+        c = ort::shade_pixel<MODE, COUNT>(A.pp, A.S, planes, rank_lut, fr, snode, stmin, A.tm.x0 + col, y, cnt);
     } else {
-        c = ort::shade_pixel<MODE, COUNT>(A.pp, A.S, planes, fr, nullptr, nullptr, A.tm.x0 + col, y, cnt);
+        c = ort::shade_pixel<MODE, COUNT>(A.pp, A.S, planes, rank_lut, fr, nullptr, nullptr, A.tm.x0 + col, y, cnt);
     }
     o[0] = c.x;
     o[1] = c.y;
@@ -119,6 +127,7 @@ struct ort_ctx {
     bool timed = false;
     std::string err;
     int force_layout = -1;
+    int exact_only = 0;
     bool has_scene = false;
     int layout = ORT_LAYOUT_EXPLICIT;
     int depth = 0;
@@ -321,6 +330,7 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     a.tilesX = (t->width + 15) / 16;
     a.out = dout;
     a.counters = dcounters;
+    a.exact_only = ctx->exact_only;
     const int tilesY = (t->rows + 15) / 16;
     const long long blocks = (long long)a.tilesX * tilesY;
     if (blocks > 0) {
@@ -388,6 +398,10 @@ int ort_set_option(ort_ctx* ctx, int option, int value) {
     if (option == ORT_OPT_FORCE_LAYOUT) {
         if (value < -1 || value > ORT_LAYOUT_EXPLICIT) return fail(ctx, ORT_ERR_INVALID_ARG, "bad layout");
         ctx->force_layout = value;
+        return ORT_OK;
+    }
+    if (option == ORT_OPT_EXACT_TRAVERSAL) {
+        ctx->exact_only = value ? 1 : 0;
         return ORT_OK;
     }
     return fail(ctx, ORT_ERR_INVALID_ARG, "unknown option");
@@ -514,7 +528,7 @@ int ort_debug_emulate_render(const float* cr, const float* ma, const float* fr, 
         if (p->use_octree == 1) {
             if (n_nodes <= 0) return fail(nullptr, ORT_ERR_NO_SCENE, "no octree");
             std::string why;
-            if (layout == ORT_LAYOUT_COMPACT) {
+            if (layout == ORT_LAYOUT_COMPACT || layout == 2) {
                 if (!ort::buildCompactLayout(in, ORT_COMPACT_MAX_DEPTH, cl, why))
                     return fail(nullptr, ORT_ERR_UNSUPPORTED, why);
                 mode = 0;
@@ -545,6 +559,9 @@ int ort_debug_emulate_render(const float* cr, const float* ma, const float* fr, 
         const TileMap tm = {t->x0, t->width, t->y0, t->rows, t->band_height, t->band_stride};
         ort::Counters total;
         for (int k = 0; k < 6; ++k) total.v[k] = 0;
+        std::vector<uint8_t> lut(kRankLutBytes);
+        for (size_t i = 0; i < lut.size(); ++i) lut[i] = ort::rank_lut_entry((uint32_t)i >> 8, (uint32_t)i & 255u);
+        const uint8_t* rank_lut = (layout == ORT_LAYOUT_COMPACT) ? lut.data() : nullptr;
         std::vector<int> snode(ORT_MAX_STACK);
         std::vector<float> stmin(ORT_MAX_STACK);
         ort::LocalFrames lf;
@@ -556,9 +573,9 @@ int ort_debug_emulate_render(const float* cr, const float* ma, const float* fr, 
                 ort::Counters cc;
                 for (int k = 0; k < 6; ++k) cc.v[k] = 0;
                 ort::V3 v;
-                if (mode == 0) v = ort::shade_pixel<0, true>(pp, S, S.planes, lf, nullptr, nullptr, t->x0 + c, y, cc);
-                else if (mode == 1) v = ort::shade_pixel<1, true>(pp, S, nullptr, lf, snode.data(), stmin.data(), t->x0 + c, y, cc);
-                else v = ort::shade_pixel<2, true>(pp, S, nullptr, lf, nullptr, nullptr, t->x0 + c, y, cc);
+                if (mode == 0) v = ort::shade_pixel<0, true>(pp, S, S.planes, rank_lut, lf, nullptr, nullptr, t->x0 + c, y, cc);
+                else if (mode == 1) v = ort::shade_pixel<1, true>(pp, S, nullptr, nullptr, lf, snode.data(), stmin.data(), t->x0 + c, y, cc);
+                else v = ort::shade_pixel<2, true>(pp, S, nullptr, nullptr, lf, nullptr, nullptr, t->x0 + c, y, cc);
                 o[0] = v.x; o[1] = v.y; o[2] = v.z;
                 cc.v[4] = 1;
                 for (int k = 0; k < 6; ++k) total.v[k] += cc.v[k];

@@ -335,6 +335,176 @@ ORT_FN bool traverse_compact(const KScene& S, const float* planes, const Ray& r,
     return hit;
 }
 
+// ---------------------------------------------------------------------------------------
+// Fast path of traverse_compact for rays whose direction has no zero (or denormal-reciprocal)
+// component, i.e. 1/d is finite on every axis.  Then no slab value can be NaN and, per
+// axis, t(p) = inv*(p - o) is monotone in p, so every GLSL min/max of the reference is
+// decided by the sign of d alone:
+//   * the entry/exit of a child slab are its near/far planes' t (no compare needed);
+//   * the traversal order (glsl:352-447) of an all-non-zero sign vector is
+//     order[r] = perm(r) ^ m, m = (d.z<0)<<2 | (d.x<0)<<1 | (d.y<0), perm = identity for
+//     d.x > 0 and "swap bits 0,1" for d.x < 0 (checked for all 8 tables), so children are
+//     evaluated directly in traversal-rank space with static role axes
+//     A = rank bit 1 (x, or y when swapped), B = rank bit 0, C = rank bit 2 (z), and
+//     rank bit 0 = near half along that axis;
+//   * IEEE max3/min3 equal the GLSL chains (no NaN); a +0/-0 tie can pick the other zero,
+//     which is harmless because every tmin is only ever compared (never divided by).
+// The pushed tmin of a child is max(childTMin, node_tmin) = max(max3(entries), node_tmin),
+// and the reference's push test (tmax >= tmin && !(tmax < node_tmin) && !(tmin > closest))
+// becomes min(tmax, FLT_MAX) >= that value.  Results are bit-identical to the exact walk
+// (tests/test_emulation.py forces both on the same rays).
+//
+// rank_lut[m*256 + childMask] maps the node's octant-space child mask to rank space.
+ORT_FN uint32_t rank_perm(uint32_t r, uint32_t m) {
+    const uint32_t swap = (m >> 1) & 1u;  // perm = swap bits 0,1 when d.x < 0
+    const uint32_t p = swap ? ((r & 4u) | ((r & 1u) << 1) | ((r >> 1) & 1u)) : r;
+    return p ^ m;
+}
+ORT_FN uint8_t rank_lut_entry(uint32_t m, uint32_t cmask) {
+    uint32_t out = 0;
+    for (uint32_t r = 0; r < 8; ++r)
+        if ((cmask >> rank_perm(r, m)) & 1u) out |= 1u << r;
+    return (uint8_t)out;
+}
+
+ORT_FN bool fast_path_ok(V3 inv) {
+    return fabsf(inv.x) <= ORT_MAXFLOAT && fabsf(inv.y) <= ORT_MAXFLOAT && fabsf(inv.z) <= ORT_MAXFLOAT;
+}
+
+ORT_FN float fmax3(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
+ORT_FN float fmin3(float a, float b, float c) { return fminf(fminf(a, b), c); }
+
+template <bool COUNT, class Frames>
+ORT_FN bool traverse_fast(const KScene& S, const float* planes, const uint8_t* rank_lut, const Ray& r, V3 inv,
+                          float t_min, float t_max, int& hitEntry, float& hitT, Frames& fr, Counters& cnt) {
+    const int D = S.depth;
+    const int P1 = (1 << D) + 1;
+    const uint32_t nx = r.d.x < 0.0f, ny = r.d.y < 0.0f, nz = r.d.z < 0.0f;
+    const uint32_t m = (nz << 2) | (nx << 1) | ny;
+    const bool swap = nx != 0;
+    // role axes: A <- x (y if swapped), B <- y (x if swapped), C <- z
+    const float* PA = planes + (swap ? P1 : 0);
+    const float* PB = planes + (swap ? 0 : P1);
+    const float* PC = planes + 2 * P1;
+    const float oA = swap ? r.o.y : r.o.x, oB = swap ? r.o.x : r.o.y, oC = r.o.z;
+    const float iA = swap ? inv.y : inv.x, iB = swap ? inv.x : inv.y, iC = inv.z;
+    const uint32_t gA = swap ? ny : nx, gB = swap ? nx : ny, gC = nz;  // axis points negative
+    const float a = dot(r.d, r.d);
+    const int top = 1 << D;
+    // root box (glsl:304-311): near/far planes per axis
+    float tNA = iA * ((gA ? PA[top] : PA[0]) - oA), tFA = iA * ((gA ? PA[0] : PA[top]) - oA);
+    float tNB = iB * ((gB ? PB[top] : PB[0]) - oB), tFB = iB * ((gB ? PB[0] : PB[top]) - oB);
+    float tNC = iC * ((gC ? PC[top] : PC[0]) - oC), tFC = iC * ((gC ? PC[0] : PC[top]) - oC);
+    if (!(fmin3(tFA, tFB, tFC) >= fmax3(tNA, tNB, tNC))) return false;
+    int node = 0, depth = 0;
+    uint32_t cA = 0, cB = 0, cC = 0;
+    float ntmin = t_min;
+    float closest = t_max;
+    bool hit = false;
+    LevelMasks masks;
+    masks.clear();
+    for (;;) {
+        const uint2 rec = S.node[node];
+        if (COUNT) cnt.v[0] += 1;
+        if (rec.y & ORT_INTERNAL_FLAG) {
+            const int co = (int)rec.x;
+            if (COUNT) {
+                const long long rem = (long long)S.n_nodes - (long long)co;
+                cnt.v[1] += (unsigned long long)(rem >= 8 ? 8 : (rem > 0 ? rem : 0));
+            }
+            const uint32_t rcm = rank_lut[m * 256u + (rec.y & 0xffu)];
+            const int s = D - depth;
+            const float tMA = iA * (PA[(2 * cA + 1) << (s - 1)] - oA);
+            const float tMB = iB * (PB[(2 * cB + 1) << (s - 1)] - oB);
+            const float tMC = iC * (PC[(2 * cC + 1) << (s - 1)] - oC);
+            // entry: near child (rank bit 0) enters at tN, far child at tM; exit: tM / tF
+            const float e00 = fmaxf(tNA, tNB), e01 = fmaxf(tNA, tMB), e10 = fmaxf(tMA, tNB), e11 = fmaxf(tMA, tMB);
+            const float x00 = fminf(tMA, tMB), x01 = fminf(tMA, tFB), x10 = fminf(tFA, tMB), x11 = fminf(tFA, tFB);
+            const float cN = fminf(tMC, ORT_MAXFLOAT), cF = fminf(tFC, ORT_MAXFLOAT);
+            uint32_t rm = 0;
+            // rank r: A = bit1, B = bit0, C = bit2
+#define ORT_CHILD(R, EAB, XAB, EC, XC)                              \
+    {                                                               \
+        const float mm = fmax3(EAB, EC, ntmin);                     \
+        const float xx = fmin3(XAB, XC, ORT_MAXFLOAT);              \
+        rm |= (xx >= mm) ? (1u << (R)) : 0u;                        \
+    }
+            ORT_CHILD(0, e00, x00, tNC, cN)
+            ORT_CHILD(1, e01, x01, tNC, cN)
+            ORT_CHILD(2, e10, x10, tNC, cN)
+            ORT_CHILD(3, e11, x11, tNC, cN)
+            ORT_CHILD(4, e00, x00, tMC, cF)
+            ORT_CHILD(5, e01, x01, tMC, cF)
+            ORT_CHILD(6, e10, x10, tMC, cF)
+            ORT_CHILD(7, e11, x11, tMC, cF)
+#undef ORT_CHILD
+            rm &= rcm;
+            if (rm) {
+                const int rk = __builtin_ctz(rm);
+                const uint32_t rest = rm & (rm - 1u);
+                if (rest) {
+                    masks.put(depth, rest);
+                    fr.set(depth, co, ntmin);
+                }
+                const uint32_t bA = (rk >> 1) & 1u, bB = rk & 1u, bC = (rk >> 2) & 1u;
+                const float eA = bA ? tMA : tNA, eB = bB ? tMB : tNB, eC = bC ? tMC : tNC;
+                ntmin = fmax3(fmaxf(eA, eB), eC, ntmin);
+                tFA = bA ? tFA : tMA;
+                tNA = eA;
+                tFB = bB ? tFB : tMB;
+                tNB = eB;
+                tFC = bC ? tFC : tMC;
+                tNC = eC;
+                cA = 2 * cA + (bA ^ gA);
+                cB = 2 * cB + (bB ^ gB);
+                cC = 2 * cC + (bC ^ gC);
+                node = co + (int)rank_perm((uint32_t)rk, m);
+                depth += 1;
+                continue;
+            }
+        } else {
+            const int off = (int)rec.x;
+            const int n = (int)rec.y;
+            for (int i = 0; i < n; ++i) {
+                const float4 sp = S.leaf_sph[off + i];
+                if (COUNT) cnt.v[2] += 1;
+                float t;
+                if (sphere_hit_t(r, a, sp, ntmin, closest, t)) {
+                    hit = true;
+                    closest = t;
+                    hitEntry = off + i;
+                    if (COUNT) cnt.v[3] += 1;
+                }
+            }
+            if (hit) break;
+        }
+        // backtrack: next child of the deepest level with one left
+        const int L = masks.top();
+        if (L < 0) break;
+        const int rk = masks.pop(L);
+        const int sh = depth - L;
+        const uint32_t bA = (rk >> 1) & 1u, bB = rk & 1u, bC = (rk >> 2) & 1u;
+        cA = ((cA >> sh) << 1) | (bA ^ gA);
+        cB = ((cB >> sh) << 1) | (bB ^ gB);
+        cC = ((cC >> sh) << 1) | (bC ^ gC);
+        depth = L + 1;
+        node = fr.getCo(L) + (int)rank_perm((uint32_t)rk, m);
+        const int s = D - depth;
+        const float loA = PA[cA << s], hiA = PA[(cA + 1) << s];
+        const float loB = PB[cB << s], hiB = PB[(cB + 1) << s];
+        const float loC = PC[cC << s], hiC = PC[(cC + 1) << s];
+        tNA = iA * ((gA ? hiA : loA) - oA);
+        tFA = iA * ((gA ? loA : hiA) - oA);
+        tNB = iB * ((gB ? hiB : loB) - oB);
+        tFB = iB * ((gB ? loB : hiB) - oB);
+        tNC = iC * ((gC ? hiC : loC) - oC);
+        tFC = iC * ((gC ? loC : hiC) - oC);
+        ntmin = fmax3(fmaxf(tNA, tNB), tNC, fr.getTm(L));
+    }
+    hitT = closest;
+    return hit;
+}
+
 // Literal restatement of traverseOctree (glsl:290-481) over the reference record layout
 // (boxes read from memory, 200-entry stack).  Used for trees the compact layout cannot
 // represent.  `stack_node`/`stack_tmin` point at ORT_MAX_STACK entries owned by the lane.
@@ -568,13 +738,19 @@ ORT_FN Ray camera_ray(const KCamera& c, float s, float t, float W, float H, ort_
 // Intersection dispatch for one ray; fills the hit record like intersectScene (glsl:500-506).
 // MODE: 0 compact octree, 1 explicit octree, 2 brute force.
 template <int MODE, bool COUNT, class Frames>
-ORT_FN bool intersect(const KScene& S, const float* planes, const Ray& r, HitRec& h, Frames& fr, int* snode,
-                      float* stmin, Counters& cnt) {
+ORT_FN bool intersect(const KScene& S, const float* planes, const uint8_t* rank_lut, const Ray& r, HitRec& h,
+                      Frames& fr, int* snode, float* stmin, Counters& cnt) {
     int entry = -1;
     float t = 0.0f;
     bool hit;
     if (COUNT) cnt.v[5] += 1;
-    if (MODE == 0) hit = traverse_compact<COUNT>(S, planes, r, 0.001f, ORT_MAXFLOAT, entry, t, fr, cnt);
+    if (MODE == 0) {
+        const V3 inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+        if (rank_lut && fast_path_ok(inv))
+            hit = traverse_fast<COUNT>(S, planes, rank_lut, r, inv, 0.001f, ORT_MAXFLOAT, entry, t, fr, cnt);
+        else
+            hit = traverse_compact<COUNT>(S, planes, r, 0.001f, ORT_MAXFLOAT, entry, t, fr, cnt);
+    }
     else if (MODE == 1) hit = traverse_explicit<COUNT>(S, r, 0.001f, ORT_MAXFLOAT, entry, t, snode, stmin, cnt);
     else hit = traverse_brute<COUNT>(S, r, 0.001f, ORT_MAXFLOAT, entry, t, cnt);
     if (!hit) return false;
@@ -609,8 +785,8 @@ struct PixelParams {
 
 // main() of the fragment shader (glsl:636-664) for pixel (px, py), py = 0 the bottom row.
 template <int MODE, bool COUNT, class Frames>
-ORT_FN V3 shade_pixel(const PixelParams& P, const KScene& S, const float* planes, Frames& fr, int* snode, float* stmin,
-                      int px, int py, Counters& cnt) {
+ORT_FN V3 shade_pixel(const PixelParams& P, const KScene& S, const float* planes, const uint8_t* rank_lut, Frames& fr,
+                      int* snode, float* stmin, int px, int py, Counters& cnt) {
     const float W = (float)P.W, H = (float)P.H;
     const float fx = (float)px + 0.5f, fy = (float)py + 0.5f;
     ort_rng st;
@@ -631,7 +807,7 @@ ORT_FN V3 shade_pixel(const PixelParams& P, const KScene& S, const float* planes
         for (int b = 0; b < P.maxDepth; ++b) {
             if (importance < 0.01f) break;
             HitRec h;
-            if (intersect<MODE, COUNT>(S, planes, ray, h, fr, snode, stmin, cnt)) {
+            if (intersect<MODE, COUNT>(S, planes, rank_lut, ray, h, fr, snode, stmin, cnt)) {
                 Ray wi;
                 wi.d = ray.d;
                 V3 att = mk(0.0f, 0.0f, 0.0f);

@@ -110,6 +110,10 @@ class Renderer:
         """Force ORT_LAYOUT_COMPACT / ORT_LAYOUT_EXPLICIT (-1 = auto) for the next upload."""
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_FORCE_LAYOUT, int(layout)))
 
+    def set_exact_traversal(self, on: bool):
+        """Disable (True) / enable the sign-specialised fast walk; pixels are identical either way."""
+        self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_EXACT_TRAVERSAL, int(bool(on))))
+
     def upload(self, spheres: SphereSet, tree: FlatOctree | None):
         cr = np.ascontiguousarray(spheres.center_radius, np.float32)
         ma = np.ascontiguousarray(spheres.mat_albedo, np.float32)

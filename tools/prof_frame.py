@@ -1,0 +1,33 @@
+"""Render N frames of a bench config with only the production kernel (no counting pass):
+the command profiled by tools/profile_box.sh under rocprofv3 PMC passes."""
+import argparse
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+import numpy as np  # noqa: E402
+
+import bench  # noqa: E402
+import octreeraytracer_amd as ort  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--config", default="c3")
+ap.add_argument("--frames", type=int, default=3)
+ap.add_argument("--layout", type=int, default=-1)
+a = ap.parse_args()
+W, H, N, D, M, NS, MD = bench.CONFIGS[a.config]
+s = ort.random_spheres(N, 42)
+t = ort.build_octree(s, D, M)
+r = ort.Renderer(0)
+r.set_layout(a.layout)
+r.upload(s, t)
+p = ort.FrameParams.default_camera(W, H, num_samples=NS, max_depth=MD)
+out = np.empty((H, W, 3), np.float32)
+ms = []
+for _ in range(a.frames):
+    r.render(p, out=out)
+    ms.append(r.last_kernel_ms())
+print(f"{a.config} layout={r.info()['layout']} kernel ms: {['%.3f' % m for m in ms]}", flush=True)
