@@ -132,9 +132,13 @@ int ort_scene_get_info(const ort_ctx* ctx, ort_scene_info* info);
 int ort_render(ort_ctx* ctx, const ort_params* params, const ort_tile* tile,
                float* rgb_out, int out_is_device, void* stream);
 
-/* Duration in milliseconds of the last ort_render's kernel, from HIP events recorded
- * around the launch on its stream.  Only valid once that stream has passed the frame. */
+/* Duration in milliseconds of the last ort_render's kernels (the whole per-frame pipeline),
+ * from HIP events recorded on its stream.  Only valid once that stream has passed the frame. */
 int ort_last_kernel_ms(ort_ctx* ctx, float* ms);
+
+/* Duration in milliseconds from the start of the last ort_render to the end of its first
+ * trace kernel (the dominant kernel: camera rays + octree walk of bounce 0, sample 0). */
+int ort_last_trace_ms(ort_ctx* ctx, float* ms);
 
 /* Run the counting variant of the kernel over the tile and return, summed over all
  * pixels, the reference-layout work counters ORT_COUNT_* (counts[ORT_COUNT_N]). */

@@ -2,12 +2,18 @@
 //
 // Replaces the reference's GL dispatch: setupBuffers' SSBO uploads
 // (src/raytracer.cpp:74-152) become ort_upload_*; the per-frame uniform update +
-// glDrawArrays (src/raytracer.cpp:491-499) becomes ort_render, which launches
-// ort_trace_kernel: one pixel per lane, a 64-lane wave = an 8x8 pixel block, a 256-lane
-// workgroup = a 16x16 tile.  The fragment shader body (glsl:636-664) runs per lane from
-// render_core.h.  The octree walk keeps one frame per tree level in LDS (columns indexed
-// by lane: conflict-free), per-level child masks in registers, and the split-plane table
-// of the tree in LDS (3 x (2^D+1) floats, loaded once per workgroup).
+// glDrawArrays (src/raytracer.cpp:491-499) becomes ort_render, which runs the fragment
+// shader (glsl:636-664) as a wavefront pipeline, per sample and bounce:
+//   ort_trace_kernel    camera ray (bounce 0) or stored ray + octree walk -> 8-byte hit
+//                       record; one path per lane, a wave = 8x8 pixels, a workgroup = 16x16.
+//                       Only the sign-specialised fast walk is compiled in, so it runs at
+//                       8 waves/SIMD; rays it cannot take are appended to a defer list.
+//   ort_trace_exact     the exact walk for the (rare) deferred rays, persistent grid.
+//   ort_shade_kernel    BSDF / sky, path state or (1 spp, 1 bounce) the final pixel.
+//   ort_finalize_kernel average + gamma for the multi-sample / multi-bounce case.
+// The walk keeps one frame per tree level in LDS (columns indexed by lane: conflict-free),
+// per-level child masks in registers, and the tree's split-plane table in LDS
+// (3 x (2^D+1) floats, loaded once per workgroup).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -31,14 +37,25 @@ struct TileMap {
     int x0, tw, y0, th, bh, bs;
 };
 
-struct LaunchArgs {
+struct PipeArgs {
     ort::PixelParams pp;
     ort::KScene S;
     TileMap tm;
     int tilesX;
+    int sample;       // s of main()'s sample loop
+    int last;         // this bounce is the last one (b == maxDepth - 1)
+    int nobounce;     // maxDepth <= 0: radiance() returns (1,1,1) without tracing
+    int exact_only;   // ORT_OPT_EXACT_TRAVERSAL: every compact ray takes the exact walk
+    int2* hit;        // per path: {entry (-1 miss, -2 deferred, -3 outside the frame), t bits}
+    int* defer_list;
+    int* defer_count;
+    float4* po;       // o.xyz, importance
+    float4* pd;       // d.xyz, alive (1/0)
+    float4* pc;       // path throughput c.xyz
+    float2* prng;     // randState
+    float4* pcol;     // running sum of samples
     float* out;
     unsigned long long* counters;
-    int exact_only;  // ORT_OPT_EXACT_TRAVERSAL: disable the fast path (A/B testing)
 };
 
 __host__ __device__ inline int tile_row_to_y(const TileMap& t, int j) {
@@ -56,61 +73,231 @@ size_t lds_bytes(int mode, int depth) {
     return planes + kRankLutBytes + 2 * levels * kBlock * sizeof(int);
 }
 
-template <int MODE, bool COUNT>
-__global__ void __launch_bounds__(kBlock) ort_trace_kernel(LaunchArgs A) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int tid = threadIdx.x;
-    const float* planes = nullptr;
-    const uint8_t* rank_lut = nullptr;
+// LDS image of one workgroup: split planes | rank LUT | frame columns (co, tmin).
+struct LdsView {
+    const float* planes;
+    const uint8_t* lut;
     ort::LdsFrames fr;
-    fr.co = nullptr;
-    fr.tm = nullptr;
-    fr.stride = kBlock;
-    fr.lane = tid;
-    if constexpr (MODE == 0) {
-        const int D = A.S.depth;
-        const int np = 3 * ((1 << D) + 1);
-        float* lp = reinterpret_cast<float*>(smem);
-        for (int i = tid; i < np; i += kBlock) lp[i] = A.S.planes[i];
-        const size_t poff = align16(sizeof(float) * (size_t)np);
-        uint8_t* lut = smem + poff;
-        for (int i = tid; i < (int)kRankLutBytes; i += kBlock) lut[i] = ort::rank_lut_entry((uint32_t)i >> 8, (uint32_t)i & 255u);
-        const size_t foff = poff + kRankLutBytes;
-        fr.co = reinterpret_cast<int*>(smem + foff);
-        fr.tm = reinterpret_cast<float*>(smem + foff + (size_t)(D > 0 ? D : 1) * kBlock * sizeof(int));
-        planes = lp;
-        if (!A.exact_only) rank_lut = lut;
-        __syncthreads();
+};
+template <bool WITH_LUT>
+__device__ inline LdsView setup_lds(unsigned char* smem, const ort::KScene& S) {
+    const int tid = threadIdx.x;
+    const int D = S.depth;
+    const int np = 3 * ((1 << D) + 1);
+    float* lp = reinterpret_cast<float*>(smem);
+    for (int i = tid; i < np; i += kBlock) lp[i] = S.planes[i];
+    const size_t poff = align16(sizeof(float) * (size_t)np);
+    uint8_t* lut = smem + poff;
+    if (WITH_LUT)
+        for (int i = tid; i < (int)kRankLutBytes; i += kBlock)
+            lut[i] = ort::rank_lut_entry((uint32_t)i >> 8, (uint32_t)i & 255u);
+    const size_t foff = poff + kRankLutBytes;
+    LdsView v;
+    v.planes = lp;
+    v.lut = WITH_LUT ? lut : nullptr;
+    v.fr.co = reinterpret_cast<int*>(smem + foff);
+    v.fr.tm = reinterpret_cast<float*>(smem + foff + (size_t)(D > 0 ? D : 1) * kBlock * sizeof(int));
+    v.fr.stride = kBlock;
+    v.fr.lane = tid;
+    __syncthreads();
+    return v;
+}
+
+// thread -> (col, row) of the tile: 16x16 pixels per workgroup, 8x8 per wave
+__device__ inline void tile_coords(int tilesX, int& col, int& row) {
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int bx = blockIdx.x % tilesX, by = blockIdx.x / tilesX;
+    col = bx * 16 + (wave & 1) * 8 + (lane & 7);
+    row = by * 16 + (wave >> 1) * 8 + (lane >> 3);
+}
+
+template <bool COUNT>
+__device__ inline void flush_counts(const ort::Counters& c, unsigned long long* dst) {
+    if (COUNT)
+        for (int k = 0; k < 6; ++k)
+            if (c.v[k]) atomicAdd(dst + k, c.v[k]);
+}
+
+__device__ inline ort::Ray load_ray(const PipeArgs& A, int p) {
+    const float4 o = A.po[p], d = A.pd[p];
+    ort::Ray r;
+    r.o = ort::mk(o.x, o.y, o.z);
+    r.d = ort::mk(d.x, d.y, d.z);
+    return r;
+}
+
+__device__ inline ort_rng start_rng(const PipeArgs& A, int p, int px, int py) {
+    ort_rng st;
+    if (A.sample == 0) {
+        ort::pixel_rng_init(A.pp, px, py, st);
+    } else {
+        const float2 v = A.prng[p];
+        st.x = v.x;
+        st.y = v.y;
     }
-    const int wave = tid >> 6, lane = tid & 63;
-    const int bx = blockIdx.x % A.tilesX, by = blockIdx.x / A.tilesX;
-    const int col = bx * 16 + (wave & 1) * 8 + (lane & 7);
-    const int row = by * 16 + (wave >> 1) * 8 + (lane >> 3);
+    return st;
+}
+
+// Bounce-b trace.  PRIMARY: the camera ray of sample A.sample is generated here.
+template <int MODE, bool COUNT, bool PRIMARY>
+__global__ void __launch_bounds__(kBlock) ort_trace_kernel(PipeArgs A) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    LdsView L;
+    L.planes = nullptr;
+    L.lut = nullptr;
+    if constexpr (MODE == 0) L = setup_lds<true>(smem, A.S);
+    int col, row;
+    tile_coords(A.tilesX, col, row);
     if (col >= A.tm.tw || row >= A.tm.th) return;
+    const int p = row * A.tm.tw + col;
     const int y = tile_row_to_y(A.tm, row);
-    float* o = A.out + 3 * ((size_t)row * (size_t)A.tm.tw + (size_t)col);
+    if (y >= A.pp.H) {
+        A.hit[p] = make_int2(-3, 0);
+        return;
+    }
+    ort::Ray ray;
+    if constexpr (PRIMARY) {
+        ort_rng st = start_rng(A, p, A.tm.x0 + col, y);
+        ray = ort::primary_ray(A.pp, A.tm.x0 + col, y, A.sample, st);
+    } else {
+        if (A.pd[p].w == 0.0f) return;
+        ray = load_ray(A, p);
+    }
+    ort::Counters cnt;
+    for (int k = 0; k < 6; ++k) cnt.v[k] = 0;
+    float t;
+    int entry;
+    int st;
+    if constexpr (MODE == 1) {
+        int snode[ORT_MAX_STACK];
+        float stmin[ORT_MAX_STACK];
+        st = ort::trace_ray<MODE, COUNT>(A.S, L.planes, L.lut, ray, false, t, entry, L.fr, snode, stmin, cnt);
+    } else {
+        const uint8_t* lut = A.exact_only ? nullptr : L.lut;
+        st = ort::trace_ray<MODE, COUNT>(A.S, L.planes, lut, ray, MODE == 0, t, entry, L.fr, nullptr, nullptr, cnt);
+    }
+    if (st == ORT_TRACE_DEFER) {
+        const int k = atomicAdd(A.defer_count, 1);
+        A.defer_list[k] = p;
+        A.hit[p] = make_int2(-2, 0);
+    } else {
+        A.hit[p] = make_int2(st == ORT_TRACE_HIT ? entry : -1, __float_as_int(t));
+    }
+    flush_counts<COUNT>(cnt, A.counters);
+}
+
+// Exact compact walk (traverse_compact) for the deferred rays; persistent grid.
+template <bool COUNT, bool PRIMARY>
+__global__ void __launch_bounds__(kBlock) ort_trace_exact(PipeArgs A) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    LdsView L = setup_lds<false>(smem, A.S);
+    const int n = *A.defer_count;
+    ort::Counters cnt;
+    for (int k = 0; k < 6; ++k) cnt.v[k] = 0;
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+        const int p = A.defer_list[i];
+        const int row = p / A.tm.tw, col = p - row * A.tm.tw;
+        const int y = tile_row_to_y(A.tm, row);
+        ort::Ray ray;
+        if constexpr (PRIMARY) {
+            ort_rng st = start_rng(A, p, A.tm.x0 + col, y);
+            ray = ort::primary_ray(A.pp, A.tm.x0 + col, y, A.sample, st);
+        } else {
+            ray = load_ray(A, p);
+        }
+        float t;
+        int entry;
+        const int st = ort::trace_ray<0, COUNT>(A.S, L.planes, nullptr, ray, false, t, entry, L.fr, nullptr, nullptr, cnt);
+        A.hit[p] = make_int2(st == ORT_TRACE_HIT ? entry : -1, __float_as_int(t));
+    }
+    flush_counts<COUNT>(cnt, A.counters);
+}
+
+// Bounce-b shading.  DIRECT (1 sample, 1 bounce): writes the final pixel.
+template <int MODE, bool PRIMARY, bool DIRECT>
+__global__ void __launch_bounds__(kBlock) ort_shade_kernel(PipeArgs A) {
+    int col, row;
+    tile_coords(A.tilesX, col, row);
+    if (col >= A.tm.tw || row >= A.tm.th) return;
+    const int p = row * A.tm.tw + col;
+    const int y = tile_row_to_y(A.tm, row);
+    if (y >= A.pp.H) {
+        if (DIRECT) {
+            float* o = A.out + 3 * (size_t)p;
+            o[0] = 0.0f; o[1] = 0.0f; o[2] = 0.0f;
+        }
+        return;
+    }
+    ort::Ray ray;
+    ort_rng st;
+    ort::V3 c;
+    float importance;
+    if constexpr (PRIMARY) {
+        st = start_rng(A, p, A.tm.x0 + col, y);
+        ray = ort::primary_ray(A.pp, A.tm.x0 + col, y, A.sample, st);
+        c = ort::mk(1.0f, 1.0f, 1.0f);
+        importance = 1.0f;
+    } else {
+        const float4 d = A.pd[p];
+        if (d.w == 0.0f) return;
+        const float4 o = A.po[p], cc = A.pc[p];
+        const float2 r2 = A.prng[p];
+        ray.o = ort::mk(o.x, o.y, o.z);
+        ray.d = ort::mk(d.x, d.y, d.z);
+        importance = o.w;
+        c = ort::mk(cc.x, cc.y, cc.z);
+        st.x = r2.x;
+        st.y = r2.y;
+    }
+    bool done = true;
+    if (!A.nobounce) {
+        const int2 h = A.hit[p];
+        ort::HitRec rec;
+        if (h.x >= 0) rec = ort::hit_record<MODE>(A.S, ray, __int_as_float(h.y), h.x);
+        done = ort::shade_bounce(h.x >= 0, rec, ray, c, importance, st);
+        if (!done && (A.last || importance < 0.01f)) done = true;  // loop bound / glsl:605
+    }
+    if constexpr (DIRECT) {
+        const ort::V3 v = ort::finish_pixel(ort::add(ort::mk(0.0f, 0.0f, 0.0f), c), 1);
+        float* o = A.out + 3 * (size_t)p;
+        o[0] = v.x; o[1] = v.y; o[2] = v.z;
+    } else {
+        if (done) {
+            ort::V3 acc = ort::mk(0.0f, 0.0f, 0.0f);
+            if (A.sample > 0) {
+                const float4 a = A.pcol[p];
+                acc = ort::mk(a.x, a.y, a.z);
+            }
+            acc = ort::add(acc, c);
+            A.pcol[p] = make_float4(acc.x, acc.y, acc.z, 0.0f);
+            A.pd[p] = make_float4(ray.d.x, ray.d.y, ray.d.z, 0.0f);
+        } else {
+            A.po[p] = make_float4(ray.o.x, ray.o.y, ray.o.z, importance);
+            A.pd[p] = make_float4(ray.d.x, ray.d.y, ray.d.z, 1.0f);
+            A.pc[p] = make_float4(c.x, c.y, c.z, 0.0f);
+        }
+        A.prng[p] = make_float2(st.x, st.y);
+    }
+}
+
+__global__ void __launch_bounds__(kBlock) ort_finalize_kernel(PipeArgs A) {
+    int col, row;
+    tile_coords(A.tilesX, col, row);
+    if (col >= A.tm.tw || row >= A.tm.th) return;
+    const int p = row * A.tm.tw + col;
+    const int y = tile_row_to_y(A.tm, row);
+    float* o = A.out + 3 * (size_t)p;
     if (y >= A.pp.H) {
         o[0] = 0.0f; o[1] = 0.0f; o[2] = 0.0f;
         return;
     }
-    ort::Counters cnt;
-    for (int k = 0; k < 6; ++k) cnt.v[k] = 0;
-    ort::V3 c;
-    if constexpr (MODE == 1) {
-        int snode[ORT_MAX_STACK];
-        float stmin[ORT_MAX_STACK];
-        c = ort::shade_pixel<MODE, COUNT>(A.pp, A.S, planes, rank_lut, fr, snode, stmin, A.tm.x0 + col, y, cnt);
-    } else {
-        c = ort::shade_pixel<MODE, COUNT>(A.pp, A.S, planes, rank_lut, fr, nullptr, nullptr, A.tm.x0 + col, y, cnt);
+    ort::V3 acc = ort::mk(0.0f, 0.0f, 0.0f);
+    if (A.pp.ns > 0) {
+        const float4 a = A.pcol[p];
+        acc = ort::mk(a.x, a.y, a.z);
     }
-    o[0] = c.x;
-    o[1] = c.y;
-    o[2] = c.z;
-    if constexpr (COUNT) {
-        cnt.v[4] = 1;
-        for (int k = 0; k < 6; ++k)
-            if (cnt.v[k]) atomicAdd(A.counters + k, cnt.v[k]);
-    }
+    const ort::V3 v = ort::finish_pixel(acc, A.pp.ns);
+    o[0] = v.x; o[1] = v.y; o[2] = v.z;
 }
 
 struct DevBuf {
@@ -123,7 +310,7 @@ struct DevBuf {
 struct ort_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_trace = nullptr;
     bool timed = false;
     std::string err;
     int force_layout = -1;
@@ -137,6 +324,8 @@ struct ort_ctx {
     DevBuf node, leaf_sph, leaf_idx, planes;    // compact
     DevBuf nodeA, nodeB, cnt, indices;           // explicit
     DevBuf scratch_out, counters;
+    // wavefront pipeline state, sized for the largest tile rendered so far
+    DevBuf hit, defer_list, defer_count, po, pd, pc, prng, pcol;
 };
 
 namespace {
@@ -295,12 +484,47 @@ ort::PixelParams pixel_params(const ort_params* p) {
     return pp;
 }
 
-template <bool COUNT>
-hipError_t launch(int mode, const LaunchArgs& a, int blocks, size_t lds, hipStream_t s) {
-    if (mode == 0) hipLaunchKernelGGL((ort_trace_kernel<0, COUNT>), dim3(blocks), dim3(kBlock), lds, s, a);
-    else if (mode == 1) hipLaunchKernelGGL((ort_trace_kernel<1, COUNT>), dim3(blocks), dim3(kBlock), lds, s, a);
-    else hipLaunchKernelGGL((ort_trace_kernel<2, COUNT>), dim3(blocks), dim3(kBlock), lds, s, a);
+int ensure(ort_ctx* ctx, DevBuf& b, size_t bytes) {
+    if (b.bytes >= bytes && b.p) return ORT_OK;
+    free_buf(b);
+    HIPCHK(ctx, hipMalloc(&b.p, bytes));
+    b.bytes = bytes;
+    return ORT_OK;
+}
+
+template <int MODE, bool COUNT>
+hipError_t launch_trace(bool primary, const PipeArgs& a, int blocks, size_t lds, hipStream_t s) {
+    if (primary) hipLaunchKernelGGL((ort_trace_kernel<MODE, COUNT, true>), dim3(blocks), dim3(kBlock), lds, s, a);
+    else hipLaunchKernelGGL((ort_trace_kernel<MODE, COUNT, false>), dim3(blocks), dim3(kBlock), lds, s, a);
     return hipGetLastError();
+}
+
+template <bool COUNT>
+hipError_t launch_trace_mode(int mode, bool primary, const PipeArgs& a, int blocks, size_t lds, hipStream_t s) {
+    if (mode == 0) return launch_trace<0, COUNT>(primary, a, blocks, lds, s);
+    if (mode == 1) return launch_trace<1, COUNT>(primary, a, blocks, lds, s);
+    return launch_trace<2, COUNT>(primary, a, blocks, lds, s);
+}
+
+template <bool COUNT>
+hipError_t launch_exact(bool primary, const PipeArgs& a, int blocks, size_t lds, hipStream_t s) {
+    if (primary) hipLaunchKernelGGL((ort_trace_exact<COUNT, true>), dim3(blocks), dim3(kBlock), lds, s, a);
+    else hipLaunchKernelGGL((ort_trace_exact<COUNT, false>), dim3(blocks), dim3(kBlock), lds, s, a);
+    return hipGetLastError();
+}
+
+template <int MODE>
+hipError_t launch_shade_mode(bool primary, bool direct, const PipeArgs& a, int blocks, hipStream_t s) {
+    if (direct) hipLaunchKernelGGL((ort_shade_kernel<MODE, true, true>), dim3(blocks), dim3(kBlock), 0, s, a);
+    else if (primary) hipLaunchKernelGGL((ort_shade_kernel<MODE, true, false>), dim3(blocks), dim3(kBlock), 0, s, a);
+    else hipLaunchKernelGGL((ort_shade_kernel<MODE, false, false>), dim3(blocks), dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_shade(int mode, bool primary, bool direct, const PipeArgs& a, int blocks, hipStream_t s) {
+    if (mode == 0) return launch_shade_mode<0>(primary, direct, a, blocks, s);
+    if (mode == 1) return launch_shade_mode<1>(primary, direct, a, blocks, s);
+    return launch_shade_mode<2>(primary, direct, a, blocks, s);
 }
 
 int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out, int out_is_device,
@@ -310,39 +534,88 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     if (!ctx->has_scene) return fail(ctx, ORT_ERR_NO_SCENE, "ort_render: no scene uploaded");
     const int mode = (p->use_octree == 1) ? (ctx->layout == ORT_LAYOUT_COMPACT ? 0 : 1) : 2;
     if (mode != 2 && ctx->n_nodes <= 0) return fail(ctx, ORT_ERR_NO_SCENE, "ort_render: scene has no octree");
-    if (!out && (size_t)t->width * (size_t)t->rows > 0) return fail(ctx, ORT_ERR_INVALID_ARG, "ort_render: null output");
+    const size_t pix = (size_t)t->width * (size_t)t->rows;
+    if (!out && pix > 0) return fail(ctx, ORT_ERR_INVALID_ARG, "ort_render: null output");
+    if (pix == 0) return ORT_OK;
+    if (pix > 0x7fffffffULL) return fail(ctx, ORT_ERR_INVALID_ARG, "ort_render: tile too large");
     HIPCHK(ctx, hipSetDevice(ctx->device));
     hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
-    const size_t pix = (size_t)t->width * (size_t)t->rows;
     float* dout = out;
-    if (!out_is_device && pix > 0) {
-        if (ctx->scratch_out.bytes < 12 * pix) {
-            free_buf(ctx->scratch_out);
-            HIPCHK(ctx, hipMalloc(&ctx->scratch_out.p, 12 * pix));
-            ctx->scratch_out.bytes = 12 * pix;
-        }
+    int rc;
+    if (!out_is_device) {
+        if ((rc = ensure(ctx, ctx->scratch_out, 12 * pix))) return rc;
         dout = (float*)ctx->scratch_out.p;
     }
-    LaunchArgs a;
+    const int ns = p->num_samples, maxd = p->max_depth;
+    const bool direct = (ns == 1 && maxd == 1);
+    if ((rc = ensure(ctx, ctx->hit, 8 * pix)) || (rc = ensure(ctx, ctx->defer_list, 4 * pix)) ||
+        (rc = ensure(ctx, ctx->defer_count, 64)))
+        return rc;
+    if (!direct) {
+        if ((rc = ensure(ctx, ctx->po, 16 * pix)) || (rc = ensure(ctx, ctx->pd, 16 * pix)) ||
+            (rc = ensure(ctx, ctx->pc, 16 * pix)) || (rc = ensure(ctx, ctx->prng, 8 * pix)) ||
+            (rc = ensure(ctx, ctx->pcol, 16 * pix)))
+            return rc;
+    }
+    PipeArgs a;
+    std::memset(&a, 0, sizeof(a));
     a.pp = pixel_params(p);
     a.S = device_scene(ctx);
     a.tm = {t->x0, t->width, t->y0, t->rows, t->band_height, t->band_stride};
     a.tilesX = (t->width + 15) / 16;
+    a.exact_only = ctx->exact_only;
+    a.hit = (int2*)ctx->hit.p;
+    a.defer_list = (int*)ctx->defer_list.p;
+    a.defer_count = (int*)ctx->defer_count.p;
+    a.po = (float4*)ctx->po.p;
+    a.pd = (float4*)ctx->pd.p;
+    a.pc = (float4*)ctx->pc.p;
+    a.prng = (float2*)ctx->prng.p;
+    a.pcol = (float4*)ctx->pcol.p;
     a.out = dout;
     a.counters = dcounters;
-    a.exact_only = ctx->exact_only;
     const int tilesY = (t->rows + 15) / 16;
     const long long blocks = (long long)a.tilesX * tilesY;
-    if (blocks > 0) {
-        if (blocks > 0x7fffffffLL) return fail(ctx, ORT_ERR_INVALID_ARG, "ort_render: tile too large");
-        const size_t lds = lds_bytes(mode, ctx->depth);
-        HIPCHK(ctx, hipEventRecord(ctx->ev0, s));
-        hipError_t e = dcounters ? launch<true>(mode, a, (int)blocks, lds, s) : launch<false>(mode, a, (int)blocks, lds, s);
-        if (e != hipSuccess) return hip_fail(ctx, e, "ort_trace_kernel launch");
-        HIPCHK(ctx, hipEventRecord(ctx->ev1, s));
-        ctx->timed = true;
+    if (blocks > 0x7fffffffLL) return fail(ctx, ORT_ERR_INVALID_ARG, "ort_render: tile too large");
+    const size_t lds = lds_bytes(mode, ctx->depth);
+    const int exact_blocks = 1024;  // persistent grid for the deferred rays (4 per CU)
+    hipError_t e;
+    HIPCHK(ctx, hipEventRecord(ctx->ev0, s));
+    bool first_trace = true;
+    for (int smp = 0; smp < ns; ++smp) {
+        a.sample = smp;
+        const int bounces = maxd > 0 ? maxd : 1;
+        a.nobounce = maxd <= 0;
+        for (int b = 0; b < bounces; ++b) {
+            const bool primary = (b == 0);
+            a.last = (b == bounces - 1);
+            if (!a.nobounce) {
+                HIPCHK(ctx, hipMemsetAsync(ctx->defer_count.p, 0, 64, s));
+                e = dcounters ? launch_trace_mode<true>(mode, primary, a, (int)blocks, lds, s)
+                              : launch_trace_mode<false>(mode, primary, a, (int)blocks, lds, s);
+                if (e != hipSuccess) return hip_fail(ctx, e, "ort_trace_kernel launch");
+                if (first_trace) {
+                    HIPCHK(ctx, hipEventRecord(ctx->ev_trace, s));
+                    first_trace = false;
+                }
+                if (mode == 0) {
+                    e = dcounters ? launch_exact<true>(primary, a, exact_blocks, lds, s)
+                                  : launch_exact<false>(primary, a, exact_blocks, lds, s);
+                    if (e != hipSuccess) return hip_fail(ctx, e, "ort_trace_exact launch");
+                }
+            }
+            e = launch_shade(mode, primary, direct, a, (int)blocks, s);
+            if (e != hipSuccess) return hip_fail(ctx, e, "ort_shade_kernel launch");
+        }
     }
-    if (!out_is_device && pix > 0) {
+    if (!direct) {
+        hipLaunchKernelGGL(ort_finalize_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, s, a);
+        if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "ort_finalize_kernel launch");
+    }
+    HIPCHK(ctx, hipEventRecord(ctx->ev1, s));
+    if (first_trace) HIPCHK(ctx, hipEventRecord(ctx->ev_trace, s));
+    ctx->timed = true;
+    if (!out_is_device) {
         HIPCHK(ctx, hipMemcpyAsync(out, dout, 12 * pix, hipMemcpyDeviceToHost, s));
         HIPCHK(ctx, hipStreamSynchronize(s));
     } else if (!stream) {
@@ -368,7 +641,8 @@ int ort_create(int device, ort_ctx** out) {
     if (!c) return fail(nullptr, ORT_ERR_OUT_OF_MEMORY, "ort_create: out of host memory");
     c->device = device;
     if ((e = hipSetDevice(device)) != hipSuccess || (e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess ||
-        (e = hipEventCreate(&c->ev0)) != hipSuccess || (e = hipEventCreate(&c->ev1)) != hipSuccess) {
+        (e = hipEventCreate(&c->ev0)) != hipSuccess || (e = hipEventCreate(&c->ev1)) != hipSuccess ||
+        (e = hipEventCreate(&c->ev_trace)) != hipSuccess) {
         const int rc = hip_fail(nullptr, e, "ort_create");
         delete c;
         return rc;
@@ -384,8 +658,11 @@ int ort_destroy(ort_ctx* ctx) {
     free_scene(ctx);
     free_buf(ctx->scratch_out);
     free_buf(ctx->counters);
+    DevBuf* pipe[] = {&ctx->hit, &ctx->defer_list, &ctx->defer_count, &ctx->po, &ctx->pd, &ctx->pc, &ctx->prng, &ctx->pcol};
+    for (DevBuf* b : pipe) free_buf(*b);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+    if (ctx->ev_trace) (void)hipEventDestroy(ctx->ev_trace);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return ORT_OK;
@@ -477,6 +754,14 @@ int ort_last_kernel_ms(ort_ctx* ctx, float* ms) {
     return ORT_OK;
 }
 
+int ort_last_trace_ms(ort_ctx* ctx, float* ms) {
+    if (!ctx || !ms) return fail(nullptr, ORT_ERR_INVALID_ARG, "ort_last_trace_ms: null argument");
+    if (!ctx->timed) return fail(ctx, ORT_ERR_NO_SCENE, "no kernel launched yet");
+    HIPCHK(ctx, hipEventSynchronize(ctx->ev1));
+    HIPCHK(ctx, hipEventElapsedTime(ms, ctx->ev0, ctx->ev_trace));
+    return ORT_OK;
+}
+
 int ort_count_traffic(ort_ctx* ctx, const ort_params* params, const ort_tile* tile, uint64_t* counts) {
     if (!ctx || !counts) return fail(nullptr, ORT_ERR_INVALID_ARG, "ort_count_traffic: null argument");
     HIPCHK(ctx, hipSetDevice(ctx->device));
@@ -494,6 +779,12 @@ int ort_count_traffic(ort_ctx* ctx, const ort_params* params, const ort_tile* ti
         hipError_t e = hipMemcpy(h, ctx->counters.p, 64, hipMemcpyDeviceToHost);
         if (e != hipSuccess) { free_buf(tmp); return hip_fail(ctx, e, "ort_count_traffic: copy counters"); }
         for (int k = 0; k < ORT_COUNT_N; ++k) counts[k] = h[k];
+        // pixels inside the frame (main() runs once per fragment)
+        const TileMap tm = {tile->x0, tile->width, tile->y0, tile->rows, tile->band_height, tile->band_stride};
+        uint64_t px = 0;
+        for (int j = 0; j < tile->rows; ++j)
+            if (tile_row_to_y(tm, j) < params->height) px += (uint64_t)tile->width;
+        counts[ORT_COUNT_PIXELS] = px;
     }
     free_buf(tmp);
     return rc;

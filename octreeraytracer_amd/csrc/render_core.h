@@ -735,25 +735,75 @@ ORT_FN Ray camera_ray(const KCamera& c, float s, float t, float W, float H, ort_
     return r;
 }
 
-// Intersection dispatch for one ray; fills the hit record like intersectScene (glsl:500-506).
-// MODE: 0 compact octree, 1 explicit octree, 2 brute force.
+// ---------------------------------------------------------------------------------------
+// Path steps.  The GPU runs them as a wavefront pipeline (ort_kernel.hip: trace kernel ->
+// rare exact-walk kernel -> shade kernel, per bounce); shade_pixel below chains the same
+// steps for one pixel (host emulation / reference order).  Both orders give identical
+// pixels because every path is independent and each step is a pure function of its state.
+
+struct PixelParams {
+    KCamera cam;
+    int W, H, ns, maxDepth;
+};
+
+// main() prologue + the sample-s part of its loop up to radiance()'s first line
+// (glsl:640, 647-654, 602): consumes 2 + 4 rand2D, returns the normalised camera ray.
+// st must hold the pixel's RNG state at the start of sample s (FragCoord/iResolution for s=0).
+ORT_FN void pixel_rng_init(const PixelParams& P, int px, int py, ort_rng& st) {
+    st.x = ((float)px + 0.5f) / (float)P.W;
+    st.y = ((float)py + 0.5f) / (float)P.H;
+}
+ORT_FN Ray primary_ray(const PixelParams& P, int px, int py, int s, ort_rng& st) {
+    const float W = (float)P.W, H = (float)P.H;
+    const float fx = (float)px + 0.5f, fy = (float)py + 0.5f;
+    const int sqrt_ns = (int)sqrtf((float)P.ns);
+    const int i = s % sqrt_ns;
+    const int j = s / sqrt_ns;
+    const float u = (fx + ((float)i + ort_rand2D(&st)) / (float)sqrt_ns) / W;
+    const float v = (fy + ((float)j + ort_rand2D(&st)) / (float)sqrt_ns) / H;
+    Ray ray = camera_ray(P.cam, u, v, W, H, st);
+    ray.d = normalize(ray.d);
+    return ray;
+}
+
+#define ORT_TRACE_MISS 0
+#define ORT_TRACE_HIT 1
+#define ORT_TRACE_DEFER 2
+
+// intersectScene(ray, 0.001, MAXFLOAT) (glsl:500-506, 607).  MODE: 0 compact octree,
+// 1 explicit octree, 2 brute force.  With MODE 0 and allow_defer, a ray the fast walk
+// cannot take (some 1/d component not finite) is reported as DEFER instead of walking
+// it exactly here, so the exact walk's registers stay out of the hot kernel.
 template <int MODE, bool COUNT, class Frames>
-ORT_FN bool intersect(const KScene& S, const float* planes, const uint8_t* rank_lut, const Ray& r, HitRec& h,
-                      Frames& fr, int* snode, float* stmin, Counters& cnt) {
-    int entry = -1;
-    float t = 0.0f;
+ORT_FN int trace_ray(const KScene& S, const float* planes, const uint8_t* rank_lut, const Ray& r, bool allow_defer,
+                     float& t, int& entry, Frames& fr, int* snode, float* stmin, Counters& cnt) {
     bool hit;
-    if (COUNT) cnt.v[5] += 1;
+    entry = -1;
+    t = 0.0f;
     if (MODE == 0) {
         const V3 inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
-        if (rank_lut && fast_path_ok(inv))
+        if (rank_lut && fast_path_ok(inv)) {
+            if (COUNT) cnt.v[5] += 1;
             hit = traverse_fast<COUNT>(S, planes, rank_lut, r, inv, 0.001f, ORT_MAXFLOAT, entry, t, fr, cnt);
-        else
+        } else if (allow_defer) {
+            return ORT_TRACE_DEFER;
+        } else {
+            if (COUNT) cnt.v[5] += 1;
             hit = traverse_compact<COUNT>(S, planes, r, 0.001f, ORT_MAXFLOAT, entry, t, fr, cnt);
+        }
+    } else if (MODE == 1) {
+        if (COUNT) cnt.v[5] += 1;
+        hit = traverse_explicit<COUNT>(S, r, 0.001f, ORT_MAXFLOAT, entry, t, snode, stmin, cnt);
+    } else {
+        if (COUNT) cnt.v[5] += 1;
+        hit = traverse_brute<COUNT>(S, r, 0.001f, ORT_MAXFLOAT, entry, t, cnt);
     }
-    else if (MODE == 1) hit = traverse_explicit<COUNT>(S, r, 0.001f, ORT_MAXFLOAT, entry, t, snode, stmin, cnt);
-    else hit = traverse_brute<COUNT>(S, r, 0.001f, ORT_MAXFLOAT, entry, t, cnt);
-    if (!hit) return false;
+    return hit ? ORT_TRACE_HIT : ORT_TRACE_MISS;
+}
+
+// The IntersectInfo Sphere_hit fills for the accepted hit (glsl:240-251).
+template <int MODE>
+ORT_FN HitRec hit_record(const KScene& S, const Ray& r, float t, int entry) {
     int sidx;
     float4 sp;
     if (MODE == 0) {
@@ -766,6 +816,7 @@ ORT_FN bool intersect(const KScene& S, const float* planes, const uint8_t* rank_
         sidx = entry;
         sp = S.sph_cr[sidx];
     }
+    HitRec h;
     h.t = t;
     h.point = mk(r.o.x + t * r.d.x, r.o.y + t * r.d.y, r.o.z + t * r.d.z);
     h.normal = mk((h.point.x - sp.x) / sp.w, (h.point.y - sp.y) / sp.w, (h.point.z - sp.z) / sp.w);
@@ -775,63 +826,63 @@ ORT_FN bool intersect(const KScene& S, const float* planes, const uint8_t* rank_
     h.albedo = mk(ma.y, ma.z, ma.w);
     h.fuzz = fr2.x;
     h.ri = fr2.y;
+    return h;
+}
+
+// One iteration of radiance()'s bounce loop after intersectScene (glsl:607-627).
+// Returns true when the path ends here (absorbed, or escaped to the sky).
+ORT_FN bool shade_bounce(bool hit, const HitRec& h, Ray& ray, V3& c, float& importance, ort_rng& st) {
+    if (hit) {
+        Ray wi;
+        wi.d = ray.d;
+        V3 att = mk(0.0f, 0.0f, 0.0f);
+        const bool scattered = bsdf(h, ray, wi, att, st);
+        ray.o = wi.o;
+        ray.d = wi.d;
+        if (!scattered) {
+            c = mul(c, mk(0.0f, 0.0f, 0.0f));
+            return true;
+        }
+        c = mul(c, att);
+        importance *= ort_maxf(att.x, ort_maxf(att.y, att.z));
+        return false;
+    }
+    c = mul(c, sky_color(ray));
     return true;
 }
 
-struct PixelParams {
-    KCamera cam;
-    int W, H, ns, maxDepth;
-};
-
-// main() of the fragment shader (glsl:636-664) for pixel (px, py), py = 0 the bottom row.
-template <int MODE, bool COUNT, class Frames>
-ORT_FN V3 shade_pixel(const PixelParams& P, const KScene& S, const float* planes, const uint8_t* rank_lut, Frames& fr,
-                      int* snode, float* stmin, int px, int py, Counters& cnt) {
-    const float W = (float)P.W, H = (float)P.H;
-    const float fx = (float)px + 0.5f, fy = (float)py + 0.5f;
-    ort_rng st;
-    st.x = fx / W;
-    st.y = fy / H;
-    V3 col = mk(0.0f, 0.0f, 0.0f);
-    for (int s = 0; s < P.ns; ++s) {
-        const int sqrt_ns = (int)sqrtf((float)P.ns);
-        const int i = s % sqrt_ns;
-        const int j = s / sqrt_ns;
-        const float u = (fx + ((float)i + ort_rand2D(&st)) / (float)sqrt_ns) / W;
-        const float v = (fy + ((float)j + ort_rand2D(&st)) / (float)sqrt_ns) / H;
-        Ray ray = camera_ray(P.cam, u, v, W, H, st);
-        // radiance (glsl:597-633)
-        V3 c = mk(1.0f, 1.0f, 1.0f);
-        float importance = 1.0f;
-        ray.d = normalize(ray.d);
-        for (int b = 0; b < P.maxDepth; ++b) {
-            if (importance < 0.01f) break;
-            HitRec h;
-            if (intersect<MODE, COUNT>(S, planes, rank_lut, ray, h, fr, snode, stmin, cnt)) {
-                Ray wi;
-                wi.d = ray.d;
-                V3 att = mk(0.0f, 0.0f, 0.0f);
-                const bool scattered = bsdf(h, ray, wi, att, st);
-                ray.o = wi.o;
-                ray.d = wi.d;
-                if (scattered) {
-                    c = mul(c, att);
-                } else {
-                    c = mul(c, mk(0.0f, 0.0f, 0.0f));
-                    break;
-                }
-                importance *= ort_maxf(att.x, ort_maxf(att.y, att.z));
-            } else {
-                c = mul(c, sky_color(ray));
-                break;
-            }
-        }
-        col = add(col, c);
-    }
-    const float fns = (float)P.ns;
+// col /= float(numSamples); pow(col, 1/2.2) (glsl:659-661)
+ORT_FN V3 finish_pixel(V3 col, int ns) {
+    const float fns = (float)ns;
     col = mk(col.x / fns, col.y / fns, col.z / fns);
     const float g = 1.0f / 2.2f;
     return mk(ort_powf(col.x, g), ort_powf(col.y, g), ort_powf(col.z, g));
+}
+
+// main() of the fragment shader (glsl:636-664) for pixel (px, py), py = 0 the bottom row,
+// as one sequential chain of the steps above (host emulation).
+template <int MODE, bool COUNT, class Frames>
+ORT_FN V3 shade_pixel(const PixelParams& P, const KScene& S, const float* planes, const uint8_t* rank_lut, Frames& fr,
+                      int* snode, float* stmin, int px, int py, Counters& cnt) {
+    ort_rng st;
+    pixel_rng_init(P, px, py, st);
+    V3 col = mk(0.0f, 0.0f, 0.0f);
+    for (int s = 0; s < P.ns; ++s) {
+        Ray ray = primary_ray(P, px, py, s, st);
+        V3 c = mk(1.0f, 1.0f, 1.0f);
+        float importance = 1.0f;
+        for (int b = 0; b < P.maxDepth; ++b) {
+            if (importance < 0.01f) break;
+            float t;
+            int entry;
+            const int tr = trace_ray<MODE, COUNT>(S, planes, rank_lut, ray, false, t, entry, fr, snode, stmin, cnt);
+            HitRec h;
+            if (tr == ORT_TRACE_HIT) h = hit_record<MODE>(S, ray, t, entry);
+            if (shade_bounce(tr == ORT_TRACE_HIT, h, ray, c, importance, st)) break;
+        }
+        col = add(col, c);
+    }
+    return finish_pixel(col, P.ns);
 }
 
 }  // namespace ort

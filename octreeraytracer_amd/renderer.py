@@ -165,6 +165,12 @@ class Renderer:
         self._check(self._lib.ort_last_kernel_ms(self._ctx, C.byref(ms)))
         return ms.value
 
+    def last_trace_ms(self) -> float:
+        """Start of the last frame to the end of its first trace kernel (the dominant kernel)."""
+        ms = C.c_float()
+        self._check(self._lib.ort_last_trace_ms(self._ctx, C.byref(ms)))
+        return ms.value
+
     def count_traffic(self, params: FrameParams, tile: Tile | None = None) -> dict:
         tile = tile or Tile.full(params)
         p, t = params.to_c(), tile.to_c()
