@@ -42,13 +42,15 @@ struct PipeArgs {
     ort::KScene S;
     TileMap tm;
     int tilesX;
+    int total;        // path slots = workgroups x 256 (tile-block order, some are holes)
     int sample;       // s of main()'s sample loop
     int last;         // this bounce is the last one (b == maxDepth - 1)
     int nobounce;     // maxDepth <= 0: radiance() returns (1,1,1) without tracing
     int exact_only;   // ORT_OPT_EXACT_TRAVERSAL: every compact ray takes the exact walk
-    int2* hit;        // per path: {entry (-1 miss, -2 deferred, -3 outside the frame), t bits}
+    int refill;       // persistent trace: refill a wave when at least this many lanes idle
+    int2* hit;        // per path: {entry (-1 miss), t bits}
     int* defer_list;
-    int* defer_count;
+    int* sync;        // [0] deferred count, [1] work cursor of the persistent trace
     float4* po;       // o.xyz, importance
     float4* pd;       // d.xyz, alive (1/0)
     float4* pc;       // path throughput c.xyz
@@ -103,12 +105,14 @@ __device__ inline LdsView setup_lds(unsigned char* smem, const ort::KScene& S) {
     return v;
 }
 
-// thread -> (col, row) of the tile: 16x16 pixels per workgroup, 8x8 per wave
-__device__ inline void tile_coords(int tilesX, int& col, int& row) {
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int bx = blockIdx.x % tilesX, by = blockIdx.x / tilesX;
+// Path slot k (tile-block order: 256 slots = one 16x16 tile, 64 = one 8x8 wave block)
+// -> tile column/row.  Returns false for slots outside the tile.
+__host__ __device__ inline bool slot_coords(const PipeArgs& A, int k, int& col, int& row) {
+    const int blk = k >> 8, tid = k & 255, wave = tid >> 6, lane = tid & 63;
+    const int bx = blk % A.tilesX, by = blk / A.tilesX;
     col = bx * 16 + (wave & 1) * 8 + (lane & 7);
     row = by * 16 + (wave >> 1) * 8 + (lane >> 3);
+    return col < A.tm.tw && row < A.tm.th;
 }
 
 template <bool COUNT>
@@ -118,140 +122,167 @@ __device__ inline void flush_counts(const ort::Counters& c, unsigned long long* 
             if (c.v[k]) atomicAdd(dst + k, c.v[k]);
 }
 
-__device__ inline ort::Ray load_ray(const PipeArgs& A, int p) {
-    const float4 o = A.po[p], d = A.pd[p];
+__device__ inline ort::Ray load_ray(const PipeArgs& A, int k, bool& alive) {
+    const float4 o = A.po[k], d = A.pd[k];
     ort::Ray r;
     r.o = ort::mk(o.x, o.y, o.z);
     r.d = ort::mk(d.x, d.y, d.z);
+    alive = d.w != 0.0f;
     return r;
 }
 
-__device__ inline ort_rng start_rng(const PipeArgs& A, int p, int px, int py) {
+// Sample-s camera rays (main() up to radiance()'s first line): path state for bounce 0.
+__global__ void __launch_bounds__(kBlock) ort_raygen_kernel(PipeArgs A) {
+    const int k = blockIdx.x * kBlock + threadIdx.x;
+    int col, row;
+    const bool in = slot_coords(A, k, col, row);
+    const int y = in ? tile_row_to_y(A.tm, row) : 0;
+    if (!in || y >= A.pp.H) {
+        A.pd[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // hole
+        return;
+    }
     ort_rng st;
     if (A.sample == 0) {
-        ort::pixel_rng_init(A.pp, px, py, st);
+        ort::pixel_rng_init(A.pp, A.tm.x0 + col, y, st);
     } else {
-        const float2 v = A.prng[p];
+        const float2 v = A.prng[k];
         st.x = v.x;
         st.y = v.y;
     }
-    return st;
+    const ort::Ray ray = ort::primary_ray(A.pp, A.tm.x0 + col, y, A.sample, st);
+    A.po[k] = make_float4(ray.o.x, ray.o.y, ray.o.z, 1.0f);
+    A.pd[k] = make_float4(ray.d.x, ray.d.y, ray.d.z, 1.0f);
+    A.prng[k] = make_float2(st.x, st.y);
 }
 
-// Bounce-b trace.  PRIMARY: the camera ray of sample A.sample is generated here.
-template <int MODE, bool COUNT, bool PRIMARY>
-__global__ void __launch_bounds__(kBlock) ort_trace_kernel(PipeArgs A) {
+// Persistent trace over the compact layout: every lane keeps one ray's FastState and,
+// when it finishes, takes the next path slot from a global cursor (wave-aggregated
+// atomic), so the wave stays full until the queue drains.  Rays the fast walk cannot
+// take are appended to the defer list for ort_trace_exact.
+template <bool COUNT>
+__global__ void __launch_bounds__(kBlock) ort_trace_persistent(PipeArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    LdsView L;
-    L.planes = nullptr;
-    L.lut = nullptr;
-    if constexpr (MODE == 0) L = setup_lds<true>(smem, A.S);
-    int col, row;
-    tile_coords(A.tilesX, col, row);
-    if (col >= A.tm.tw || row >= A.tm.th) return;
-    const int p = row * A.tm.tw + col;
-    const int y = tile_row_to_y(A.tm, row);
-    if (y >= A.pp.H) {
-        A.hit[p] = make_int2(-3, 0);
-        return;
-    }
-    ort::Ray ray;
-    if constexpr (PRIMARY) {
-        ort_rng st = start_rng(A, p, A.tm.x0 + col, y);
-        ray = ort::primary_ray(A.pp, A.tm.x0 + col, y, A.sample, st);
-    } else {
-        if (A.pd[p].w == 0.0f) return;
-        ray = load_ray(A, p);
-    }
+    LdsView L = setup_lds<true>(smem, A.S);
+    const uint8_t* lut = L.lut;
     ort::Counters cnt;
-    for (int k = 0; k < 6; ++k) cnt.v[k] = 0;
+    for (int q = 0; q < 6; ++q) cnt.v[q] = 0;
+    ort::FastState st;
+    int k = -1;
+    bool drained = false;  // wave-uniform: the cursor passed A.total
+    for (;;) {
+        const unsigned long long idle = __ballot(k < 0);
+        if (idle == __ballot(true)) {
+            if (drained) break;
+        }
+        if (!drained && (unsigned)__popcll(idle) >= (unsigned)A.refill) {
+            if (k < 0) {
+                const int cand = atomicAdd(A.sync + 1, 1);
+                if (cand < A.total) {
+                    bool alive;
+                    const ort::Ray ray = load_ray(A, cand, alive);
+                    if (alive) {
+                        const ort::V3 inv = ort::mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
+                        if (A.exact_only || !ort::fast_path_ok(inv)) {
+                            A.defer_list[atomicAdd(A.sync, 1)] = cand;
+                        } else {
+                            if (COUNT) cnt.v[5] += 1;
+                            if (ort::fast_begin(A.S, L.planes, ray, inv, 0.001f, ORT_MAXFLOAT, st)) k = cand;
+                            else A.hit[cand] = make_int2(-1, 0);
+                        }
+                    }
+                }
+            }
+            // uniform: once any lane saw the end of the queue, later fetches are all past it
+            drained = __ballot(__hip_atomic_load(A.sync + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= A.total) != 0;
+            continue;
+        }
+        if (k >= 0) {
+            if (ort::fast_step<COUNT>(A.S, L.planes, lut, st, L.fr, cnt)) {
+                A.hit[k] = make_int2(st.hit ? st.hitEntry : -1, __float_as_int(st.closest));
+                k = -1;
+            }
+        }
+    }
+    flush_counts<COUNT>(cnt, A.counters);
+}
+
+// One-ray-per-lane trace for the explicit layout (MODE 1) and brute force (MODE 2).
+template <int MODE, bool COUNT>
+__global__ void __launch_bounds__(kBlock) ort_trace_kernel(PipeArgs A) {
+    const int k = blockIdx.x * kBlock + threadIdx.x;
+    bool alive;
+    const ort::Ray ray = load_ray(A, k, alive);
+    if (!alive) return;
+    ort::Counters cnt;
+    for (int q = 0; q < 6; ++q) cnt.v[q] = 0;
+    ort::LocalFrames unused;
     float t;
     int entry;
     int st;
     if constexpr (MODE == 1) {
         int snode[ORT_MAX_STACK];
         float stmin[ORT_MAX_STACK];
-        st = ort::trace_ray<MODE, COUNT>(A.S, L.planes, L.lut, ray, false, t, entry, L.fr, snode, stmin, cnt);
+        st = ort::trace_ray<MODE, COUNT>(A.S, nullptr, nullptr, ray, false, t, entry, unused, snode, stmin, cnt);
     } else {
-        const uint8_t* lut = A.exact_only ? nullptr : L.lut;
-        st = ort::trace_ray<MODE, COUNT>(A.S, L.planes, lut, ray, MODE == 0, t, entry, L.fr, nullptr, nullptr, cnt);
+        st = ort::trace_ray<MODE, COUNT>(A.S, nullptr, nullptr, ray, false, t, entry, unused, nullptr, nullptr, cnt);
     }
-    if (st == ORT_TRACE_DEFER) {
-        const int k = atomicAdd(A.defer_count, 1);
-        A.defer_list[k] = p;
-        A.hit[p] = make_int2(-2, 0);
-    } else {
-        A.hit[p] = make_int2(st == ORT_TRACE_HIT ? entry : -1, __float_as_int(t));
-    }
+    A.hit[k] = make_int2(st == ORT_TRACE_HIT ? entry : -1, __float_as_int(t));
     flush_counts<COUNT>(cnt, A.counters);
 }
 
-// Exact compact walk (traverse_compact) for the deferred rays; persistent grid.
-template <bool COUNT, bool PRIMARY>
+// Exact compact walk (traverse_compact) for the deferred rays; grid-stride loop.
+template <bool COUNT>
 __global__ void __launch_bounds__(kBlock) ort_trace_exact(PipeArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     LdsView L = setup_lds<false>(smem, A.S);
-    const int n = *A.defer_count;
+    const int n = *A.sync;
     ort::Counters cnt;
-    for (int k = 0; k < 6; ++k) cnt.v[k] = 0;
+    for (int q = 0; q < 6; ++q) cnt.v[q] = 0;
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
-        const int p = A.defer_list[i];
-        const int row = p / A.tm.tw, col = p - row * A.tm.tw;
-        const int y = tile_row_to_y(A.tm, row);
-        ort::Ray ray;
-        if constexpr (PRIMARY) {
-            ort_rng st = start_rng(A, p, A.tm.x0 + col, y);
-            ray = ort::primary_ray(A.pp, A.tm.x0 + col, y, A.sample, st);
-        } else {
-            ray = load_ray(A, p);
-        }
+        const int k = A.defer_list[i];
+        bool alive;
+        const ort::Ray ray = load_ray(A, k, alive);
         float t;
         int entry;
         const int st = ort::trace_ray<0, COUNT>(A.S, L.planes, nullptr, ray, false, t, entry, L.fr, nullptr, nullptr, cnt);
-        A.hit[p] = make_int2(st == ORT_TRACE_HIT ? entry : -1, __float_as_int(t));
+        A.hit[k] = make_int2(st == ORT_TRACE_HIT ? entry : -1, __float_as_int(t));
     }
     flush_counts<COUNT>(cnt, A.counters);
 }
 
-// Bounce-b shading.  DIRECT (1 sample, 1 bounce): writes the final pixel.
-template <int MODE, bool PRIMARY, bool DIRECT>
+// Bounce shading (glsl:607-627).  FIRST: bounce 0 (c = 1, importance = 1).
+// DIRECT (1 sample, 1 bounce): writes the final pixel.
+template <int MODE, bool FIRST, bool DIRECT>
 __global__ void __launch_bounds__(kBlock) ort_shade_kernel(PipeArgs A) {
+    const int k = blockIdx.x * kBlock + threadIdx.x;
     int col, row;
-    tile_coords(A.tilesX, col, row);
-    if (col >= A.tm.tw || row >= A.tm.th) return;
-    const int p = row * A.tm.tw + col;
+    if (!slot_coords(A, k, col, row)) return;
     const int y = tile_row_to_y(A.tm, row);
+    const size_t p = (size_t)row * A.tm.tw + col;
     if (y >= A.pp.H) {
         if (DIRECT) {
-            float* o = A.out + 3 * (size_t)p;
+            float* o = A.out + 3 * p;
             o[0] = 0.0f; o[1] = 0.0f; o[2] = 0.0f;
         }
         return;
     }
-    ort::Ray ray;
+    bool alive;
+    ort::Ray ray = load_ray(A, k, alive);
+    if (!alive) return;
+    const float2 r2 = A.prng[k];
     ort_rng st;
-    ort::V3 c;
-    float importance;
-    if constexpr (PRIMARY) {
-        st = start_rng(A, p, A.tm.x0 + col, y);
-        ray = ort::primary_ray(A.pp, A.tm.x0 + col, y, A.sample, st);
-        c = ort::mk(1.0f, 1.0f, 1.0f);
-        importance = 1.0f;
-    } else {
-        const float4 d = A.pd[p];
-        if (d.w == 0.0f) return;
-        const float4 o = A.po[p], cc = A.pc[p];
-        const float2 r2 = A.prng[p];
-        ray.o = ort::mk(o.x, o.y, o.z);
-        ray.d = ort::mk(d.x, d.y, d.z);
-        importance = o.w;
+    st.x = r2.x;
+    st.y = r2.y;
+    ort::V3 c = ort::mk(1.0f, 1.0f, 1.0f);
+    float importance = 1.0f;
+    if (!FIRST) {
+        const float4 cc = A.pc[k];
         c = ort::mk(cc.x, cc.y, cc.z);
-        st.x = r2.x;
-        st.y = r2.y;
+        importance = A.po[k].w;
     }
     bool done = true;
     if (!A.nobounce) {
-        const int2 h = A.hit[p];
+        const int2 h = A.hit[k];
         ort::HitRec rec;
         if (h.x >= 0) rec = ort::hit_record<MODE>(A.S, ray, __int_as_float(h.y), h.x);
         done = ort::shade_bounce(h.x >= 0, rec, ray, c, importance, st);
@@ -259,41 +290,41 @@ __global__ void __launch_bounds__(kBlock) ort_shade_kernel(PipeArgs A) {
     }
     if constexpr (DIRECT) {
         const ort::V3 v = ort::finish_pixel(ort::add(ort::mk(0.0f, 0.0f, 0.0f), c), 1);
-        float* o = A.out + 3 * (size_t)p;
+        float* o = A.out + 3 * p;
         o[0] = v.x; o[1] = v.y; o[2] = v.z;
     } else {
         if (done) {
             ort::V3 acc = ort::mk(0.0f, 0.0f, 0.0f);
             if (A.sample > 0) {
-                const float4 a = A.pcol[p];
+                const float4 a = A.pcol[k];
                 acc = ort::mk(a.x, a.y, a.z);
             }
             acc = ort::add(acc, c);
-            A.pcol[p] = make_float4(acc.x, acc.y, acc.z, 0.0f);
-            A.pd[p] = make_float4(ray.d.x, ray.d.y, ray.d.z, 0.0f);
+            A.pcol[k] = make_float4(acc.x, acc.y, acc.z, 0.0f);
+            A.pd[k] = make_float4(ray.d.x, ray.d.y, ray.d.z, 0.0f);
         } else {
-            A.po[p] = make_float4(ray.o.x, ray.o.y, ray.o.z, importance);
-            A.pd[p] = make_float4(ray.d.x, ray.d.y, ray.d.z, 1.0f);
-            A.pc[p] = make_float4(c.x, c.y, c.z, 0.0f);
+            A.po[k] = make_float4(ray.o.x, ray.o.y, ray.o.z, importance);
+            A.pd[k] = make_float4(ray.d.x, ray.d.y, ray.d.z, 1.0f);
+            A.pc[k] = make_float4(c.x, c.y, c.z, 0.0f);
         }
-        A.prng[p] = make_float2(st.x, st.y);
+        A.prng[k] = make_float2(st.x, st.y);
     }
 }
 
+// col / ns, gamma (glsl:659-661) for the multi-sample / multi-bounce case.
 __global__ void __launch_bounds__(kBlock) ort_finalize_kernel(PipeArgs A) {
+    const int k = blockIdx.x * kBlock + threadIdx.x;
     int col, row;
-    tile_coords(A.tilesX, col, row);
-    if (col >= A.tm.tw || row >= A.tm.th) return;
-    const int p = row * A.tm.tw + col;
+    if (!slot_coords(A, k, col, row)) return;
     const int y = tile_row_to_y(A.tm, row);
-    float* o = A.out + 3 * (size_t)p;
+    float* o = A.out + 3 * ((size_t)row * A.tm.tw + col);
     if (y >= A.pp.H) {
         o[0] = 0.0f; o[1] = 0.0f; o[2] = 0.0f;
         return;
     }
     ort::V3 acc = ort::mk(0.0f, 0.0f, 0.0f);
     if (A.pp.ns > 0) {
-        const float4 a = A.pcol[p];
+        const float4 a = A.pcol[k];
         acc = ort::mk(a.x, a.y, a.z);
     }
     const ort::V3 v = ort::finish_pixel(acc, A.pp.ns);
@@ -315,6 +346,7 @@ struct ort_ctx {
     std::string err;
     int force_layout = -1;
     int exact_only = 0;
+    int refill = 16;
     bool has_scene = false;
     int layout = ORT_LAYOUT_EXPLICIT;
     int depth = 0;
@@ -492,39 +524,39 @@ int ensure(ort_ctx* ctx, DevBuf& b, size_t bytes) {
     return ORT_OK;
 }
 
-template <int MODE, bool COUNT>
-hipError_t launch_trace(bool primary, const PipeArgs& a, int blocks, size_t lds, hipStream_t s) {
-    if (primary) hipLaunchKernelGGL((ort_trace_kernel<MODE, COUNT, true>), dim3(blocks), dim3(kBlock), lds, s, a);
-    else hipLaunchKernelGGL((ort_trace_kernel<MODE, COUNT, false>), dim3(blocks), dim3(kBlock), lds, s, a);
-    return hipGetLastError();
-}
-
 template <bool COUNT>
-hipError_t launch_trace_mode(int mode, bool primary, const PipeArgs& a, int blocks, size_t lds, hipStream_t s) {
-    if (mode == 0) return launch_trace<0, COUNT>(primary, a, blocks, lds, s);
-    if (mode == 1) return launch_trace<1, COUNT>(primary, a, blocks, lds, s);
-    return launch_trace<2, COUNT>(primary, a, blocks, lds, s);
-}
-
-template <bool COUNT>
-hipError_t launch_exact(bool primary, const PipeArgs& a, int blocks, size_t lds, hipStream_t s) {
-    if (primary) hipLaunchKernelGGL((ort_trace_exact<COUNT, true>), dim3(blocks), dim3(kBlock), lds, s, a);
-    else hipLaunchKernelGGL((ort_trace_exact<COUNT, false>), dim3(blocks), dim3(kBlock), lds, s, a);
+hipError_t launch_trace(int mode, const PipeArgs& a, int blocks, int pblocks, size_t lds, hipStream_t s) {
+    if (mode == 0) hipLaunchKernelGGL((ort_trace_persistent<COUNT>), dim3(pblocks), dim3(kBlock), lds, s, a);
+    else if (mode == 1) hipLaunchKernelGGL((ort_trace_kernel<1, COUNT>), dim3(blocks), dim3(kBlock), 0, s, a);
+    else hipLaunchKernelGGL((ort_trace_kernel<2, COUNT>), dim3(blocks), dim3(kBlock), 0, s, a);
     return hipGetLastError();
 }
 
 template <int MODE>
-hipError_t launch_shade_mode(bool primary, bool direct, const PipeArgs& a, int blocks, hipStream_t s) {
+hipError_t launch_shade_mode(bool first, bool direct, const PipeArgs& a, int blocks, hipStream_t s) {
     if (direct) hipLaunchKernelGGL((ort_shade_kernel<MODE, true, true>), dim3(blocks), dim3(kBlock), 0, s, a);
-    else if (primary) hipLaunchKernelGGL((ort_shade_kernel<MODE, true, false>), dim3(blocks), dim3(kBlock), 0, s, a);
+    else if (first) hipLaunchKernelGGL((ort_shade_kernel<MODE, true, false>), dim3(blocks), dim3(kBlock), 0, s, a);
     else hipLaunchKernelGGL((ort_shade_kernel<MODE, false, false>), dim3(blocks), dim3(kBlock), 0, s, a);
     return hipGetLastError();
 }
 
-hipError_t launch_shade(int mode, bool primary, bool direct, const PipeArgs& a, int blocks, hipStream_t s) {
-    if (mode == 0) return launch_shade_mode<0>(primary, direct, a, blocks, s);
-    if (mode == 1) return launch_shade_mode<1>(primary, direct, a, blocks, s);
-    return launch_shade_mode<2>(primary, direct, a, blocks, s);
+hipError_t launch_shade(int mode, bool first, bool direct, const PipeArgs& a, int blocks, hipStream_t s) {
+    if (mode == 0) return launch_shade_mode<0>(first, direct, a, blocks, s);
+    if (mode == 1) return launch_shade_mode<1>(first, direct, a, blocks, s);
+    return launch_shade_mode<2>(first, direct, a, blocks, s);
+}
+
+// Resident workgroups of the persistent trace kernel (a plain launch: extra groups just
+// start when others finish; no grid-wide synchronisation depends on residency).
+int persistent_blocks(int device, bool count, size_t lds, long long needed) {
+    int per_cu = 0, cus = 0;
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+    if (count)
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ort_trace_persistent<true>, kBlock, lds);
+    else
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ort_trace_persistent<false>, kBlock, lds);
+    long long b = (long long)std::max(per_cu, 1) * std::max(cus, 1);
+    return (int)std::max(1LL, std::min(b, needed));
 }
 
 int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out, int out_is_device,
@@ -537,7 +569,10 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     const size_t pix = (size_t)t->width * (size_t)t->rows;
     if (!out && pix > 0) return fail(ctx, ORT_ERR_INVALID_ARG, "ort_render: null output");
     if (pix == 0) return ORT_OK;
-    if (pix > 0x7fffffffULL) return fail(ctx, ORT_ERR_INVALID_ARG, "ort_render: tile too large");
+    const int tilesX = (t->width + 15) / 16, tilesY = (t->rows + 15) / 16;
+    const long long blocks = (long long)tilesX * tilesY;
+    if (blocks * kBlock > 0x7fffffffLL) return fail(ctx, ORT_ERR_INVALID_ARG, "ort_render: tile too large");
+    const size_t slots = (size_t)blocks * kBlock;
     HIPCHK(ctx, hipSetDevice(ctx->device));
     hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
     float* dout = out;
@@ -548,25 +583,25 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     }
     const int ns = p->num_samples, maxd = p->max_depth;
     const bool direct = (ns == 1 && maxd == 1);
-    if ((rc = ensure(ctx, ctx->hit, 8 * pix)) || (rc = ensure(ctx, ctx->defer_list, 4 * pix)) ||
-        (rc = ensure(ctx, ctx->defer_count, 64)))
+    if ((rc = ensure(ctx, ctx->hit, 8 * slots)) || (rc = ensure(ctx, ctx->defer_list, 4 * slots)) ||
+        (rc = ensure(ctx, ctx->defer_count, 64)) || (rc = ensure(ctx, ctx->po, 16 * slots)) ||
+        (rc = ensure(ctx, ctx->pd, 16 * slots)) || (rc = ensure(ctx, ctx->prng, 8 * slots)))
         return rc;
     if (!direct) {
-        if ((rc = ensure(ctx, ctx->po, 16 * pix)) || (rc = ensure(ctx, ctx->pd, 16 * pix)) ||
-            (rc = ensure(ctx, ctx->pc, 16 * pix)) || (rc = ensure(ctx, ctx->prng, 8 * pix)) ||
-            (rc = ensure(ctx, ctx->pcol, 16 * pix)))
-            return rc;
+        if ((rc = ensure(ctx, ctx->pc, 16 * slots)) || (rc = ensure(ctx, ctx->pcol, 16 * slots))) return rc;
     }
     PipeArgs a;
     std::memset(&a, 0, sizeof(a));
     a.pp = pixel_params(p);
     a.S = device_scene(ctx);
     a.tm = {t->x0, t->width, t->y0, t->rows, t->band_height, t->band_stride};
-    a.tilesX = (t->width + 15) / 16;
+    a.tilesX = tilesX;
+    a.total = (int)slots;
     a.exact_only = ctx->exact_only;
+    a.refill = ctx->refill;
     a.hit = (int2*)ctx->hit.p;
     a.defer_list = (int*)ctx->defer_list.p;
-    a.defer_count = (int*)ctx->defer_count.p;
+    a.sync = (int*)ctx->defer_count.p;
     a.po = (float4*)ctx->po.p;
     a.pd = (float4*)ctx->pd.p;
     a.pc = (float4*)ctx->pc.p;
@@ -574,37 +609,36 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     a.pcol = (float4*)ctx->pcol.p;
     a.out = dout;
     a.counters = dcounters;
-    const int tilesY = (t->rows + 15) / 16;
-    const long long blocks = (long long)a.tilesX * tilesY;
-    if (blocks > 0x7fffffffLL) return fail(ctx, ORT_ERR_INVALID_ARG, "ort_render: tile too large");
     const size_t lds = lds_bytes(mode, ctx->depth);
-    const int exact_blocks = 1024;  // persistent grid for the deferred rays (4 per CU)
+    const int pblocks = mode == 0 ? persistent_blocks(ctx->device, dcounters != nullptr, lds, blocks) : 0;
+    const int exact_blocks = 1024;
     hipError_t e;
     HIPCHK(ctx, hipEventRecord(ctx->ev0, s));
     bool first_trace = true;
     for (int smp = 0; smp < ns; ++smp) {
         a.sample = smp;
+        hipLaunchKernelGGL(ort_raygen_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, s, a);
+        if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "ort_raygen_kernel launch");
         const int bounces = maxd > 0 ? maxd : 1;
         a.nobounce = maxd <= 0;
         for (int b = 0; b < bounces; ++b) {
-            const bool primary = (b == 0);
             a.last = (b == bounces - 1);
             if (!a.nobounce) {
                 HIPCHK(ctx, hipMemsetAsync(ctx->defer_count.p, 0, 64, s));
-                e = dcounters ? launch_trace_mode<true>(mode, primary, a, (int)blocks, lds, s)
-                              : launch_trace_mode<false>(mode, primary, a, (int)blocks, lds, s);
-                if (e != hipSuccess) return hip_fail(ctx, e, "ort_trace_kernel launch");
+                e = dcounters ? launch_trace<true>(mode, a, (int)blocks, pblocks, lds, s)
+                              : launch_trace<false>(mode, a, (int)blocks, pblocks, lds, s);
+                if (e != hipSuccess) return hip_fail(ctx, e, "trace kernel launch");
                 if (first_trace) {
                     HIPCHK(ctx, hipEventRecord(ctx->ev_trace, s));
                     first_trace = false;
                 }
                 if (mode == 0) {
-                    e = dcounters ? launch_exact<true>(primary, a, exact_blocks, lds, s)
-                                  : launch_exact<false>(primary, a, exact_blocks, lds, s);
-                    if (e != hipSuccess) return hip_fail(ctx, e, "ort_trace_exact launch");
+                    if (dcounters) hipLaunchKernelGGL((ort_trace_exact<true>), dim3(exact_blocks), dim3(kBlock), lds, s, a);
+                    else hipLaunchKernelGGL((ort_trace_exact<false>), dim3(exact_blocks), dim3(kBlock), lds, s, a);
+                    if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "ort_trace_exact launch");
                 }
             }
-            e = launch_shade(mode, primary, direct, a, (int)blocks, s);
+            e = launch_shade(mode, b == 0, direct, a, (int)blocks, s);
             if (e != hipSuccess) return hip_fail(ctx, e, "ort_shade_kernel launch");
         }
     }
@@ -675,6 +709,11 @@ int ort_set_option(ort_ctx* ctx, int option, int value) {
     if (option == ORT_OPT_FORCE_LAYOUT) {
         if (value < -1 || value > ORT_LAYOUT_EXPLICIT) return fail(ctx, ORT_ERR_INVALID_ARG, "bad layout");
         ctx->force_layout = value;
+        return ORT_OK;
+    }
+    if (option == ORT_OPT_REFILL) {
+        if (value < 1 || value > 64) return fail(ctx, ORT_ERR_INVALID_ARG, "refill must be 1..64");
+        ctx->refill = value;
         return ORT_OK;
     }
     if (option == ORT_OPT_EXACT_TRAVERSAL) {

@@ -374,135 +374,186 @@ ORT_FN bool fast_path_ok(V3 inv) {
 ORT_FN float fmax3(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
 ORT_FN float fmin3(float a, float b, float c) { return fminf(fminf(a, b), c); }
 
-template <bool COUNT, class Frames>
-ORT_FN bool traverse_fast(const KScene& S, const float* planes, const uint8_t* rank_lut, const Ray& r, V3 inv,
-                          float t_min, float t_max, int& hitEntry, float& hitT, Frames& fr, Counters& cnt) {
+// Resumable per-lane state of the fast walk (so a persistent kernel can interleave rays).
+struct FastState {
+    Ray r;           // original-axis ray (Sphere_hit uses it as is)
+    float a;         // dot(d, d)
+    float oA, oB, oC, iA, iB, iC;  // role-axis origin / 1/d
+    float tNA, tFA, tNB, tFB, tNC, tFC;  // near/far plane t of the current node's box
+    uint32_t cA, cB, cC;  // cell of the current node (original-axis cell indices)
+    uint32_t flags;  // bit0 gA, bit1 gB, bit2 gC (axis points negative); bits 4-6 m; bit 8 swap
+    int node, depth;
+    float ntmin, closest;
+    int hitEntry;
+    bool hit;
+    LevelMasks masks;
+};
+
+// Root test and state setup (glsl:296-311).  Returns false when the root box is missed.
+ORT_FN bool fast_begin(const KScene& S, const float* planes, const Ray& r, V3 inv, float t_min, float t_max,
+                       FastState& st) {
     const int D = S.depth;
     const int P1 = (1 << D) + 1;
     const uint32_t nx = r.d.x < 0.0f, ny = r.d.y < 0.0f, nz = r.d.z < 0.0f;
     const uint32_t m = (nz << 2) | (nx << 1) | ny;
     const bool swap = nx != 0;
-    // role axes: A <- x (y if swapped), B <- y (x if swapped), C <- z
     const float* PA = planes + (swap ? P1 : 0);
     const float* PB = planes + (swap ? 0 : P1);
     const float* PC = planes + 2 * P1;
-    const float oA = swap ? r.o.y : r.o.x, oB = swap ? r.o.x : r.o.y, oC = r.o.z;
-    const float iA = swap ? inv.y : inv.x, iB = swap ? inv.x : inv.y, iC = inv.z;
-    const uint32_t gA = swap ? ny : nx, gB = swap ? nx : ny, gC = nz;  // axis points negative
-    const float a = dot(r.d, r.d);
+    st.r = r;
+    st.a = dot(r.d, r.d);
+    st.oA = swap ? r.o.y : r.o.x;
+    st.oB = swap ? r.o.x : r.o.y;
+    st.oC = r.o.z;
+    st.iA = swap ? inv.y : inv.x;
+    st.iB = swap ? inv.x : inv.y;
+    st.iC = inv.z;
+    const uint32_t gA = swap ? ny : nx, gB = swap ? nx : ny, gC = nz;
+    st.flags = gA | (gB << 1) | (gC << 2) | (m << 4) | ((uint32_t)swap << 8);
     const int top = 1 << D;
-    // root box (glsl:304-311): near/far planes per axis
-    float tNA = iA * ((gA ? PA[top] : PA[0]) - oA), tFA = iA * ((gA ? PA[0] : PA[top]) - oA);
-    float tNB = iB * ((gB ? PB[top] : PB[0]) - oB), tFB = iB * ((gB ? PB[0] : PB[top]) - oB);
-    float tNC = iC * ((gC ? PC[top] : PC[0]) - oC), tFC = iC * ((gC ? PC[0] : PC[top]) - oC);
-    if (!(fmin3(tFA, tFB, tFC) >= fmax3(tNA, tNB, tNC))) return false;
-    int node = 0, depth = 0;
-    uint32_t cA = 0, cB = 0, cC = 0;
-    float ntmin = t_min;
-    float closest = t_max;
-    bool hit = false;
-    LevelMasks masks;
-    masks.clear();
-    for (;;) {
-        const uint2 rec = S.node[node];
-        if (COUNT) cnt.v[0] += 1;
-        if (rec.y & ORT_INTERNAL_FLAG) {
-            const int co = (int)rec.x;
-            if (COUNT) {
-                const long long rem = (long long)S.n_nodes - (long long)co;
-                cnt.v[1] += (unsigned long long)(rem >= 8 ? 8 : (rem > 0 ? rem : 0));
-            }
-            const uint32_t rcm = rank_lut[m * 256u + (rec.y & 0xffu)];
-            const int s = D - depth;
-            const float tMA = iA * (PA[(2 * cA + 1) << (s - 1)] - oA);
-            const float tMB = iB * (PB[(2 * cB + 1) << (s - 1)] - oB);
-            const float tMC = iC * (PC[(2 * cC + 1) << (s - 1)] - oC);
-            // entry: near child (rank bit 0) enters at tN, far child at tM; exit: tM / tF
-            const float e00 = fmaxf(tNA, tNB), e01 = fmaxf(tNA, tMB), e10 = fmaxf(tMA, tNB), e11 = fmaxf(tMA, tMB);
-            const float x00 = fminf(tMA, tMB), x01 = fminf(tMA, tFB), x10 = fminf(tFA, tMB), x11 = fminf(tFA, tFB);
-            const float cN = fminf(tMC, ORT_MAXFLOAT), cF = fminf(tFC, ORT_MAXFLOAT);
-            uint32_t rm = 0;
-            // rank r: A = bit1, B = bit0, C = bit2
-#define ORT_CHILD(R, EAB, XAB, EC, XC)                              \
-    {                                                               \
-        const float mm = fmax3(EAB, EC, ntmin);                     \
-        const float xx = fmin3(XAB, XC, ORT_MAXFLOAT);              \
-        rm |= (xx >= mm) ? (1u << (R)) : 0u;                        \
-    }
-            ORT_CHILD(0, e00, x00, tNC, cN)
-            ORT_CHILD(1, e01, x01, tNC, cN)
-            ORT_CHILD(2, e10, x10, tNC, cN)
-            ORT_CHILD(3, e11, x11, tNC, cN)
-            ORT_CHILD(4, e00, x00, tMC, cF)
-            ORT_CHILD(5, e01, x01, tMC, cF)
-            ORT_CHILD(6, e10, x10, tMC, cF)
-            ORT_CHILD(7, e11, x11, tMC, cF)
-#undef ORT_CHILD
-            rm &= rcm;
-            if (rm) {
-                const int rk = __builtin_ctz(rm);
-                const uint32_t rest = rm & (rm - 1u);
-                if (rest) {
-                    masks.put(depth, rest);
-                    fr.set(depth, co, ntmin);
-                }
-                const uint32_t bA = (rk >> 1) & 1u, bB = rk & 1u, bC = (rk >> 2) & 1u;
-                const float eA = bA ? tMA : tNA, eB = bB ? tMB : tNB, eC = bC ? tMC : tNC;
-                ntmin = fmax3(fmaxf(eA, eB), eC, ntmin);
-                tFA = bA ? tFA : tMA;
-                tNA = eA;
-                tFB = bB ? tFB : tMB;
-                tNB = eB;
-                tFC = bC ? tFC : tMC;
-                tNC = eC;
-                cA = 2 * cA + (bA ^ gA);
-                cB = 2 * cB + (bB ^ gB);
-                cC = 2 * cC + (bC ^ gC);
-                node = co + (int)rank_perm((uint32_t)rk, m);
-                depth += 1;
-                continue;
-            }
-        } else {
-            const int off = (int)rec.x;
-            const int n = (int)rec.y;
-            for (int i = 0; i < n; ++i) {
-                const float4 sp = S.leaf_sph[off + i];
-                if (COUNT) cnt.v[2] += 1;
-                float t;
-                if (sphere_hit_t(r, a, sp, ntmin, closest, t)) {
-                    hit = true;
-                    closest = t;
-                    hitEntry = off + i;
-                    if (COUNT) cnt.v[3] += 1;
-                }
-            }
-            if (hit) break;
+    st.tNA = st.iA * ((gA ? PA[top] : PA[0]) - st.oA);
+    st.tFA = st.iA * ((gA ? PA[0] : PA[top]) - st.oA);
+    st.tNB = st.iB * ((gB ? PB[top] : PB[0]) - st.oB);
+    st.tFB = st.iB * ((gB ? PB[0] : PB[top]) - st.oB);
+    st.tNC = st.iC * ((gC ? PC[top] : PC[0]) - st.oC);
+    st.tFC = st.iC * ((gC ? PC[0] : PC[top]) - st.oC);
+    st.node = 0;
+    st.depth = 0;
+    st.cA = st.cB = st.cC = 0;
+    st.ntmin = t_min;
+    st.closest = t_max;
+    st.hitEntry = -1;
+    st.hit = false;
+    st.masks.clear();
+    return fmin3(st.tFA, st.tFB, st.tFC) >= fmax3(st.tNA, st.tNB, st.tNC);
+}
+
+// One node of the walk: visit st.node, then descend or backtrack to the next node.
+// Returns true when the walk is over (hit found, or stack exhausted).
+template <bool COUNT, class Frames>
+ORT_FN bool fast_step(const KScene& S, const float* planes, const uint8_t* rank_lut, FastState& st, Frames& fr,
+                      Counters& cnt) {
+    const int D = S.depth;
+    const int P1 = (1 << D) + 1;
+    const uint32_t gA = st.flags & 1u, gB = (st.flags >> 1) & 1u, gC = (st.flags >> 2) & 1u;
+    const uint32_t m = (st.flags >> 4) & 7u;
+    const bool swap = (st.flags >> 8) & 1u;
+    const float* PA = planes + (swap ? P1 : 0);
+    const float* PB = planes + (swap ? 0 : P1);
+    const float* PC = planes + 2 * P1;
+    const uint2 rec = S.node[st.node];
+    if (COUNT) cnt.v[0] += 1;
+    if (rec.y & ORT_INTERNAL_FLAG) {
+        const int co = (int)rec.x;
+        if (COUNT) {
+            const long long rem = (long long)S.n_nodes - (long long)co;
+            cnt.v[1] += (unsigned long long)(rem >= 8 ? 8 : (rem > 0 ? rem : 0));
         }
-        // backtrack: next child of the deepest level with one left
-        const int L = masks.top();
-        if (L < 0) break;
-        const int rk = masks.pop(L);
-        const int sh = depth - L;
-        const uint32_t bA = (rk >> 1) & 1u, bB = rk & 1u, bC = (rk >> 2) & 1u;
-        cA = ((cA >> sh) << 1) | (bA ^ gA);
-        cB = ((cB >> sh) << 1) | (bB ^ gB);
-        cC = ((cC >> sh) << 1) | (bC ^ gC);
-        depth = L + 1;
-        node = fr.getCo(L) + (int)rank_perm((uint32_t)rk, m);
-        const int s = D - depth;
-        const float loA = PA[cA << s], hiA = PA[(cA + 1) << s];
-        const float loB = PB[cB << s], hiB = PB[(cB + 1) << s];
-        const float loC = PC[cC << s], hiC = PC[(cC + 1) << s];
-        tNA = iA * ((gA ? hiA : loA) - oA);
-        tFA = iA * ((gA ? loA : hiA) - oA);
-        tNB = iB * ((gB ? hiB : loB) - oB);
-        tFB = iB * ((gB ? loB : hiB) - oB);
-        tNC = iC * ((gC ? hiC : loC) - oC);
-        tFC = iC * ((gC ? loC : hiC) - oC);
-        ntmin = fmax3(fmaxf(tNA, tNB), tNC, fr.getTm(L));
+        const uint32_t rcm = rank_lut[m * 256u + (rec.y & 0xffu)];
+        const int s = D - st.depth;
+        const float tMA = st.iA * (PA[(2 * st.cA + 1) << (s - 1)] - st.oA);
+        const float tMB = st.iB * (PB[(2 * st.cB + 1) << (s - 1)] - st.oB);
+        const float tMC = st.iC * (PC[(2 * st.cC + 1) << (s - 1)] - st.oC);
+        const float tNA = st.tNA, tNB = st.tNB, tNC = st.tNC, tFA = st.tFA, tFB = st.tFB, tFC = st.tFC;
+        const float ntmin = st.ntmin;
+        // entry: near child (rank bit 0) enters at tN, far child at tM; exit: tM / tF
+        const float e00 = fmaxf(tNA, tNB), e01 = fmaxf(tNA, tMB), e10 = fmaxf(tMA, tNB), e11 = fmaxf(tMA, tMB);
+        const float x00 = fminf(tMA, tMB), x01 = fminf(tMA, tFB), x10 = fminf(tFA, tMB), x11 = fminf(tFA, tFB);
+        const float cN = fminf(tMC, ORT_MAXFLOAT), cF = fminf(tFC, ORT_MAXFLOAT);
+        uint32_t rm = 0;
+#define ORT_CHILD(R, EAB, XAB, EC, XC)                 \
+    {                                                  \
+        const float mm = fmax3(EAB, EC, ntmin);        \
+        const float xx = fmin3(XAB, XC, ORT_MAXFLOAT); \
+        rm |= (xx >= mm) ? (1u << (R)) : 0u;           \
     }
-    hitT = closest;
-    return hit;
+        ORT_CHILD(0, e00, x00, tNC, cN)
+        ORT_CHILD(1, e01, x01, tNC, cN)
+        ORT_CHILD(2, e10, x10, tNC, cN)
+        ORT_CHILD(3, e11, x11, tNC, cN)
+        ORT_CHILD(4, e00, x00, tMC, cF)
+        ORT_CHILD(5, e01, x01, tMC, cF)
+        ORT_CHILD(6, e10, x10, tMC, cF)
+        ORT_CHILD(7, e11, x11, tMC, cF)
+#undef ORT_CHILD
+        rm &= rcm;
+        if (rm) {
+            const int rk = __builtin_ctz(rm);
+            const uint32_t rest = rm & (rm - 1u);
+            if (rest) {
+                st.masks.put(st.depth, rest);
+                fr.set(st.depth, co, ntmin);
+            }
+            const uint32_t bA = (rk >> 1) & 1u, bB = rk & 1u, bC = (rk >> 2) & 1u;
+            const float eA = bA ? tMA : tNA, eB = bB ? tMB : tNB, eC = bC ? tMC : tNC;
+            st.ntmin = fmax3(fmaxf(eA, eB), eC, ntmin);
+            st.tFA = bA ? tFA : tMA;
+            st.tNA = eA;
+            st.tFB = bB ? tFB : tMB;
+            st.tNB = eB;
+            st.tFC = bC ? tFC : tMC;
+            st.tNC = eC;
+            st.cA = 2 * st.cA + (bA ^ gA);
+            st.cB = 2 * st.cB + (bB ^ gB);
+            st.cC = 2 * st.cC + (bC ^ gC);
+            st.node = co + (int)rank_perm((uint32_t)rk, m);
+            st.depth += 1;
+            return false;
+        }
+    } else {
+        const int off = (int)rec.x;
+        const int n = (int)rec.y;
+        for (int i = 0; i < n; ++i) {
+            const float4 sp = S.leaf_sph[off + i];
+            if (COUNT) cnt.v[2] += 1;
+            float t;
+            if (sphere_hit_t(st.r, st.a, sp, st.ntmin, st.closest, t)) {
+                st.hit = true;
+                st.closest = t;
+                st.hitEntry = off + i;
+                if (COUNT) cnt.v[3] += 1;
+            }
+        }
+        if (st.hit) return true;  // glsl:336: the walk ends after the leaf that produced a hit
+    }
+    // backtrack: next child of the deepest level with one left
+    const int L = st.masks.top();
+    if (L < 0) return true;
+    const int rk = st.masks.pop(L);
+    const int sh = st.depth - L;
+    const uint32_t bA = (rk >> 1) & 1u, bB = rk & 1u, bC = (rk >> 2) & 1u;
+    const uint32_t cA = ((st.cA >> sh) << 1) | (bA ^ gA);
+    const uint32_t cB = ((st.cB >> sh) << 1) | (bB ^ gB);
+    const uint32_t cC = ((st.cC >> sh) << 1) | (bC ^ gC);
+    st.cA = cA;
+    st.cB = cB;
+    st.cC = cC;
+    st.depth = L + 1;
+    st.node = fr.getCo(L) + (int)rank_perm((uint32_t)rk, m);
+    const int s = D - st.depth;
+    const float loA = PA[cA << s], hiA = PA[(cA + 1) << s];
+    const float loB = PB[cB << s], hiB = PB[(cB + 1) << s];
+    const float loC = PC[cC << s], hiC = PC[(cC + 1) << s];
+    st.tNA = st.iA * ((gA ? hiA : loA) - st.oA);
+    st.tFA = st.iA * ((gA ? loA : hiA) - st.oA);
+    st.tNB = st.iB * ((gB ? hiB : loB) - st.oB);
+    st.tFB = st.iB * ((gB ? loB : hiB) - st.oB);
+    st.tNC = st.iC * ((gC ? hiC : loC) - st.oC);
+    st.tFC = st.iC * ((gC ? loC : hiC) - st.oC);
+    st.ntmin = fmax3(fmaxf(st.tNA, st.tNB), st.tNC, fr.getTm(L));
+    return false;
+}
+
+template <bool COUNT, class Frames>
+ORT_FN bool traverse_fast(const KScene& S, const float* planes, const uint8_t* rank_lut, const Ray& r, V3 inv,
+                          float t_min, float t_max, int& hitEntry, float& hitT, Frames& fr, Counters& cnt) {
+    FastState st;
+    if (!fast_begin(S, planes, r, inv, t_min, t_max, st)) return false;
+    while (!fast_step<COUNT>(S, planes, rank_lut, st, fr, cnt)) {
+    }
+    hitEntry = st.hitEntry;
+    hitT = st.closest;
+    return st.hit;
 }
 
 // Literal restatement of traverseOctree (glsl:290-481) over the reference record layout

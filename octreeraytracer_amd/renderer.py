@@ -114,6 +114,10 @@ class Renderer:
         """Disable (True) / enable the sign-specialised fast walk; pixels are identical either way."""
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_EXACT_TRAVERSAL, int(bool(on))))
 
+    def set_refill(self, lanes: int):
+        """Persistent trace: refill a wave once at least `lanes` of its 64 lanes are idle."""
+        self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_REFILL, int(lanes)))
+
     def upload(self, spheres: SphereSet, tree: FlatOctree | None):
         cr = np.ascontiguousarray(spheres.center_radius, np.float32)
         ma = np.ascontiguousarray(spheres.mat_albedo, np.float32)

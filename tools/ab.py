@@ -1,6 +1,6 @@
 """Interleaved A/B timing of kernel variants in one process (cdna_hip_programming.md 5.4
-rule 24): fast vs exact traversal (and layouts) on a bench config.
-usage: python tools/ab.py [config] [rounds]"""
+rule 24).  Variants: exact walk, and persistent-trace refill thresholds.
+usage: python tools/ab.py [config] [rounds] [refill,refill,...]"""
 import sys
 from pathlib import Path
 
@@ -13,24 +13,30 @@ import octreeraytracer_amd as ort  # noqa: E402
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+refills = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else [16]
 W, H, N, D, M, NS, MD = bench.CONFIGS[cfg]
 s = ort.random_spheres(N, 42)
 t = ort.build_octree(s, D, M)
 p = ort.FrameParams.default_camera(W, H, num_samples=NS, max_depth=MD)
-variants = {}
 r = ort.Renderer(0)
 r.upload(s, t)
 out = np.empty((H, W, 3), np.float32)
 ref = None
-res = {"fast": [], "exact": []}
+variants = [("exact", True, 16)] + [(f"refill{f}", False, f) for f in refills]
+res = {v[0]: [] for v in variants}
+tr = {v[0]: [] for v in variants}
 for k in range(rounds):
-    for name in ("fast", "exact"):
-        r.set_exact_traversal(name == "exact")
+    for name, exact, f in variants:
+        r.set_exact_traversal(exact)
+        r.set_refill(f)
         r.render(p, out=out)
         res[name].append(r.last_kernel_ms())
+        tr[name].append(r.last_trace_ms())
         if ref is None:
             ref = out.copy()
         else:
             assert np.array_equal(ref, out), name
-for name, v in res.items():
-    print(f"{cfg} {name:6s} median {np.median(v):.3f} ms  min {np.min(v):.3f}  -> {W*H*NS/np.median(v)/1e3:.1f} Mrays/s")
+for name in res:
+    v = res[name]
+    print(f"{cfg} {name:9s} frame median {np.median(v):.3f} ms (min {np.min(v):.3f}; first trace {np.median(tr[name]):.3f})"
+          f" -> {W*H*NS/np.median(v)/1e3:.1f} Mrays/s")
