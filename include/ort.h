@@ -84,6 +84,7 @@ typedef struct ort_scene_info {
 #define ORT_OPT_FORCE_LAYOUT 1     /* -1 auto (default), or ORT_LAYOUT_* */
 #define ORT_OPT_EXACT_TRAVERSAL 2  /* 1: disable the sign-specialised fast walk (A/B testing; same pixels) */
 #define ORT_OPT_REFILL 3           /* persistent trace: refill a wave when >= value of its 64 lanes idle (16) */
+#define ORT_OPT_PERSISTENT 4       /* 1: persistent trace kernel with per-lane ray refill (default 0) */
 
 /* Traffic counters (ort_count_traffic), in the REFERENCE layout's terms. */
 #define ORT_COUNT_NODES_POPPED 0

@@ -48,6 +48,7 @@ struct PipeArgs {
     int nobounce;     // maxDepth <= 0: radiance() returns (1,1,1) without tracing
     int exact_only;   // ORT_OPT_EXACT_TRAVERSAL: every compact ray takes the exact walk
     int refill;       // persistent trace: refill a wave when at least this many lanes idle
+    int rays_stored;  // bounce-0 rays were written by ort_raygen_kernel (persistent pipeline)
     int2* hit;        // per path: {entry (-1 miss), t bits}
     int* defer_list;
     int* sync;        // [0] deferred count, [1] work cursor of the persistent trace
@@ -155,29 +156,47 @@ __global__ void __launch_bounds__(kBlock) ort_raygen_kernel(PipeArgs A) {
     A.prng[k] = make_float2(st.x, st.y);
 }
 
-// Persistent trace over the compact layout: every lane keeps one ray's FastState and,
-// when it finishes, takes the next path slot from a global cursor (wave-aggregated
-// atomic), so the wave stays full until the queue drains.  Rays the fast walk cannot
-// take are appended to the defer list for ort_trace_exact.
+// Persistent trace over the compact layout: every lane keeps one ray's FastState; the
+// wave owns a chunk of kChunk consecutive path slots (one atomic on the global cursor per
+// chunk, MI355X_MICROARCH.md 'dequeue') and hands the next slots of its chunk to lanes
+// that finished, so the wave stays full until the queue drains.  Rays the fast walk
+// cannot take are appended to the defer list for ort_trace_exact.
+constexpr int kChunk = 256;
+
 template <bool COUNT>
 __global__ void __launch_bounds__(kBlock) ort_trace_persistent(PipeArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     LdsView L = setup_lds<true>(smem, A.S);
     const uint8_t* lut = L.lut;
+    const int lane = threadIdx.x & 63;
+    const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     ort::Counters cnt;
     for (int q = 0; q < 6; ++q) cnt.v[q] = 0;
     ort::FastState st;
     int k = -1;
-    bool drained = false;  // wave-uniform: the cursor passed A.total
+    int next = 0, end = 0;   // wave-uniform: remaining slots [next, end) of the wave's chunk
+    bool drained = false;    // wave-uniform: the global cursor passed A.total
     for (;;) {
         const unsigned long long idle = __ballot(k < 0);
-        if (idle == __ballot(true)) {
-            if (drained) break;
-        }
-        if (!drained && (unsigned)__popcll(idle) >= (unsigned)A.refill) {
+        const int n_idle = __popcll(idle);
+        if (n_idle == 64 && drained) break;
+        if (!drained && n_idle >= A.refill) {
+            if (next == end) {
+                int base = 0;
+                if (lane == 0) base = atomicAdd(A.sync + 1, kChunk);
+                base = __shfl(base, 0);
+                if (base >= A.total) {
+                    drained = true;
+                    continue;
+                }
+                next = base;
+                end = min(base + kChunk, A.total);
+            }
+            const int take = min(n_idle, end - next);
             if (k < 0) {
-                const int cand = atomicAdd(A.sync + 1, 1);
-                if (cand < A.total) {
+                const int rank = __popcll(idle & below);
+                if (rank < take) {
+                    const int cand = next + rank;
                     bool alive;
                     const ort::Ray ray = load_ray(A, cand, alive);
                     if (alive) {
@@ -192,8 +211,7 @@ __global__ void __launch_bounds__(kBlock) ort_trace_persistent(PipeArgs A) {
                     }
                 }
             }
-            // uniform: once any lane saw the end of the queue, later fetches are all past it
-            drained = __ballot(__hip_atomic_load(A.sync + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= A.total) != 0;
+            next += take;
             continue;
         }
         if (k >= 0) {
@@ -206,12 +224,65 @@ __global__ void __launch_bounds__(kBlock) ort_trace_persistent(PipeArgs A) {
     flush_counts<COUNT>(cnt, A.counters);
 }
 
+// Path-slot ray for the trace kernels: bounce 0 generates the sample's camera ray here
+// (main() up to radiance()'s first line; the shade kernel regenerates it identically),
+// later bounces read the ray the previous shade kernel stored.
+template <bool PRIMARY>
+__device__ inline ort::Ray slot_ray(const PipeArgs& A, int k, bool& alive) {
+    if constexpr (PRIMARY) {
+        int col, row;
+        alive = slot_coords(A, k, col, row);
+        const int y = alive ? tile_row_to_y(A.tm, row) : 0;
+        alive = alive && y < A.pp.H;
+        ort::Ray ray;
+        ray.o = ort::mk(0.0f, 0.0f, 0.0f);
+        ray.d = ray.o;
+        if (!alive) return ray;
+        ort_rng st;
+        if (A.sample == 0) {
+            ort::pixel_rng_init(A.pp, A.tm.x0 + col, y, st);
+        } else {
+            const float2 v = A.prng[k];
+            st.x = v.x;
+            st.y = v.y;
+        }
+        return ort::primary_ray(A.pp, A.tm.x0 + col, y, A.sample, st);
+    } else {
+        return load_ray(A, k, alive);
+    }
+}
+
+// One ray per lane over the compact layout (default): the tile-block order of the path
+// slots keeps each wave on an 8x8 pixel block, whose rays walk nearly the same nodes.
+template <bool COUNT, bool PRIMARY>
+__global__ void __launch_bounds__(kBlock) ort_trace_compact(PipeArgs A) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    LdsView L = setup_lds<true>(smem, A.S);
+    const int k = blockIdx.x * kBlock + threadIdx.x;
+    bool alive;
+    const ort::Ray ray = slot_ray<PRIMARY>(A, k, alive);
+    if (!alive) return;
+    ort::Counters cnt;
+    for (int q = 0; q < 6; ++q) cnt.v[q] = 0;
+    const ort::V3 inv = ort::mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
+    if (A.exact_only || !ort::fast_path_ok(inv)) {
+        A.defer_list[atomicAdd(A.sync, 1)] = k;
+        return;
+    }
+    if (COUNT) cnt.v[5] += 1;
+    float t = 0.0f;
+    int entry = -1;
+    const bool hit = ort::traverse_fast<COUNT>(A.S, L.planes, L.lut, ray, inv, 0.001f, ORT_MAXFLOAT, entry, t, L.fr, cnt);
+    A.hit[k] = make_int2(hit ? entry : -1, __float_as_int(t));
+    flush_counts<COUNT>(cnt, A.counters);
+}
+
 // One-ray-per-lane trace for the explicit layout (MODE 1) and brute force (MODE 2).
-template <int MODE, bool COUNT>
+template <int MODE, bool COUNT, bool PRIMARY>
 __global__ void __launch_bounds__(kBlock) ort_trace_kernel(PipeArgs A) {
     const int k = blockIdx.x * kBlock + threadIdx.x;
     bool alive;
-    const ort::Ray ray = load_ray(A, k, alive);
+    const ort::Ray ray = slot_ray<PRIMARY>(A, k, alive);
     if (!alive) return;
     ort::Counters cnt;
     for (int q = 0; q < 6; ++q) cnt.v[q] = 0;
@@ -231,7 +302,7 @@ __global__ void __launch_bounds__(kBlock) ort_trace_kernel(PipeArgs A) {
 }
 
 // Exact compact walk (traverse_compact) for the deferred rays; grid-stride loop.
-template <bool COUNT>
+template <bool COUNT, bool PRIMARY>
 __global__ void __launch_bounds__(kBlock) ort_trace_exact(PipeArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     LdsView L = setup_lds<false>(smem, A.S);
@@ -241,7 +312,7 @@ __global__ void __launch_bounds__(kBlock) ort_trace_exact(PipeArgs A) {
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
         const int k = A.defer_list[i];
         bool alive;
-        const ort::Ray ray = load_ray(A, k, alive);
+        const ort::Ray ray = slot_ray<PRIMARY>(A, k, alive);
         float t;
         int entry;
         const int st = ort::trace_ray<0, COUNT>(A.S, L.planes, nullptr, ray, false, t, entry, L.fr, nullptr, nullptr, cnt);
@@ -266,13 +337,25 @@ __global__ void __launch_bounds__(kBlock) ort_shade_kernel(PipeArgs A) {
         }
         return;
     }
-    bool alive;
-    ort::Ray ray = load_ray(A, k, alive);
-    if (!alive) return;
-    const float2 r2 = A.prng[k];
+    bool alive = true;
+    ort::Ray ray;
     ort_rng st;
-    st.x = r2.x;
-    st.y = r2.y;
+    if (FIRST && !A.rays_stored) {
+        if (A.sample == 0) {
+            ort::pixel_rng_init(A.pp, A.tm.x0 + col, y, st);
+        } else {
+            const float2 v = A.prng[k];
+            st.x = v.x;
+            st.y = v.y;
+        }
+        ray = ort::primary_ray(A.pp, A.tm.x0 + col, y, A.sample, st);
+    } else {
+        ray = load_ray(A, k, alive);
+        if (!alive) return;
+        const float2 r2 = A.prng[k];
+        st.x = r2.x;
+        st.y = r2.y;
+    }
     ort::V3 c = ort::mk(1.0f, 1.0f, 1.0f);
     float importance = 1.0f;
     if (!FIRST) {
@@ -347,6 +430,7 @@ struct ort_ctx {
     int force_layout = -1;
     int exact_only = 0;
     int refill = 16;
+    int persistent = 0;
     bool has_scene = false;
     int layout = ORT_LAYOUT_EXPLICIT;
     int depth = 0;
@@ -524,12 +608,19 @@ int ensure(ort_ctx* ctx, DevBuf& b, size_t bytes) {
     return ORT_OK;
 }
 
-template <bool COUNT>
-hipError_t launch_trace(int mode, const PipeArgs& a, int blocks, int pblocks, size_t lds, hipStream_t s) {
-    if (mode == 0) hipLaunchKernelGGL((ort_trace_persistent<COUNT>), dim3(pblocks), dim3(kBlock), lds, s, a);
-    else if (mode == 1) hipLaunchKernelGGL((ort_trace_kernel<1, COUNT>), dim3(blocks), dim3(kBlock), 0, s, a);
-    else hipLaunchKernelGGL((ort_trace_kernel<2, COUNT>), dim3(blocks), dim3(kBlock), 0, s, a);
+template <bool COUNT, bool PRIMARY>
+hipError_t launch_trace_p(int mode, const PipeArgs& a, int blocks, int pblocks, size_t lds, hipStream_t s) {
+    if (mode == 0 && pblocks > 0) hipLaunchKernelGGL((ort_trace_persistent<COUNT>), dim3(pblocks), dim3(kBlock), lds, s, a);
+    else if (mode == 0) hipLaunchKernelGGL((ort_trace_compact<COUNT, PRIMARY>), dim3(blocks), dim3(kBlock), lds, s, a);
+    else if (mode == 1) hipLaunchKernelGGL((ort_trace_kernel<1, COUNT, PRIMARY>), dim3(blocks), dim3(kBlock), 0, s, a);
+    else hipLaunchKernelGGL((ort_trace_kernel<2, COUNT, PRIMARY>), dim3(blocks), dim3(kBlock), 0, s, a);
     return hipGetLastError();
+}
+
+template <bool COUNT>
+hipError_t launch_trace(int mode, bool primary, const PipeArgs& a, int blocks, int pblocks, size_t lds, hipStream_t s) {
+    return primary ? launch_trace_p<COUNT, true>(mode, a, blocks, pblocks, lds, s)
+                   : launch_trace_p<COUNT, false>(mode, a, blocks, pblocks, lds, s);
 }
 
 template <int MODE>
@@ -584,11 +675,13 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     const int ns = p->num_samples, maxd = p->max_depth;
     const bool direct = (ns == 1 && maxd == 1);
     if ((rc = ensure(ctx, ctx->hit, 8 * slots)) || (rc = ensure(ctx, ctx->defer_list, 4 * slots)) ||
-        (rc = ensure(ctx, ctx->defer_count, 64)) || (rc = ensure(ctx, ctx->po, 16 * slots)) ||
-        (rc = ensure(ctx, ctx->pd, 16 * slots)) || (rc = ensure(ctx, ctx->prng, 8 * slots)))
+        (rc = ensure(ctx, ctx->defer_count, 64)))
         return rc;
-    if (!direct) {
-        if ((rc = ensure(ctx, ctx->pc, 16 * slots)) || (rc = ensure(ctx, ctx->pcol, 16 * slots))) return rc;
+    if (!direct || ctx->persistent) {
+        if ((rc = ensure(ctx, ctx->po, 16 * slots)) || (rc = ensure(ctx, ctx->pd, 16 * slots)) ||
+            (rc = ensure(ctx, ctx->prng, 8 * slots)) || (rc = ensure(ctx, ctx->pc, 16 * slots)) ||
+            (rc = ensure(ctx, ctx->pcol, 16 * slots)))
+            return rc;
     }
     PipeArgs a;
     std::memset(&a, 0, sizeof(a));
@@ -610,31 +703,38 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     a.out = dout;
     a.counters = dcounters;
     const size_t lds = lds_bytes(mode, ctx->depth);
-    const int pblocks = mode == 0 ? persistent_blocks(ctx->device, dcounters != nullptr, lds, blocks) : 0;
+    const int pblocks = (mode == 0 && ctx->persistent) ? persistent_blocks(ctx->device, dcounters != nullptr, lds, blocks) : 0;
     const int exact_blocks = 1024;
     hipError_t e;
     HIPCHK(ctx, hipEventRecord(ctx->ev0, s));
     bool first_trace = true;
     for (int smp = 0; smp < ns; ++smp) {
         a.sample = smp;
-        hipLaunchKernelGGL(ort_raygen_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, s, a);
-        if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "ort_raygen_kernel launch");
+        a.rays_stored = pblocks > 0;
+        if (pblocks > 0) {  // the persistent kernel refills lanes from stored rays
+            hipLaunchKernelGGL(ort_raygen_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, s, a);
+            if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "ort_raygen_kernel launch");
+        }
         const int bounces = maxd > 0 ? maxd : 1;
         a.nobounce = maxd <= 0;
         for (int b = 0; b < bounces; ++b) {
             a.last = (b == bounces - 1);
             if (!a.nobounce) {
                 HIPCHK(ctx, hipMemsetAsync(ctx->defer_count.p, 0, 64, s));
-                e = dcounters ? launch_trace<true>(mode, a, (int)blocks, pblocks, lds, s)
-                              : launch_trace<false>(mode, a, (int)blocks, pblocks, lds, s);
+                const bool prim = (b == 0) && pblocks == 0;
+                e = dcounters ? launch_trace<true>(mode, prim, a, (int)blocks, pblocks, lds, s)
+                              : launch_trace<false>(mode, prim, a, (int)blocks, pblocks, lds, s);
                 if (e != hipSuccess) return hip_fail(ctx, e, "trace kernel launch");
                 if (first_trace) {
                     HIPCHK(ctx, hipEventRecord(ctx->ev_trace, s));
                     first_trace = false;
                 }
                 if (mode == 0) {
-                    if (dcounters) hipLaunchKernelGGL((ort_trace_exact<true>), dim3(exact_blocks), dim3(kBlock), lds, s, a);
-                    else hipLaunchKernelGGL((ort_trace_exact<false>), dim3(exact_blocks), dim3(kBlock), lds, s, a);
+                    const bool prim = (b == 0) && pblocks == 0;
+                    if (dcounters && prim) hipLaunchKernelGGL((ort_trace_exact<true, true>), dim3(exact_blocks), dim3(kBlock), lds, s, a);
+                    else if (dcounters) hipLaunchKernelGGL((ort_trace_exact<true, false>), dim3(exact_blocks), dim3(kBlock), lds, s, a);
+                    else if (prim) hipLaunchKernelGGL((ort_trace_exact<false, true>), dim3(exact_blocks), dim3(kBlock), lds, s, a);
+                    else hipLaunchKernelGGL((ort_trace_exact<false, false>), dim3(exact_blocks), dim3(kBlock), lds, s, a);
                     if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "ort_trace_exact launch");
                 }
             }
@@ -709,6 +809,10 @@ int ort_set_option(ort_ctx* ctx, int option, int value) {
     if (option == ORT_OPT_FORCE_LAYOUT) {
         if (value < -1 || value > ORT_LAYOUT_EXPLICIT) return fail(ctx, ORT_ERR_INVALID_ARG, "bad layout");
         ctx->force_layout = value;
+        return ORT_OK;
+    }
+    if (option == ORT_OPT_PERSISTENT) {
+        ctx->persistent = value ? 1 : 0;
         return ORT_OK;
     }
     if (option == ORT_OPT_REFILL) {

@@ -114,6 +114,10 @@ class Renderer:
         """Disable (True) / enable the sign-specialised fast walk; pixels are identical either way."""
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_EXACT_TRAVERSAL, int(bool(on))))
 
+    def set_persistent(self, on: bool):
+        """Use the persistent trace kernel with per-lane ray refill (default: one ray per lane)."""
+        self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_PERSISTENT, int(bool(on))))
+
     def set_refill(self, lanes: int):
         """Persistent trace: refill a wave once at least `lanes` of its 64 lanes are idle."""
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_REFILL, int(lanes)))

@@ -118,3 +118,27 @@ def test_errors(ort, renderer, scene_c1):
     with pytest.raises(ort.OrtError):
         fresh.render(p)  # no scene
     fresh.close()
+
+
+@pytest.mark.parametrize("persistent,exact,refill", [(False, False, 16), (False, True, 16), (True, False, 1),
+                                                     (True, False, 16), (True, True, 64)])
+def test_kernel_variants_identical(ort, oracle, renderer, scene_c2, persistent, exact, refill):
+    """Every trace-kernel variant (one ray per lane / persistent with refill, fast / exact
+    walk) produces the oracle's pixels, also with several samples and bounces."""
+    s, t = scene_c2
+    renderer.upload(s, t)
+    renderer.set_persistent(persistent)
+    renderer.set_exact_traversal(exact)
+    renderer.set_refill(refill)
+    try:
+        p = ort.FrameParams.default_camera(1920, 1080, num_samples=2, max_depth=3)
+        tile = ort.Tile(700, 200, 300, 120)
+        got = renderer.render(p, tile)
+        ref = oracle.render(s, t, p, 700, 300, 200, 120)
+        assert_same(got, ref, f"variant persistent={persistent} exact={exact}")
+        p1 = ort.FrameParams.default_camera(1920, 1080)
+        assert_same(renderer.render(p1, tile), oracle.render(s, t, p1, 700, 300, 200, 120), "primary")
+    finally:
+        renderer.set_persistent(False)
+        renderer.set_exact_traversal(False)
+        renderer.set_refill(16)

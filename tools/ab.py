@@ -22,13 +22,15 @@ r = ort.Renderer(0)
 r.upload(s, t)
 out = np.empty((H, W, 3), np.float32)
 ref = None
-variants = [("exact", True, 16)] + [(f"refill{f}", False, f) for f in refills]
+variants = [("exact", True, 0), ("lane", False, 0)] + [(f"refill{f}", False, f) for f in refills]
 res = {v[0]: [] for v in variants}
 tr = {v[0]: [] for v in variants}
 for k in range(rounds):
     for name, exact, f in variants:
         r.set_exact_traversal(exact)
-        r.set_refill(f)
+        r.set_persistent(f > 0)
+        if f > 0:
+            r.set_refill(f)
         r.render(p, out=out)
         res[name].append(r.last_kernel_ms())
         tr[name].append(r.last_trace_ms())
