@@ -9,13 +9,13 @@ LIB := octreeraytracer_amd/lib/libort.so
 CXXFLAGS := -O3 -std=c++17 -ffp-contract=off -fno-fast-math -fPIC -Wall -Wextra -Wno-unused-parameter
 HIPFLAGS := -O3 -std=c++17 --offload-arch=$(ARCH) -ffp-contract=off -fno-fast-math -fPIC -Wall -Wno-unused-parameter
 
-HOST_SRCS := octree.cpp scene.cpp host_abi.cpp layout.cpp
+HOST_SRCS := octree.cpp scene.cpp host_abi.cpp layout.cpp raytracer.cpp
 HOST_OBJS := $(addprefix $(OBJ)/,$(HOST_SRCS:.cpp=.o))
 HIP_OBJS := $(OBJ)/ort_kernel.o
 HDRS := $(wildcard $(SRC)/*.h) $(SRC)/prebuilt_scene.inc include/ort.h include/ort_math.h
 
-.PHONY: all lib oracle ref clean
-all: lib oracle
+.PHONY: all lib oracle ref examples clean
+all: lib oracle examples
 
 lib: $(LIB)
 
@@ -30,6 +30,11 @@ $(OBJ)/ort_kernel.o: $(SRC)/ort_kernel.hip $(HDRS)
 $(LIB): $(HOST_OBJS) $(HIP_OBJS)
 	@mkdir -p $(dir $(LIB))
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -Wl,-soname,libort.so
+
+examples: build/ort_main
+
+build/ort_main: examples/main.cpp $(LIB) $(HDRS)
+	$(CXX) -O2 -std=c++17 -I$(SRC) -o $@ examples/main.cpp -L$(dir $(LIB)) -lort -Wl,-rpath,'$$ORIGIN/../$(dir $(LIB))'
 
 oracle:
 	$(MAKE) -C oracle all

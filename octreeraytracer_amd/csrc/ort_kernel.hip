@@ -641,11 +641,11 @@ hipError_t launch_shade(int mode, bool first, bool direct, const PipeArgs& a, in
 // start when others finish; no grid-wide synchronisation depends on residency).
 int persistent_blocks(int device, bool count, size_t lds, long long needed) {
     int per_cu = 0, cus = 0;
-    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
     if (count)
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ort_trace_persistent<true>, kBlock, lds);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ort_trace_persistent<true>, kBlock, lds);
     else
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ort_trace_persistent<false>, kBlock, lds);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ort_trace_persistent<false>, kBlock, lds);
     long long b = (long long)std::max(per_cu, 1) * std::max(cus, 1);
     return (int)std::max(1LL, std::min(b, needed));
 }

@@ -1,0 +1,181 @@
+// raytracer.cpp -- Raytracer on the gfx950 kernel (see raytracer.h).
+#include "raytracer.h"
+
+#include <chrono>
+#include <cmath>
+#include <fstream>
+#include <iostream>
+
+#include "scene.h"
+
+Raytracer::Raytracer() : Raytracer(RaytracerConfig()) {}
+
+Raytracer::Raytracer(const RaytracerConfig& c)
+    : camera(ortm::vec3(0.0f, 8.0f, 30.0f)),
+      cfg(c),
+      width((int)c.width),
+      height((int)c.height),
+      ctx(nullptr),
+      sceneReady(false),
+      octree(c.debug ? c.debugDepth : c.maxDepth, c.debug ? c.debugSpheresPerNode : c.maxSpheresPerNode),
+      statsFilename(c.outputFile),
+      frameCount(0) {
+    // camera pose of main() (src/main.cpp:29-40)
+    if (cfg.debug) camera.Position = ortm::vec3(30.0f, 20.0f, -50.0f);
+    else camera.Position = ortm::vec3(0.0f, 2.5f, -10.0f);
+    camera.updateCameraVectors();
+}
+
+Raytracer::~Raytracer() { cleanupBuffers(); }
+
+bool Raytracer::initialize() {
+    if (ctx) return true;
+    if (ort_create(cfg.device, &ctx) != ORT_OK) {
+        std::cerr << "Failed to create the MI355X context: " << ort_last_error(nullptr) << std::endl;
+        ctx = nullptr;
+        return false;
+    }
+    return true;
+}
+
+const char* Raytracer::lastError() const { return ort_last_error(ctx); }
+
+std::vector<Sphere> Raytracer::generatePreBuiltSpheres() { return ort::generatePreBuiltSpheres(); }
+std::vector<Sphere> Raytracer::generateRandomSpheres() { return ort::generateRandomSpheres(cfg.numSpheres, cfg.seed); }
+
+std::vector<Sphere> Raytracer::generateSpheres() {
+    if (cfg.debug) return ort::generateDebugSpheres();
+    if (cfg.usePrebuilt) return generatePreBuiltSpheres();
+    return generateRandomSpheres();
+}
+
+void Raytracer::setupScene() {
+    spheres = generateSpheres();
+    const int maxDepth = cfg.debug ? cfg.debugDepth : cfg.maxDepth;
+    const int maxSpheresPerNode = cfg.debug ? cfg.debugSpheresPerNode : cfg.maxSpheresPerNode;
+    octree = Octree(maxDepth, maxSpheresPerNode);
+    octree.build(spheres, cfg.debug);
+    if (cfg.debug) octree.printFlattenedTree();
+}
+
+void Raytracer::setupBuffers() {
+    // SoA packing of src/raytracer.cpp:87-101, then one upload (replaces 7x glBufferData)
+    std::vector<float> cr(4 * spheres.size()), ma(4 * spheres.size()), fr(4 * spheres.size());
+    ort::packSpheres(spheres, cr.data(), ma.data(), fr.data());
+    const int rc = ort_upload_octree_nodes(ctx, cr.data(), ma.data(), fr.data(), (int32_t)spheres.size(),
+                                           octree.flattenedTree.data(), (int32_t)octree.flattenedTree.size(),
+                                           octree.objectIndices.data(), (int64_t)octree.objectIndices.size());
+    if (rc != ORT_OK) std::cerr << "scene upload failed: " << ort_last_error(ctx) << std::endl;
+    sceneReady = rc == ORT_OK;
+}
+
+void Raytracer::cleanupBuffers() {
+    if (ctx) ort_destroy(ctx);
+    ctx = nullptr;
+    sceneReady = false;
+}
+
+ort_params Raytracer::frameParams(const Camera& cam) const {
+    ort_params p;
+    p.width = width;
+    p.height = height;
+    p.num_samples = cfg.numSamples;
+    p.max_depth = cfg.maxRaysDepth;
+    p.use_octree = cfg.useOctree;
+    const ortm::mat4 v = cam.GetViewMatrix();
+    for (int c = 0; c < 4; ++c)
+        for (int r = 0; r < 4; ++r) p.view[4 * c + r] = v[c][r];
+    p.camera_position[0] = cam.Position.x;
+    p.camera_position[1] = cam.Position.y;
+    p.camera_position[2] = cam.Position.z;
+    p.camera_zoom = cam.Zoom;
+    return p;
+}
+
+int Raytracer::render(const Camera& cam, const ort_tile& tile, float* out, bool outIsDevice, void* stream) {
+    if (!ctx && !initialize()) return ORT_ERR_HIP;
+    if (!sceneReady) {
+        setupScene();
+        setupBuffers();
+        if (!sceneReady) return ORT_ERR_INVALID_ARG;
+    }
+    const ort_params p = frameParams(cam);
+    return ort_render(ctx, &p, &tile, out, outIsDevice ? 1 : 0, stream);
+}
+
+int Raytracer::render(const Camera& cam, float* rgb) {
+    ort_tile t{0, width, 0, height, 0, 0};
+    return render(cam, t, rgb, false, nullptr);
+}
+
+void Raytracer::run() {
+    if (!initialize()) return;
+    setupScene();
+    setupBuffers();
+    if (!sceneReady) return;
+    frame.assign((size_t)width * height * 3, 0.0f);
+    for (int i = 0; i < cfg.warmupFrames; i++) render(camera, frame.data());
+    for (int i = 0; i < cfg.frames; i++) {
+        const auto frameStart = std::chrono::steady_clock::now();
+        if (render(camera, frame.data()) != ORT_OK) {
+            std::cerr << "render failed: " << lastError() << std::endl;
+            break;
+        }
+        const double frameTime = std::chrono::duration<double>(std::chrono::steady_clock::now() - frameStart).count();
+        if (cfg.collectStats) {
+            renderTimes.push_back(frameTime);
+            frameCount++;
+        }
+    }
+    if (cfg.collectStats) saveStats();
+}
+
+// saveStats (src/raytracer.cpp:359-449): 2.5-sigma z-score filter, one ';' row.
+void Raytracer::saveStats() {
+    if (renderTimes.empty()) {
+        std::cout << "No render times recorded." << std::endl;
+        return;
+    }
+    std::ofstream outFile(statsFilename, std::ios::out | std::ios::app);
+    if (!outFile || !outFile.is_open()) {
+        std::cerr << "Error opening file for writing: " << statsFilename << std::endl;
+        return;
+    }
+    const std::vector<double>& all = renderTimes;
+    double sum = 0.0;
+    for (double t : all) sum += t;
+    const double mean = sum / all.size();
+    double variance = 0.0;
+    for (double t : all) variance += (t - mean) * (t - mean);
+    const double stdDev = std::sqrt(variance / all.size());
+    const double THRESHOLD = 2.5;
+    std::vector<double> clean;
+    int outliers = 0;
+    for (double t : all) {
+        const double z = std::abs(t - mean) / stdDev;
+        if (z <= THRESHOLD) clean.push_back(t);
+        else outliers++;
+    }
+    if (outliers > 0) std::cout << "Removed " << outliers << " outliers from " << all.size() << " samples" << std::endl;
+    double total = 0.0, mn = clean.empty() ? 9999 : clean[0], mx = clean.empty() ? 0 : clean[0], fpsTotal = 0.0;
+    for (double t : clean) {
+        total += t;
+        mn = std::min(mn, t);
+        mx = std::max(mx, t);
+        fpsTotal += 1.0 / t;
+    }
+    if (clean.empty()) {
+        clean = all;
+        total = sum;
+        for (double t : clean) {
+            mn = std::min(mn, t);
+            mx = std::max(mx, t);
+            fpsTotal += 1.0 / t;
+        }
+    }
+    const double avg = total / clean.size();
+    const double fpsAvg = fpsTotal / clean.size();
+    outFile << cfg.useOctree << ";" << cfg.numSpheres << ";" << cfg.maxDepth << ";" << cfg.maxSpheresPerNode << ";"
+            << cfg.numSamples << ";" << cfg.maxRaysDepth << ";" << cfg.width << ";" << cfg.height << ";" << mn << ";" << mx
+            << ";" << avg << ";" << 1.0 / mx << ";" << 1.0 / mn << ";" << fpsAvg << ";" << octree.buildTime << std::endl;
+}
