@@ -113,7 +113,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    kern_ms = [a.elapsed_time(b) for a, b in evs]
+    kern_ms = [a.elapsed_time(b) for a, b in evs]          # whole per-frame pipeline (trace+shade)
+    trace_ms = r.trace_times_ms(min(args.steps, 64))         # the dominant kernel, same frames
     t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -123,20 +124,21 @@ def main():
     counts = r.count_traffic(p, tile)
     alg_bytes = ort.algorithmic_bytes(counts)
     kern_avg_ms = float(np.mean(kern_ms))
+    trace_avg_ms = float(np.mean(trace_ms))
     rays_per_frame = W * H * NS
 
     result = None
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
         value = rays_per_frame * args.steps / elapsed / 1e6
-        achieved = alg_bytes / (kern_avg_ms * 1e-3) / 1e9
+        achieved = alg_bytes / (trace_avg_ms * 1e-3) / 1e9
         traffic = None
         tj = Path(args.traffic_json)
         if tj.exists():
             try:
                 tr = json.loads(tj.read_text())
                 if tr.get("config") == args.config and tr.get("tile_rows") == tile.rows:
-                    traffic = tr.get("hbm_bytes_per_launch")
+                    traffic = int(tr.get("hbm_bytes_per_launch"))
             except Exception:
                 traffic = None
         result = {
@@ -160,8 +162,9 @@ def main():
                 "layout": info["layout"], "partition": "16-row bands round-robin + RCCL gather" if world > 1
                 else "full frame", "rays_per_step": rays_per_frame,
             },
-            "kernel_ms_avg": round(kern_avg_ms, 4),
-            "kernel_ms_min": round(float(np.min(kern_ms)), 4),
+            "frame_gpu_ms_avg": round(kern_avg_ms, 4),
+            "trace_kernel_ms_avg": round(trace_avg_ms, 4),
+            "trace_kernel_ms_min": round(float(np.min(trace_ms)), 4),
             "roofline": {
                 "bound": "hbm",
                 "achieved": round(achieved, 1),
@@ -172,7 +175,10 @@ def main():
                 "algorithmic_bytes_per_launch": int(alg_bytes),
                 "bytes_per_ray": round(alg_bytes / max(1, counts["pixels"]), 1),
                 "counts": counts,
-                "kernel": "ort_trace_kernel<0,false>",
+                "kernel": "ort_trace_compact<false,true> (camera rays + octree walk)",
+                "note": "achieved = reference-layout record bytes (SURVEY.md 8(d)) the reference walk reads per "
+                        "frame / trace-kernel time; this kernel reads far fewer bytes (compact layout, L2/MALL "
+                        "residency) and is instruction-issue bound -- see traffic and DESIGN.md",
             },
             "setup_s": {"scene_build": round(t_build, 3), "upload": round(t_upload, 3)},
         }

@@ -138,9 +138,13 @@ int ort_render(ort_ctx* ctx, const ort_params* params, const ort_tile* tile,
  * from HIP events recorded on its stream.  Only valid once that stream has passed the frame. */
 int ort_last_kernel_ms(ort_ctx* ctx, float* ms);
 
-/* Duration in milliseconds from the start of the last ort_render to the end of its first
- * trace kernel (the dominant kernel: camera rays + octree walk of bounce 0, sample 0). */
+/* Duration in milliseconds of the first trace kernel (camera rays + octree walk of bounce
+ * 0, sample 0: the dominant kernel) of the last ort_render, from HIP events on its stream. */
 int ort_last_trace_ms(ort_ctx* ctx, float* ms);
+
+/* The same for the last n frames (at most 64), oldest first; returns how many were
+ * written, or a negative ORT_ERR_* code. */
+int ort_trace_times_ms(ort_ctx* ctx, int n, float* ms);
 
 /* Run the counting variant of the kernel over the tile and return, summed over all
  * pixels, the reference-layout work counters ORT_COUNT_* (counts[ORT_COUNT_N]). */

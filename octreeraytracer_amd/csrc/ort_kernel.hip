@@ -424,7 +424,10 @@ struct DevBuf {
 struct ort_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_trace = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    static constexpr int kRing = 64;           // trace-kernel timing of the last 64 frames
+    hipEvent_t tr0[kRing] = {}, tr1[kRing] = {};
+    long long frames = 0;                      // frames whose first trace kernel was timed
     bool timed = false;
     std::string err;
     int force_layout = -1;
@@ -721,12 +724,15 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
             a.last = (b == bounces - 1);
             if (!a.nobounce) {
                 HIPCHK(ctx, hipMemsetAsync(ctx->defer_count.p, 0, 64, s));
+                const int slot = (int)(ctx->frames % ort_ctx::kRing);
+                if (first_trace) HIPCHK(ctx, hipEventRecord(ctx->tr0[slot], s));
                 const bool prim = (b == 0) && pblocks == 0;
                 e = dcounters ? launch_trace<true>(mode, prim, a, (int)blocks, pblocks, lds, s)
                               : launch_trace<false>(mode, prim, a, (int)blocks, pblocks, lds, s);
                 if (e != hipSuccess) return hip_fail(ctx, e, "trace kernel launch");
                 if (first_trace) {
-                    HIPCHK(ctx, hipEventRecord(ctx->ev_trace, s));
+                    HIPCHK(ctx, hipEventRecord(ctx->tr1[slot], s));
+                    ctx->frames += 1;
                     first_trace = false;
                 }
                 if (mode == 0) {
@@ -747,7 +753,6 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
         if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "ort_finalize_kernel launch");
     }
     HIPCHK(ctx, hipEventRecord(ctx->ev1, s));
-    if (first_trace) HIPCHK(ctx, hipEventRecord(ctx->ev_trace, s));
     ctx->timed = true;
     if (!out_is_device) {
         HIPCHK(ctx, hipMemcpyAsync(out, dout, 12 * pix, hipMemcpyDeviceToHost, s));
@@ -775,11 +780,17 @@ int ort_create(int device, ort_ctx** out) {
     if (!c) return fail(nullptr, ORT_ERR_OUT_OF_MEMORY, "ort_create: out of host memory");
     c->device = device;
     if ((e = hipSetDevice(device)) != hipSuccess || (e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess ||
-        (e = hipEventCreate(&c->ev0)) != hipSuccess || (e = hipEventCreate(&c->ev1)) != hipSuccess ||
-        (e = hipEventCreate(&c->ev_trace)) != hipSuccess) {
+        (e = hipEventCreate(&c->ev0)) != hipSuccess || (e = hipEventCreate(&c->ev1)) != hipSuccess) {
         const int rc = hip_fail(nullptr, e, "ort_create");
         delete c;
         return rc;
+    }
+    for (int i = 0; i < ort_ctx::kRing; ++i) {
+        if ((e = hipEventCreate(&c->tr0[i])) != hipSuccess || (e = hipEventCreate(&c->tr1[i])) != hipSuccess) {
+            const int rc = hip_fail(nullptr, e, "ort_create: events");
+            ort_destroy(c);
+            return rc;
+        }
     }
     *out = c;
     return ORT_OK;
@@ -796,7 +807,10 @@ int ort_destroy(ort_ctx* ctx) {
     for (DevBuf* b : pipe) free_buf(*b);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
-    if (ctx->ev_trace) (void)hipEventDestroy(ctx->ev_trace);
+    for (int i = 0; i < ort_ctx::kRing; ++i) {
+        if (ctx->tr0[i]) (void)hipEventDestroy(ctx->tr0[i]);
+        if (ctx->tr1[i]) (void)hipEventDestroy(ctx->tr1[i]);
+    }
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return ORT_OK;
@@ -899,10 +913,20 @@ int ort_last_kernel_ms(ort_ctx* ctx, float* ms) {
 
 int ort_last_trace_ms(ort_ctx* ctx, float* ms) {
     if (!ctx || !ms) return fail(nullptr, ORT_ERR_INVALID_ARG, "ort_last_trace_ms: null argument");
-    if (!ctx->timed) return fail(ctx, ORT_ERR_NO_SCENE, "no kernel launched yet");
-    HIPCHK(ctx, hipEventSynchronize(ctx->ev1));
-    HIPCHK(ctx, hipEventElapsedTime(ms, ctx->ev0, ctx->ev_trace));
-    return ORT_OK;
+    return ort_trace_times_ms(ctx, 1, ms) == 1 ? ORT_OK : fail(ctx, ORT_ERR_NO_SCENE, "no trace kernel timed yet");
+}
+
+int ort_trace_times_ms(ort_ctx* ctx, int n, float* ms) {
+    if (!ctx || !ms || n < 0) return -ORT_ERR_INVALID_ARG;
+    const long long have = std::min<long long>(ctx->frames, ort_ctx::kRing);
+    const int k = (int)std::min<long long>(n, have);
+    for (int i = 0; i < k; ++i) {
+        const int slot = (int)((ctx->frames - k + i) % ort_ctx::kRing);
+        if (hipEventSynchronize(ctx->tr1[slot]) != hipSuccess ||
+            hipEventElapsedTime(&ms[i], ctx->tr0[slot], ctx->tr1[slot]) != hipSuccess)
+            return -ORT_ERR_HIP;
+    }
+    return k;
 }
 
 int ort_count_traffic(ort_ctx* ctx, const ort_params* params, const ort_tile* tile, uint64_t* counts) {

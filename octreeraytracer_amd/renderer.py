@@ -174,10 +174,18 @@ class Renderer:
         return ms.value
 
     def last_trace_ms(self) -> float:
-        """Start of the last frame to the end of its first trace kernel (the dominant kernel)."""
+        """First trace kernel of the last frame (camera rays + octree walk; the dominant kernel)."""
         ms = C.c_float()
         self._check(self._lib.ort_last_trace_ms(self._ctx, C.byref(ms)))
         return ms.value
+
+    def trace_times_ms(self, n: int) -> list:
+        """Trace-kernel durations (ms) of the last n frames (n <= 64), oldest first."""
+        buf = (C.c_float * max(1, n))()
+        k = self._lib.ort_trace_times_ms(self._ctx, int(n), buf)
+        if k < 0:
+            L.check(-k, self._ctx)
+        return [buf[i] for i in range(k)]
 
     def count_traffic(self, params: FrameParams, tile: Tile | None = None) -> dict:
         tile = tile or Tile.full(params)

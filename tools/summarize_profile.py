@@ -7,7 +7,7 @@ from collections import defaultdict
 from pathlib import Path
 
 src, dst = Path(sys.argv[1]), Path(sys.argv[2])
-KERNEL = sys.argv[3] if len(sys.argv) > 3 else "ort_trace_kernel<0, false, true>"
+KERNEL = sys.argv[3] if len(sys.argv) > 3 else "ort_trace_compact<false, true>"
 
 stats = {}
 ks = next(src.glob("trace/*kernel_stats.csv"), None)
@@ -58,6 +58,15 @@ if "GRBM_GUI_ACTIVE" in per_launch and avg_ns:
     d["effective_clock_GHz"] = per_launch["GRBM_GUI_ACTIVE"] / 8 / avg_ns
 res["derived"] = d
 dst.parent.mkdir(parents=True, exist_ok=True)
+# traffic record consumed by bench.py (roofline.traffic) for the bench config
+if len(sys.argv) > 4 and "hbm_bytes_per_launch" in d:
+    cfg, rows = sys.argv[4].split(":")
+    (dst.parent / "pmc_traffic.json").write_text(json.dumps({
+        "config": cfg, "tile_rows": int(rows), "kernel": KERNEL,
+        "hbm_bytes_per_launch": d["hbm_bytes_per_launch"],
+        "method": "rocprofv3 separate --pmc passes: FETCH_SIZE*1024*2 (gfx950: FETCH_SIZE reads 1/2 of the "
+                  "bytes, MI355X_MICROARCH.md HBM) + WRITE_SIZE*1024, averaged over launches",
+        "source": str(src)}, indent=1))
 Path(str(dst) + ".json").write_text(json.dumps(res, indent=1))
 lines = [f"# rocprofv3 summary: {src.name}", "", "## kernel stats (kernel trace of bench.py)", "",
          "| kernel | calls | avg ns | min ns | max ns | % |", "|---|---|---|---|---|---|"]
