@@ -91,6 +91,7 @@ bool buildCompactLayout(const SceneInput& in, int maxDepth, CompactLayout& out, 
     // Pass 2: the split-plane tables, checked against every reachable node's stored box.
     const size_t P1 = ((size_t)1 << D) + 1;
     out.depth = D;
+    out.ordered = true;
     out.planes.assign(3 * P1, 0.0f);
     std::vector<uint8_t> set(3 * P1, 0);
     for (int32_t i : order) {
@@ -101,6 +102,7 @@ bool buildCompactLayout(const SceneInput& in, int maxDepth, CompactLayout& out, 
             const size_t hi = a * P1 + ((size_t)(c[a] + 1) << s);
             const float vlo = in.node_min[3 * (size_t)i + a];
             const float vhi = in.node_max[3 * (size_t)i + a];
+            if (!(vlo <= vhi)) out.ordered = false;  // also false for NaN
             if (!set[lo]) { out.planes[lo] = vlo; set[lo] = 1; }
             else if (!same_bits(out.planes[lo], vlo)) { why = "node box not derivable from split planes"; return false; }
             if (!set[hi]) { out.planes[hi] = vhi; set[hi] = 1; }

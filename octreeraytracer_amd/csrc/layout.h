@@ -48,6 +48,10 @@ struct CompactLayout {
     std::vector<uint32_t> node;    // 2 per node
     std::vector<float> leaf_sph;   // 4 per index entry
     std::vector<int32_t> leaf_idx; // 1 per index entry
+    // Every reachable box has min <= max and no NaN coordinate: then the plane tables are
+    // monotone and the kernel's sign-decided fast walk applies; otherwise every ray takes
+    // the exact (GLSL min/max) walk.
+    bool ordered = true;
 };
 
 // Validates the scene like the reference would need (index ranges); returns "" or a message.

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cstring>
 #include <new>
 #include <string>
@@ -69,14 +70,15 @@ __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t
 
 constexpr size_t kRankLutBytes = 8 * 256;  // ort::rank_lut_entry table
 
-size_t lds_bytes(int mode, int depth) {
+// with_tm: the exact walk also keeps a per-level tmin column; the fast walk needs none.
+size_t lds_bytes(int mode, int depth, bool with_tm) {
     if (mode != 0) return 0;
     const size_t planes = align16(sizeof(float) * 3 * (((size_t)1 << depth) + 1));
     const size_t levels = (size_t)std::max(depth, 1);
-    return planes + kRankLutBytes + 2 * levels * kBlock * sizeof(int);
+    return planes + kRankLutBytes + (with_tm ? 2 : 1) * levels * kBlock * sizeof(int);
 }
 
-// LDS image of one workgroup: split planes | rank LUT | frame columns (co, tmin).
+// LDS image of one workgroup: split planes | rank LUT | frame columns (co[, tmin]).
 struct LdsView {
     const float* planes;
     const uint8_t* lut;
@@ -201,7 +203,7 @@ __global__ void __launch_bounds__(kBlock) ort_trace_persistent(PipeArgs A) {
                     const ort::Ray ray = load_ray(A, cand, alive);
                     if (alive) {
                         const ort::V3 inv = ort::mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
-                        if (A.exact_only || !ort::fast_path_ok(inv)) {
+                        if (A.exact_only || !ort::fast_path_ok(ray, inv, 0.001f, ORT_MAXFLOAT)) {
                             A.defer_list[atomicAdd(A.sync, 1)] = cand;
                         } else {
                             if (COUNT) cnt.v[5] += 1;
@@ -215,7 +217,7 @@ __global__ void __launch_bounds__(kBlock) ort_trace_persistent(PipeArgs A) {
             continue;
         }
         if (k >= 0) {
-            if (ort::fast_step<COUNT>(A.S, L.planes, lut, st, L.fr, cnt)) {
+            if (ort::fast_step<COUNT>(A.S, lut, st, L.fr, cnt)) {
                 A.hit[k] = make_int2(st.hit ? st.hitEntry : -1, __float_as_int(st.closest));
                 k = -1;
             }
@@ -254,8 +256,9 @@ __device__ inline ort::Ray slot_ray(const PipeArgs& A, int k, bool& alive) {
 
 // One ray per lane over the compact layout (default): the tile-block order of the path
 // slots keeps each wave on an 8x8 pixel block, whose rays walk nearly the same nodes.
-template <bool COUNT, bool PRIMARY>
-__global__ void __launch_bounds__(kBlock) ort_trace_compact(PipeArgs A) {
+// DEEP: trees deeper than 8 levels need the 96-bit level masks.
+template <bool COUNT, bool PRIMARY, bool DEEP>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) ort_trace_compact(PipeArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     LdsView L = setup_lds<true>(smem, A.S);
     const int k = blockIdx.x * kBlock + threadIdx.x;
@@ -265,14 +268,16 @@ __global__ void __launch_bounds__(kBlock) ort_trace_compact(PipeArgs A) {
     ort::Counters cnt;
     for (int q = 0; q < 6; ++q) cnt.v[q] = 0;
     const ort::V3 inv = ort::mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
-    if (A.exact_only || !ort::fast_path_ok(inv)) {
+    if (A.exact_only || !ort::fast_path_ok(ray, inv, 0.001f, ORT_MAXFLOAT)) {
         A.defer_list[atomicAdd(A.sync, 1)] = k;
         return;
     }
     if (COUNT) cnt.v[5] += 1;
     float t = 0.0f;
     int entry = -1;
-    const bool hit = ort::traverse_fast<COUNT>(A.S, L.planes, L.lut, ray, inv, 0.001f, ORT_MAXFLOAT, entry, t, L.fr, cnt);
+    using Masks = typename std::conditional<DEEP, ort::Masks96, ort::Masks64>::type;
+    const bool hit = ort::traverse_fast_t<COUNT, Masks>(A.S, L.planes, L.lut, ray, inv, 0.001f, ORT_MAXFLOAT, entry, t,
+                                                        L.fr, cnt);
     A.hit[k] = make_int2(hit ? entry : -1, __float_as_int(t));
     flush_counts<COUNT>(cnt, A.counters);
 }
@@ -437,6 +442,7 @@ struct ort_ctx {
     bool has_scene = false;
     int layout = ORT_LAYOUT_EXPLICIT;
     int depth = 0;
+    bool ordered = true;  // compact layout: fast walk allowed (CompactLayout::ordered)
     int32_t n_spheres = 0, n_nodes = 0;
     int64_t n_indices = 0;
     DevBuf sph_cr, sph_ma, sph_fr;
@@ -518,6 +524,7 @@ int upload_impl(ort_ctx* ctx, const ort::SceneInput& in) {
         if (compact_ok) {
             ctx->layout = ORT_LAYOUT_COMPACT;
             ctx->depth = cl.depth;
+            ctx->ordered = cl.ordered;
             if ((rc = upload(ctx, ctx->node, cl.node.data(), 4 * cl.node.size()))) return rc;
             if ((rc = upload(ctx, ctx->leaf_sph, cl.leaf_sph.data(), 4 * cl.leaf_sph.size()))) return rc;
             if ((rc = upload(ctx, ctx->leaf_idx, cl.leaf_idx.data(), 4 * cl.leaf_idx.size()))) return rc;
@@ -614,7 +621,9 @@ int ensure(ort_ctx* ctx, DevBuf& b, size_t bytes) {
 template <bool COUNT, bool PRIMARY>
 hipError_t launch_trace_p(int mode, const PipeArgs& a, int blocks, int pblocks, size_t lds, hipStream_t s) {
     if (mode == 0 && pblocks > 0) hipLaunchKernelGGL((ort_trace_persistent<COUNT>), dim3(pblocks), dim3(kBlock), lds, s, a);
-    else if (mode == 0) hipLaunchKernelGGL((ort_trace_compact<COUNT, PRIMARY>), dim3(blocks), dim3(kBlock), lds, s, a);
+    else if (mode == 0 && a.S.depth > 8)
+        hipLaunchKernelGGL((ort_trace_compact<COUNT, PRIMARY, true>), dim3(blocks), dim3(kBlock), lds, s, a);
+    else if (mode == 0) hipLaunchKernelGGL((ort_trace_compact<COUNT, PRIMARY, false>), dim3(blocks), dim3(kBlock), lds, s, a);
     else if (mode == 1) hipLaunchKernelGGL((ort_trace_kernel<1, COUNT, PRIMARY>), dim3(blocks), dim3(kBlock), 0, s, a);
     else hipLaunchKernelGGL((ort_trace_kernel<2, COUNT, PRIMARY>), dim3(blocks), dim3(kBlock), 0, s, a);
     return hipGetLastError();
@@ -693,7 +702,7 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     a.tm = {t->x0, t->width, t->y0, t->rows, t->band_height, t->band_stride};
     a.tilesX = tilesX;
     a.total = (int)slots;
-    a.exact_only = ctx->exact_only;
+    a.exact_only = ctx->exact_only || !ctx->ordered;
     a.refill = ctx->refill;
     a.hit = (int2*)ctx->hit.p;
     a.defer_list = (int*)ctx->defer_list.p;
@@ -705,7 +714,8 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     a.pcol = (float4*)ctx->pcol.p;
     a.out = dout;
     a.counters = dcounters;
-    const size_t lds = lds_bytes(mode, ctx->depth);
+    const size_t lds = lds_bytes(mode, ctx->depth, false);
+    const size_t lds_exact = lds_bytes(mode, ctx->depth, true);
     const int pblocks = (mode == 0 && ctx->persistent) ? persistent_blocks(ctx->device, dcounters != nullptr, lds, blocks) : 0;
     const int exact_blocks = 1024;
     hipError_t e;
@@ -737,10 +747,10 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                 }
                 if (mode == 0) {
                     const bool prim = (b == 0) && pblocks == 0;
-                    if (dcounters && prim) hipLaunchKernelGGL((ort_trace_exact<true, true>), dim3(exact_blocks), dim3(kBlock), lds, s, a);
-                    else if (dcounters) hipLaunchKernelGGL((ort_trace_exact<true, false>), dim3(exact_blocks), dim3(kBlock), lds, s, a);
-                    else if (prim) hipLaunchKernelGGL((ort_trace_exact<false, true>), dim3(exact_blocks), dim3(kBlock), lds, s, a);
-                    else hipLaunchKernelGGL((ort_trace_exact<false, false>), dim3(exact_blocks), dim3(kBlock), lds, s, a);
+                    if (dcounters && prim) hipLaunchKernelGGL((ort_trace_exact<true, true>), dim3(exact_blocks), dim3(kBlock), lds_exact, s, a);
+                    else if (dcounters) hipLaunchKernelGGL((ort_trace_exact<true, false>), dim3(exact_blocks), dim3(kBlock), lds_exact, s, a);
+                    else if (prim) hipLaunchKernelGGL((ort_trace_exact<false, true>), dim3(exact_blocks), dim3(kBlock), lds_exact, s, a);
+                    else hipLaunchKernelGGL((ort_trace_exact<false, false>), dim3(exact_blocks), dim3(kBlock), lds_exact, s, a);
                     if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "ort_trace_exact launch");
                 }
             }
@@ -1019,7 +1029,7 @@ int ort_debug_emulate_render(const float* cr, const float* ma, const float* fr, 
         for (int k = 0; k < 6; ++k) total.v[k] = 0;
         std::vector<uint8_t> lut(kRankLutBytes);
         for (size_t i = 0; i < lut.size(); ++i) lut[i] = ort::rank_lut_entry((uint32_t)i >> 8, (uint32_t)i & 255u);
-        const uint8_t* rank_lut = (layout == ORT_LAYOUT_COMPACT) ? lut.data() : nullptr;
+        const uint8_t* rank_lut = (layout == ORT_LAYOUT_COMPACT && cl.ordered) ? lut.data() : nullptr;
         std::vector<int> snode(ORT_MAX_STACK);
         std::vector<float> stmin(ORT_MAX_STACK);
         ort::LocalFrames lf;

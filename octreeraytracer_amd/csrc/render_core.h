@@ -51,6 +51,7 @@ struct V3 {
     float x, y, z;
 };
 ORT_FN int f2i(float f) { int i; __builtin_memcpy(&i, &f, 4); return i; }
+ORT_FN uint32_t f2u(float f) { uint32_t i; __builtin_memcpy(&i, &f, 4); return i; }
 ORT_FN V3 mk(float x, float y, float z) { V3 r; r.x = x; r.y = y; r.z = z; return r; }
 ORT_FN V3 add(V3 a, V3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
 ORT_FN V3 sub(V3 a, V3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
@@ -184,6 +185,7 @@ struct LdsFrames {
     int stride;
     int lane;
     ORT_FN void set(int L, int c, float t) { co[L * stride + lane] = c; tm[L * stride + lane] = t; }
+    ORT_FN void setCo(int L, int c) { co[L * stride + lane] = c; }
     ORT_FN int getCo(int L) const { return co[L * stride + lane]; }
     ORT_FN float getTm(int L) const { return tm[L * stride + lane]; }
 };
@@ -191,6 +193,7 @@ struct LocalFrames {
     int co[ORT_COMPACT_MAX_DEPTH + 1];
     float tm[ORT_COMPACT_MAX_DEPTH + 1];
     ORT_FN void set(int L, int c, float t) { co[L] = c; tm[L] = t; }
+    ORT_FN void setCo(int L, int c) { co[L] = c; }
     ORT_FN int getCo(int L) const { return co[L]; }
     ORT_FN float getTm(int L) const { return tm[L]; }
 };
@@ -340,21 +343,32 @@ ORT_FN bool traverse_compact(const KScene& S, const float* planes, const Ray& r,
 // component, i.e. 1/d is finite on every axis.  Then no slab value can be NaN and, per
 // axis, t(p) = inv*(p - o) is monotone in p, so every GLSL min/max of the reference is
 // decided by the sign of d alone:
-//   * the entry/exit of a child slab are its near/far planes' t (no compare needed);
+//   * the entry/exit of a child slab are its near/far planes' t (no compare needed); the
+//     plane tables are read in ray order (index i -> table[g ? 2^D - i : i], g = d < 0), so
+//     a node's near plane is its lower ray-order index and rank bit = "far half";
 //   * the traversal order (glsl:352-447) of an all-non-zero sign vector is
 //     order[r] = perm(r) ^ m, m = (d.z<0)<<2 | (d.x<0)<<1 | (d.y<0), perm = identity for
 //     d.x > 0 and "swap bits 0,1" for d.x < 0 (checked for all 8 tables), so children are
 //     evaluated directly in traversal-rank space with static role axes
-//     A = rank bit 1 (x, or y when swapped), B = rank bit 0, C = rank bit 2 (z), and
-//     rank bit 0 = near half along that axis;
+//     A = rank bit 1 (x, or y when swapped), B = rank bit 0, C = rank bit 2 (z);
 //   * IEEE max3/min3 equal the GLSL chains (no NaN); a +0/-0 tie can pick the other zero,
 //     which is harmless because every tmin is only ever compared (never divided by).
-// The pushed tmin of a child is max(childTMin, node_tmin) = max(max3(entries), node_tmin),
-// and the reference's push test (tmax >= tmin && !(tmax < node_tmin) && !(tmin > closest))
-// becomes min(tmax, FLT_MAX) >= that value.  Results are bit-identical to the exact walk
+// The reference pushes max(childTMin, node_tmin).  A child box lies inside its parent's
+// (midpoint splits; checked at upload, layout.cpp), so its entry t on every axis is >= the
+// parent's (fl is monotone), hence by induction node_tmin = max(max3(entries), t_min) for
+// every node below the root: no per-level tmin has to be kept, and the push test
+// (tmax >= tmin && !(tmax < node_tmin) && !(tmin > closest)) becomes
+// min(tmax, t_max) >= max(tmin, t_min).  Results are bit-identical to the exact walk
 // (tests/test_emulation.py forces both on the same rays).
 //
-// rank_lut[m*256 + childMask] maps the node's octant-space child mask to rank space.
+// Stack: the reference stack holds exactly the unvisited surviving siblings of every
+// ancestor in traversal order, i.e. per tree level a set of ranks plus the level's children
+// offset.  Ranks are kept as "rank-reversed" bytes (rank r of level L = bit 8L + 7 - r) so the
+// next node -- lowest rank of the deepest non-empty level -- is the highest set bit, and a
+// descent is the same pop as a backtrack: every visited internal node pushes all its
+// surviving children, then one uniform pop picks the next node.
+//
+// rank_lut[m*256 + childMask] maps the node's octant-space child mask to reversed rank space.
 ORT_FN uint32_t rank_perm(uint32_t r, uint32_t m) {
     const uint32_t swap = (m >> 1) & 1u;  // perm = swap bits 0,1 when d.x < 0
     const uint32_t p = swap ? ((r & 4u) | ((r & 1u) << 1) | ((r >> 1) & 1u)) : r;
@@ -363,43 +377,116 @@ ORT_FN uint32_t rank_perm(uint32_t r, uint32_t m) {
 ORT_FN uint8_t rank_lut_entry(uint32_t m, uint32_t cmask) {
     uint32_t out = 0;
     for (uint32_t r = 0; r < 8; ++r)
-        if ((cmask >> rank_perm(r, m)) & 1u) out |= 1u << r;
+        if ((cmask >> rank_perm(r, m)) & 1u) out |= 0x80u >> r;
     return (uint8_t)out;
 }
 
-ORT_FN bool fast_path_ok(V3 inv) {
-    return fabsf(inv.x) <= ORT_MAXFLOAT && fabsf(inv.y) <= ORT_MAXFLOAT && fabsf(inv.z) <= ORT_MAXFLOAT;
+// The fast walk's preconditions: finite 1/d and origin (no slab value can be NaN), a
+// positive t_min and finite t_max (the push test below relies on both).
+ORT_FN bool fast_path_ok(const Ray& r, V3 inv, float t_min, float t_max) {
+    return fabsf(inv.x) <= ORT_MAXFLOAT && fabsf(inv.y) <= ORT_MAXFLOAT && fabsf(inv.z) <= ORT_MAXFLOAT &&
+           fabsf(r.o.x) <= ORT_MAXFLOAT && fabsf(r.o.y) <= ORT_MAXFLOAT && fabsf(r.o.z) <= ORT_MAXFLOAT &&
+           t_min > 0.0f && t_max <= ORT_MAXFLOAT;
 }
 
+// 24-bit signed multiply (plane indices are < 2^11): one full-rate VALU op on the device.
+ORT_FN int imul24(int a, int b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __mul24(a, b);
+#else
+    return a * b;
+#endif
+}
+
+// min/max for NaN-free operands.  On the device these are the raw VALU instructions: the
+// libm-style fmaxf would first canonicalise every operand the compiler cannot prove
+// canonical (one v_max x,x each), which the fast walk never needs.
+#if defined(__HIP_DEVICE_COMPILE__)
+ORT_FN float fmax2(float a, float b) { float r; asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); return r; }
+ORT_FN float fmin2(float a, float b) { float r; asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); return r; }
+ORT_FN float fmax3(float a, float b, float c) {
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+ORT_FN float fmin3(float a, float b, float c) {
+    float r;
+    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+#else
+ORT_FN float fmax2(float a, float b) { return fmaxf(a, b); }
+ORT_FN float fmin2(float a, float b) { return fminf(a, b); }
 ORT_FN float fmax3(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
 ORT_FN float fmin3(float a, float b, float c) { return fminf(fminf(a, b), c); }
+#endif
+
+// Rank-reversed level masks (see above).  pop() returns hb = 8L + 7 - rank.
+struct Masks64 {  // levels 0..7: trees of depth <= 8
+    uint64_t m;
+    ORT_FN void clear() { m = 0; }
+    ORT_FN bool empty() const { return m == 0; }
+    ORT_FN void put(int L, uint32_t rev) { m |= (uint64_t)rev << (8 * L); }
+    ORT_FN int pop() {
+        const int hb = 63 - __builtin_clzll(m);
+        m ^= (uint64_t)1 << hb;
+        return hb;
+    }
+};
+struct Masks96 {  // levels 0..11
+    uint64_t lo;
+    uint32_t hi;
+    ORT_FN void clear() { lo = 0; hi = 0; }
+    ORT_FN bool empty() const { return (lo | hi) == 0; }
+    ORT_FN void put(int L, uint32_t rev) {
+        if (L < 8) lo |= (uint64_t)rev << (8 * L);
+        else hi |= rev << (8 * (L - 8));
+    }
+    ORT_FN int pop() {
+        if (hi) {
+            const int hb = 31 - __builtin_clz(hi);
+            hi ^= 1u << hb;
+            return 64 + hb;
+        }
+        const int hb = 63 - __builtin_clzll(lo);
+        lo ^= (uint64_t)1 << hb;
+        return hb;
+    }
+};
 
 // Resumable per-lane state of the fast walk (so a persistent kernel can interleave rays).
-struct FastState {
+template <class Masks>
+struct FastStateT {
     Ray r;           // original-axis ray (Sphere_hit uses it as is)
     float a;         // dot(d, d)
     float oA, oB, oC, iA, iB, iC;  // role-axis origin / 1/d
+    const float* pA;  // ray-order plane table of each role axis: plane(i) = pA[sA * i]
+    const float* pB;
+    const float* pC;
+    int sA, sB, sC;
     float tNA, tFA, tNB, tFB, tNC, tFC;  // near/far plane t of the current node's box
-    uint32_t cA, cB, cC;  // cell of the current node (original-axis cell indices)
-    uint32_t flags;  // bit0 gA, bit1 gB, bit2 gC (axis points negative); bits 4-6 m; bit 8 swap
+    int cA, cB, cC;  // ray-order index of the current node's near plane
+    uint32_t otab;   // nibble r = octant of rank r
+    uint32_t m;      // order xor (rank LUT row)
     int node, depth;
-    float ntmin, closest;
+    float tmin0, closest;
     int hitEntry;
     bool hit;
-    LevelMasks masks;
+    Masks masks;
 };
+using FastState = FastStateT<Masks96>;
 
 // Root test and state setup (glsl:296-311).  Returns false when the root box is missed.
+template <class Masks>
 ORT_FN bool fast_begin(const KScene& S, const float* planes, const Ray& r, V3 inv, float t_min, float t_max,
-                       FastState& st) {
+                       FastStateT<Masks>& st) {
     const int D = S.depth;
-    const int P1 = (1 << D) + 1;
+    const int top = 1 << D;
+    const int P1 = top + 1;
     const uint32_t nx = r.d.x < 0.0f, ny = r.d.y < 0.0f, nz = r.d.z < 0.0f;
     const uint32_t m = (nz << 2) | (nx << 1) | ny;
     const bool swap = nx != 0;
-    const float* PA = planes + (swap ? P1 : 0);
-    const float* PB = planes + (swap ? 0 : P1);
-    const float* PC = planes + 2 * P1;
+    const uint32_t gA = swap ? ny : nx, gB = swap ? nx : ny, gC = nz;
     st.r = r;
     st.a = dot(r.d, r.d);
     st.oA = swap ? r.o.y : r.o.x;
@@ -408,19 +495,26 @@ ORT_FN bool fast_begin(const KScene& S, const float* planes, const Ray& r, V3 in
     st.iA = swap ? inv.y : inv.x;
     st.iB = swap ? inv.x : inv.y;
     st.iC = inv.z;
-    const uint32_t gA = swap ? ny : nx, gB = swap ? nx : ny, gC = nz;
-    st.flags = gA | (gB << 1) | (gC << 2) | (m << 4) | ((uint32_t)swap << 8);
-    const int top = 1 << D;
-    st.tNA = st.iA * ((gA ? PA[top] : PA[0]) - st.oA);
-    st.tFA = st.iA * ((gA ? PA[0] : PA[top]) - st.oA);
-    st.tNB = st.iB * ((gB ? PB[top] : PB[0]) - st.oB);
-    st.tFB = st.iB * ((gB ? PB[0] : PB[top]) - st.oB);
-    st.tNC = st.iC * ((gC ? PC[top] : PC[0]) - st.oC);
-    st.tFC = st.iC * ((gC ? PC[0] : PC[top]) - st.oC);
+    st.pA = planes + (swap ? P1 : 0) + (gA ? top : 0);
+    st.pB = planes + (swap ? 0 : P1) + (gB ? top : 0);
+    st.pC = planes + 2 * P1 + (gC ? top : 0);
+    st.sA = gA ? -1 : 1;
+    st.sB = gB ? -1 : 1;
+    st.sC = gC ? -1 : 1;
+    uint32_t ot = 0;
+    for (uint32_t k = 0; k < 8; ++k) ot |= rank_perm(k, m) << (4 * k);
+    st.otab = ot;
+    st.m = m;
+    st.tNA = st.iA * (st.pA[0] - st.oA);
+    st.tFA = st.iA * (st.pA[st.sA * top] - st.oA);
+    st.tNB = st.iB * (st.pB[0] - st.oB);
+    st.tFB = st.iB * (st.pB[st.sB * top] - st.oB);
+    st.tNC = st.iC * (st.pC[0] - st.oC);
+    st.tFC = st.iC * (st.pC[st.sC * top] - st.oC);
+    st.cA = st.cB = st.cC = 0;
     st.node = 0;
     st.depth = 0;
-    st.cA = st.cB = st.cC = 0;
-    st.ntmin = t_min;
+    st.tmin0 = t_min;
     st.closest = t_max;
     st.hitEntry = -1;
     st.hit = false;
@@ -428,19 +522,11 @@ ORT_FN bool fast_begin(const KScene& S, const float* planes, const Ray& r, V3 in
     return fmin3(st.tFA, st.tFB, st.tFC) >= fmax3(st.tNA, st.tNB, st.tNC);
 }
 
-// One node of the walk: visit st.node, then descend or backtrack to the next node.
-// Returns true when the walk is over (hit found, or stack exhausted).
-template <bool COUNT, class Frames>
-ORT_FN bool fast_step(const KScene& S, const float* planes, const uint8_t* rank_lut, FastState& st, Frames& fr,
-                      Counters& cnt) {
+// One node of the walk: visit st.node (push its surviving children, or test its spheres),
+// then pop the next node.  Returns true when the walk is over (hit found, or stack empty).
+template <bool COUNT, class Masks, class Frames>
+ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks>& st, Frames& fr, Counters& cnt) {
     const int D = S.depth;
-    const int P1 = (1 << D) + 1;
-    const uint32_t gA = st.flags & 1u, gB = (st.flags >> 1) & 1u, gC = (st.flags >> 2) & 1u;
-    const uint32_t m = (st.flags >> 4) & 7u;
-    const bool swap = (st.flags >> 8) & 1u;
-    const float* PA = planes + (swap ? P1 : 0);
-    const float* PB = planes + (swap ? 0 : P1);
-    const float* PC = planes + 2 * P1;
     const uint2 rec = S.node[st.node];
     if (COUNT) cnt.v[0] += 1;
     if (rec.y & ORT_INTERNAL_FLAG) {
@@ -449,65 +535,45 @@ ORT_FN bool fast_step(const KScene& S, const float* planes, const uint8_t* rank_
             const long long rem = (long long)S.n_nodes - (long long)co;
             cnt.v[1] += (unsigned long long)(rem >= 8 ? 8 : (rem > 0 ? rem : 0));
         }
-        const uint32_t rcm = rank_lut[m * 256u + (rec.y & 0xffu)];
-        const int s = D - st.depth;
-        const float tMA = st.iA * (PA[(2 * st.cA + 1) << (s - 1)] - st.oA);
-        const float tMB = st.iB * (PB[(2 * st.cB + 1) << (s - 1)] - st.oB);
-        const float tMC = st.iC * (PC[(2 * st.cC + 1) << (s - 1)] - st.oC);
+        const uint32_t rcm = rank_lut[st.m * 256u + (rec.y & 0xffu)];
+        const int h = (1 << (D - st.depth)) >> 1;  // half the node width, in plane steps
+        const float tMA = st.iA * (st.pA[imul24(st.sA, st.cA + h)] - st.oA);
+        const float tMB = st.iB * (st.pB[imul24(st.sB, st.cB + h)] - st.oB);
+        const float tMC = st.iC * (st.pC[imul24(st.sC, st.cC + h)] - st.oC);
         const float tNA = st.tNA, tNB = st.tNB, tNC = st.tNC, tFA = st.tFA, tFB = st.tFB, tFC = st.tFC;
-        const float ntmin = st.ntmin;
-        // entry: near child (rank bit 0) enters at tN, far child at tM; exit: tM / tF
-        const float e00 = fmaxf(tNA, tNB), e01 = fmaxf(tNA, tMB), e10 = fmaxf(tMA, tNB), e11 = fmaxf(tMA, tMB);
-        const float x00 = fminf(tMA, tMB), x01 = fminf(tMA, tFB), x10 = fminf(tFA, tMB), x11 = fminf(tFA, tFB);
-        const float cN = fminf(tMC, ORT_MAXFLOAT), cF = fminf(tFC, ORT_MAXFLOAT);
-        uint32_t rm = 0;
-#define ORT_CHILD(R, EAB, XAB, EC, XC)                 \
-    {                                                  \
-        const float mm = fmax3(EAB, EC, ntmin);        \
-        const float xx = fmin3(XAB, XC, ORT_MAXFLOAT); \
-        rm |= (xx >= mm) ? (1u << (R)) : 0u;           \
-    }
-        ORT_CHILD(0, e00, x00, tNC, cN)
-        ORT_CHILD(1, e01, x01, tNC, cN)
-        ORT_CHILD(2, e10, x10, tNC, cN)
-        ORT_CHILD(3, e11, x11, tNC, cN)
-        ORT_CHILD(4, e00, x00, tMC, cF)
-        ORT_CHILD(5, e01, x01, tMC, cF)
-        ORT_CHILD(6, e10, x10, tMC, cF)
-        ORT_CHILD(7, e11, x11, tMC, cF)
+        // entry: near child (rank bit clear) enters at tN, far child at tM; exit: tM / tF
+        const float e00 = fmax2(tNA, tNB), e01 = fmax2(tNA, tMB), e10 = fmax2(tMA, tNB), e11 = fmax2(tMA, tMB);
+        const float x00 = fmin2(tMA, tMB), x01 = fmin2(tMA, tFB), x10 = fmin2(tFA, tMB), x11 = fmin2(tFA, tFB);
+        const float nN = fmax2(tNC, st.tmin0), nF = fmax2(tMC, st.tmin0);
+        const float cN = fmin2(tMC, st.closest), cF = fmin2(tFC, st.closest);  // closest == t_max here
+        // keep child R <=> exit >= entry, with entry >= t_min > 0 and exit <= t_max finite, so
+        // exit - entry is never NaN and is +0 when equal: its sign bit is "drop".  The drop
+        // bits are shifted in rank order (rank 0 ends at bit 7: the reversed layout) -- one
+        // v_sub + one v_alignbit per child, no compare/select.
+        uint32_t drop = 0;
+#define ORT_CHILD(R, EAB, XAB, EC, XC) drop = (drop << 1) | (f2u(fmin2(XAB, XC) - fmax2(EAB, EC)) >> 31);
+        ORT_CHILD(0, e00, x00, nN, cN)
+        ORT_CHILD(1, e01, x01, nN, cN)
+        ORT_CHILD(2, e10, x10, nN, cN)
+        ORT_CHILD(3, e11, x11, nN, cN)
+        ORT_CHILD(4, e00, x00, nF, cF)
+        ORT_CHILD(5, e01, x01, nF, cF)
+        ORT_CHILD(6, e10, x10, nF, cF)
+        ORT_CHILD(7, e11, x11, nF, cF)
 #undef ORT_CHILD
-        rm &= rcm;
-        if (rm) {
-            const int rk = __builtin_ctz(rm);
-            const uint32_t rest = rm & (rm - 1u);
-            if (rest) {
-                st.masks.put(st.depth, rest);
-                fr.set(st.depth, co, ntmin);
-            }
-            const uint32_t bA = (rk >> 1) & 1u, bB = rk & 1u, bC = (rk >> 2) & 1u;
-            const float eA = bA ? tMA : tNA, eB = bB ? tMB : tNB, eC = bC ? tMC : tNC;
-            st.ntmin = fmax3(fmaxf(eA, eB), eC, ntmin);
-            st.tFA = bA ? tFA : tMA;
-            st.tNA = eA;
-            st.tFB = bB ? tFB : tMB;
-            st.tNB = eB;
-            st.tFC = bC ? tFC : tMC;
-            st.tNC = eC;
-            st.cA = 2 * st.cA + (bA ^ gA);
-            st.cB = 2 * st.cB + (bB ^ gB);
-            st.cC = 2 * st.cC + (bC ^ gC);
-            st.node = co + (int)rank_perm((uint32_t)rk, m);
-            st.depth += 1;
-            return false;
-        }
+        // level depth holds nothing yet (every deeper level is empty), so both writes are
+        // harmless when no child survives
+        st.masks.put(st.depth, rcm & ~drop);
+        fr.setCo(st.depth, co);
     } else {
         const int off = (int)rec.x;
         const int n = (int)rec.y;
+        const float ntmin = st.depth == 0 ? st.tmin0 : fmax2(fmax3(st.tNA, st.tNB, st.tNC), st.tmin0);
         for (int i = 0; i < n; ++i) {
             const float4 sp = S.leaf_sph[off + i];
             if (COUNT) cnt.v[2] += 1;
             float t;
-            if (sphere_hit_t(st.r, st.a, sp, st.ntmin, st.closest, t)) {
+            if (sphere_hit_t(st.r, st.a, sp, ntmin, st.closest, t)) {
                 st.hit = true;
                 st.closest = t;
                 st.hitEntry = off + i;
@@ -516,44 +582,44 @@ ORT_FN bool fast_step(const KScene& S, const float* planes, const uint8_t* rank_
         }
         if (st.hit) return true;  // glsl:336: the walk ends after the leaf that produced a hit
     }
-    // backtrack: next child of the deepest level with one left
-    const int L = st.masks.top();
-    if (L < 0) return true;
-    const int rk = st.masks.pop(L);
-    const int sh = st.depth - L;
-    const uint32_t bA = (rk >> 1) & 1u, bB = rk & 1u, bC = (rk >> 2) & 1u;
-    const uint32_t cA = ((st.cA >> sh) << 1) | (bA ^ gA);
-    const uint32_t cB = ((st.cB >> sh) << 1) | (bB ^ gB);
-    const uint32_t cC = ((st.cC >> sh) << 1) | (bC ^ gC);
-    st.cA = cA;
-    st.cB = cB;
-    st.cC = cC;
+    if (st.masks.empty()) return true;
+    // next node: lowest remaining rank of the deepest level with one left
+    const int hb = st.masks.pop();
+    const int L = hb >> 3;
+    const uint32_t rk = (uint32_t)(~hb) & 7u;
+    const int w = 1 << (D - 1 - L);  // child width in plane steps
+    const int keep = -2 * w;         // clears the offsets below the level-L ancestor
+    st.cA = (st.cA & keep) | (((rk >> 1) & 1) ? w : 0);
+    st.cB = (st.cB & keep) | ((rk & 1) ? w : 0);
+    st.cC = (st.cC & keep) | (((rk >> 2) & 1) ? w : 0);
     st.depth = L + 1;
-    st.node = fr.getCo(L) + (int)rank_perm((uint32_t)rk, m);
-    const int s = D - st.depth;
-    const float loA = PA[cA << s], hiA = PA[(cA + 1) << s];
-    const float loB = PB[cB << s], hiB = PB[(cB + 1) << s];
-    const float loC = PC[cC << s], hiC = PC[(cC + 1) << s];
-    st.tNA = st.iA * ((gA ? hiA : loA) - st.oA);
-    st.tFA = st.iA * ((gA ? loA : hiA) - st.oA);
-    st.tNB = st.iB * ((gB ? hiB : loB) - st.oB);
-    st.tFB = st.iB * ((gB ? loB : hiB) - st.oB);
-    st.tNC = st.iC * ((gC ? hiC : loC) - st.oC);
-    st.tFC = st.iC * ((gC ? loC : hiC) - st.oC);
-    st.ntmin = fmax3(fmaxf(st.tNA, st.tNB), st.tNC, fr.getTm(L));
+    st.node = fr.getCo(L) + (int)((st.otab >> (4 * rk)) & 15u);
+    st.tNA = st.iA * (st.pA[imul24(st.sA, st.cA)] - st.oA);
+    st.tFA = st.iA * (st.pA[imul24(st.sA, st.cA + w)] - st.oA);
+    st.tNB = st.iB * (st.pB[imul24(st.sB, st.cB)] - st.oB);
+    st.tFB = st.iB * (st.pB[imul24(st.sB, st.cB + w)] - st.oB);
+    st.tNC = st.iC * (st.pC[imul24(st.sC, st.cC)] - st.oC);
+    st.tFC = st.iC * (st.pC[imul24(st.sC, st.cC + w)] - st.oC);
     return false;
+}
+
+template <bool COUNT, class Masks, class Frames>
+ORT_FN bool traverse_fast_t(const KScene& S, const float* planes, const uint8_t* rank_lut, const Ray& r, V3 inv,
+                            float t_min, float t_max, int& hitEntry, float& hitT, Frames& fr, Counters& cnt) {
+    FastStateT<Masks> st;
+    if (!fast_begin(S, planes, r, inv, t_min, t_max, st)) return false;
+    while (!fast_step<COUNT>(S, rank_lut, st, fr, cnt)) {
+    }
+    hitEntry = st.hitEntry;
+    hitT = st.closest;
+    return st.hit;
 }
 
 template <bool COUNT, class Frames>
 ORT_FN bool traverse_fast(const KScene& S, const float* planes, const uint8_t* rank_lut, const Ray& r, V3 inv,
                           float t_min, float t_max, int& hitEntry, float& hitT, Frames& fr, Counters& cnt) {
-    FastState st;
-    if (!fast_begin(S, planes, r, inv, t_min, t_max, st)) return false;
-    while (!fast_step<COUNT>(S, planes, rank_lut, st, fr, cnt)) {
-    }
-    hitEntry = st.hitEntry;
-    hitT = st.closest;
-    return st.hit;
+    if (S.depth <= 8) return traverse_fast_t<COUNT, Masks64>(S, planes, rank_lut, r, inv, t_min, t_max, hitEntry, hitT, fr, cnt);
+    return traverse_fast_t<COUNT, Masks96>(S, planes, rank_lut, r, inv, t_min, t_max, hitEntry, hitT, fr, cnt);
 }
 
 // Literal restatement of traverseOctree (glsl:290-481) over the reference record layout
@@ -833,7 +899,7 @@ ORT_FN int trace_ray(const KScene& S, const float* planes, const uint8_t* rank_l
     t = 0.0f;
     if (MODE == 0) {
         const V3 inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
-        if (rank_lut && fast_path_ok(inv)) {
+        if (rank_lut && fast_path_ok(r, inv, 0.001f, ORT_MAXFLOAT)) {
             if (COUNT) cnt.v[5] += 1;
             hit = traverse_fast<COUNT>(S, planes, rank_lut, r, inv, 0.001f, ORT_MAXFLOAT, entry, t, fr, cnt);
         } else if (allow_defer) {

@@ -87,3 +87,20 @@ def test_non_derivable_tree_falls_back_to_explicit(ort, oracle, scene_c1):
         emulate_render_host(s, bad, p, layout=L.ORT_LAYOUT_COMPACT)
     img, _ = emulate_render_host(s, bad, p, layout=L.ORT_LAYOUT_EXPLICIT)
     assert same_bits(img, oracle.render(s, bad, p))
+
+
+def test_inverted_or_nan_boxes_take_the_exact_walk(ort, oracle):
+    """A box with min > max (or a NaN coordinate) is still a valid compact layout, but the
+    sign-decided fast walk would misorder its slabs: such scenes take the exact walk."""
+    s = ort.random_spheres(50, 11)
+    t = ort.build_octree(s, 0, 0)  # the root is the only (leaf) node
+    p = ort.FrameParams.default_camera(40, 30, max_depth=2)
+    for bad in ("swap", "nan"):
+        u = ort.FlatOctree(t.node_min.copy(), t.node_max.copy(), t.children_offset, t.objects_offset,
+                           t.object_count, t.object_indices)
+        if bad == "swap":
+            u.node_min[0, 0], u.node_max[0, 0] = t.node_max[0, 0], t.node_min[0, 0]
+        else:
+            u.node_min[0, 2] = np.float32("nan")
+        img, _ = emulate_render_host(s, u, p, layout=L.ORT_LAYOUT_COMPACT)
+        assert same_bits(img, oracle.render(s, u, p)), bad
