@@ -60,6 +60,11 @@ int treeDepth(const SceneInput& in) {
 bool buildCompactLayout(const SceneInput& in, int maxDepth, CompactLayout& out, std::string& why) {
     const int32_t n = in.n_nodes;
     if (n <= 0) { why = "no nodes"; return false; }
+    // the kernel addresses node records and leaf spheres with 32-bit byte offsets
+    if (8 * (uint64_t)n >= ((uint64_t)1 << 32) || 16 * (uint64_t)in.n_indices >= ((uint64_t)1 << 32)) {
+        why = "compact buffers exceed 4 GiB";
+        return false;
+    }
     // Pass 1: BFS for depth and cell coordinates of every reachable node.
     std::vector<int8_t> depth((size_t)n, -1);
     std::vector<uint32_t> cell((size_t)n, 0);  // 10 bits per axis: x | y << 10 | z << 20

@@ -565,6 +565,8 @@ ort::KScene device_scene(const ort_ctx* c) {
     S.n_nodes = c->n_nodes;
     S.node = (const uint2*)c->node.p;
     S.leaf_sph = (const float4*)c->leaf_sph.p;
+    S.node_bytes = (uint32_t)c->node.bytes;
+    S.leaf_bytes = (uint32_t)c->leaf_sph.bytes;
     S.leaf_idx = (const int*)c->leaf_idx.p;
     S.planes = (const float*)c->planes.p;
     S.depth = c->depth;

@@ -92,6 +92,8 @@ struct KScene {
     const int* leaf_idx;     // per entry: sphere index (= objectIndices)
     const float* planes;     // 3 x (2^depth + 1) split-plane coordinates (global copy)
     int depth;               // tree depth D (root = 0)
+    uint32_t node_bytes;     // buffer sizes for the range-checked buffer loads (< 2^32)
+    uint32_t leaf_bytes;
     // explicit (reference) layout
     const float4* nodeA;     // min.xyz, int bits of childrenOffset (binding 3)
     const float4* nodeB;     // max.xyz, int bits of objectsOffset  (binding 4)
@@ -381,12 +383,14 @@ ORT_FN uint8_t rank_lut_entry(uint32_t m, uint32_t cmask) {
     return (uint8_t)out;
 }
 
+ORT_FN bool a_in_qdiv_range(float a) { return a >= 0.125f && a <= 8.0f; }
 // The fast walk's preconditions: finite 1/d and origin (no slab value can be NaN), a
-// positive t_min and finite t_max (the push test below relies on both).
+// positive t_min and finite t_max (the push test below relies on both), dot(d,d) in
+// qdiv's range.
 ORT_FN bool fast_path_ok(const Ray& r, V3 inv, float t_min, float t_max) {
     return fabsf(inv.x) <= ORT_MAXFLOAT && fabsf(inv.y) <= ORT_MAXFLOAT && fabsf(inv.z) <= ORT_MAXFLOAT &&
            fabsf(r.o.x) <= ORT_MAXFLOAT && fabsf(r.o.y) <= ORT_MAXFLOAT && fabsf(r.o.z) <= ORT_MAXFLOAT &&
-           t_min > 0.0f && t_max <= ORT_MAXFLOAT;
+           t_min > 0.0f && t_max <= ORT_MAXFLOAT && a_in_qdiv_range(dot(r.d, r.d));
 }
 
 // 24-bit signed multiply (plane indices are < 2^11): one full-rate VALU op on the device.
@@ -420,6 +424,72 @@ ORT_FN float fmin2(float a, float b) { return fminf(a, b); }
 ORT_FN float fmax3(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
 ORT_FN float fmin3(float a, float b, float c) { return fminf(fminf(a, b), c); }
 #endif
+
+// Correctly rounded n / a given y = RN(1/a): q0 = n*y is faithful, r = n - a*q0 is exact
+// (fma), and RN(q0 + r*y) = RN(n/a) (Markstein's theorem; no division is ever exactly a
+// midpoint).  Valid without underflow/overflow in r and q: |n| in [2^-60, 2^100] and
+// a in [2^-3, 2^3] (checked per ray by fast_path_ok); otherwise the IEEE division.
+// 2.56e9 random (n, a) pairs in those ranges were checked bitwise against n / a on the host.
+ORT_FN float qdiv(float n, float a, float y) {
+    const float an = fabsf(n);
+    if (!(an >= 0x1p-60f && an <= 0x1p100f)) return n / a;
+    const float q0 = n * y;
+    return fmaf(fmaf(-q0, a, n), y, q0);
+}
+// Correctly rounded sqrt for x in [2^-96, 2^100]: the hardware estimate corrected by the
+// two residual tests of the compiler's own IEEE expansion, minus its denormal scaling and
+// special-value handling (not needed in that range); otherwise sqrtf.
+ORT_FN float qsqrt(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (!(x >= 0x1p-96f && x <= 0x1p100f)) return sqrtf(x);
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sm = __uint_as_float(__float_as_uint(s) - 1u);
+    const float sp = __uint_as_float(__float_as_uint(s) + 1u);
+    float r = (fmaf(-sm, s, x) <= 0.0f) ? sm : s;
+    r = (fmaf(-sp, s, x) > 0.0f) ? sp : r;
+    return r;
+#else
+    return sqrtf(x);
+#endif
+}
+
+// Sphere_hit_t with the fast division/sqrt (ya = RN(1 / a)); same results.
+ORT_FN bool sphere_hit_fast(const Ray& r, float a, float ya, float4 sp, float t_min, float t_max, float& t) {
+    const V3 oc = mk(r.o.x - sp.x, r.o.y - sp.y, r.o.z - sp.z);
+    const float half_b = dot(oc, r.d);
+    const float c = dot(oc, oc) - sp.w * sp.w;
+    const float disc = half_b * half_b - a * c;
+    if (disc > 0.0f) {
+        const float sq = qsqrt(disc);
+        float temp = qdiv(-half_b - sq, a, ya);
+        if (temp < t_max && temp > t_min) { t = temp; return true; }
+        temp = qdiv(-half_b + sq, a, ya);
+        if (temp < t_max && temp > t_min) { t = temp; return true; }
+    }
+    return false;
+}
+
+// Node record / leaf sphere loads of the fast walk.  On the device: buffer loads with a
+// 32-bit byte offset (descriptor from the kernel arguments, so it stays in SGPRs) instead of
+// 64-bit flat addresses -- fewer VALU ops and VGPRs per fetch (cdna_hip_programming.md T8).
+ORT_FN uint2 fetch_node(const KScene& S, int i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)S.node, 0, (int)S.node_bytes, 0x00020000);
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, (uint32_t)i * 8u, 0, 0);
+    return make_uint2(v[0], v[1]);
+#else
+    return S.node[i];
+#endif
+}
+ORT_FN float4 fetch_sphere(const KScene& S, int e) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)S.leaf_sph, 0, (int)S.leaf_bytes, 0x00020000);
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)e * 16u, 0, 0);
+    return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+#else
+    return S.leaf_sph[e];
+#endif
+}
 
 // Rank-reversed level masks (see above).  pop() returns hb = 8L + 7 - rank.
 struct Masks64 {  // levels 0..7: trees of depth <= 8
@@ -459,6 +529,7 @@ template <class Masks>
 struct FastStateT {
     Ray r;           // original-axis ray (Sphere_hit uses it as is)
     float a;         // dot(d, d)
+    float ya;        // RN(1 / a)
     float oA, oB, oC, iA, iB, iC;  // role-axis origin / 1/d
     const float* pA;  // ray-order plane table of each role axis: plane(i) = pA[sA * i]
     const float* pB;
@@ -489,6 +560,7 @@ ORT_FN bool fast_begin(const KScene& S, const float* planes, const Ray& r, V3 in
     const uint32_t gA = swap ? ny : nx, gB = swap ? nx : ny, gC = nz;
     st.r = r;
     st.a = dot(r.d, r.d);
+    st.ya = 1.0f / st.a;
     st.oA = swap ? r.o.y : r.o.x;
     st.oB = swap ? r.o.x : r.o.y;
     st.oC = r.o.z;
@@ -527,7 +599,7 @@ ORT_FN bool fast_begin(const KScene& S, const float* planes, const Ray& r, V3 in
 template <bool COUNT, class Masks, class Frames>
 ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks>& st, Frames& fr, Counters& cnt) {
     const int D = S.depth;
-    const uint2 rec = S.node[st.node];
+    const uint2 rec = fetch_node(S, st.node);
     if (COUNT) cnt.v[0] += 1;
     if (rec.y & ORT_INTERNAL_FLAG) {
         const int co = (int)rec.x;
@@ -570,10 +642,10 @@ ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks
         const int n = (int)rec.y;
         const float ntmin = st.depth == 0 ? st.tmin0 : fmax2(fmax3(st.tNA, st.tNB, st.tNC), st.tmin0);
         for (int i = 0; i < n; ++i) {
-            const float4 sp = S.leaf_sph[off + i];
+            const float4 sp = fetch_sphere(S, off + i);
             if (COUNT) cnt.v[2] += 1;
             float t;
-            if (sphere_hit_t(st.r, st.a, sp, ntmin, st.closest, t)) {
+            if (sphere_hit_fast(st.r, st.a, st.ya, sp, ntmin, st.closest, t)) {
                 st.hit = true;
                 st.closest = t;
                 st.hitEntry = off + i;

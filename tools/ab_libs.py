@@ -1,7 +1,8 @@
-"""Interleaved A/B timing of two builds of libort.so in one process (e.g. the committed
-HEAD build against the working tree), frames alternating so clocks/thermals hit both alike.
-Also checks that both builds produce bit-identical frames.
-usage: python tools/ab_libs.py LIB_A LIB_B [config] [rounds]"""
+"""Interleaved A/B timing of builds of libort.so in one process (e.g. the committed HEAD
+build against the working tree), frames alternating so clocks/thermals hit all alike.
+Also checks that all builds produce bit-identical frames.
+usage: python tools/ab_libs.py LIB_A LIB_B [LIB_C ...] [--config c3] [--rounds 10]"""
+import argparse
 import ctypes as C
 import sys
 from pathlib import Path
@@ -14,9 +15,12 @@ import bench  # noqa: E402
 import octreeraytracer_amd as ort  # noqa: E402
 from octreeraytracer_amd import _lib as L  # noqa: E402
 
-paths = sys.argv[1:3]
-cfg = sys.argv[3] if len(sys.argv) > 3 else "c3"
-rounds = int(sys.argv[4]) if len(sys.argv) > 4 else 10
+ap = argparse.ArgumentParser()
+ap.add_argument("libs", nargs="+")
+ap.add_argument("--config", default="c3")
+ap.add_argument("--rounds", type=int, default=10)
+args = ap.parse_args()
+paths, cfg, rounds = args.libs, args.config, args.rounds
 libs = []
 for p in paths:
     lib = C.CDLL(str(Path(p).resolve()), mode=C.RTLD_LOCAL)
@@ -43,10 +47,12 @@ for k in range(rounds + 1):
         if k > 0:  # first round = warm-up
             frame[i].append(r.last_kernel_ms())
             trace[i].append(r.last_trace_ms())
-    assert np.array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32)), "builds differ"
+    for i in range(1, len(libs)):
+        assert np.array_equal(outs[0].view(np.uint32), outs[i].view(np.uint32)), f"build {paths[i]} differs"
 for i, path in enumerate(paths):
     f, tr = np.median(frame[i]), np.median(trace[i])
     print(f"{cfg} {Path(path).name:18s} frame {f:.3f} ms (min {np.min(frame[i]):.3f})  trace {tr:.3f} ms"
           f"  -> {W * H * NS / f / 1e3:.1f} Mrays/s")
-print(f"speedup B/A: frame {np.median(frame[0]) / np.median(frame[1]):.3f}x, "
-      f"trace {np.median(trace[0]) / np.median(trace[1]):.3f}x")
+for i in range(1, len(libs)):
+    print(f"speedup {Path(paths[i]).name} vs {Path(paths[0]).name}: frame "
+          f"{np.median(frame[0]) / np.median(frame[i]):.3f}x, trace {np.median(trace[0]) / np.median(trace[i]):.3f}x")
