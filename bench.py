@@ -89,7 +89,10 @@ def main():
     tile = rank_tile(W, H, rank, world)
     out = torch.empty((tile.rows, W, 3), dtype=torch.float32, device="cuda")
     gather = FrameGather(dist, W, H, world, rank, "cuda")
-    stream = torch.cuda.current_stream()
+    # a dedicated stream: torch's default stream is the HIP null stream (handle 0), which the
+    # C ABI reads as "no stream" and then renders synchronously on the context's stream
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
 
     def step():
         r.render(p, tile, out=out, stream=stream.cuda_stream)

@@ -85,6 +85,7 @@ typedef struct ort_scene_info {
 #define ORT_OPT_EXACT_TRAVERSAL 2  /* 1: disable the sign-specialised fast walk (A/B testing; same pixels) */
 #define ORT_OPT_REFILL 3           /* persistent trace: refill a wave when >= value of its 64 lanes idle (16) */
 #define ORT_OPT_PERSISTENT 4       /* 1: persistent trace kernel with per-lane ray refill (default 0) */
+#define ORT_OPT_PACKET 5           /* 1: wave-level walk for camera rays; 0 (default): per-lane walk (same pixels) */
 
 /* Traffic counters (ort_count_traffic), in the REFERENCE layout's terms. */
 #define ORT_COUNT_NODES_POPPED 0
@@ -129,8 +130,9 @@ int ort_scene_get_info(const ort_ctx* ctx, ort_scene_info* info);
 
 /* Render the tile; rgb_out receives tile->rows * tile->width RGB float triples, row-major,
  * output row 0 first.  out_is_device != 0: rgb_out is a device pointer on ctx's device.
- * stream: a hipStream_t on ctx's device, or NULL for the context's own stream (then the
- * call returns after the frame is complete). */
+ * stream: a hipStream_t on ctx's device (stream-ordered, returns at once), or NULL for the
+ * context's own stream (then the call returns after the frame is complete).  The HIP null
+ * stream has the NULL handle, so passing it also means "synchronous". */
 int ort_render(ort_ctx* ctx, const ort_params* params, const ort_tile* tile,
                float* rgb_out, int out_is_device, void* stream);
 

@@ -50,6 +50,7 @@ struct PipeArgs {
     int exact_only;   // ORT_OPT_EXACT_TRAVERSAL: every compact ray takes the exact walk
     int refill;       // persistent trace: refill a wave when at least this many lanes idle
     int rays_stored;  // bounce-0 rays were written by ort_raygen_kernel (persistent pipeline)
+    const uint8_t* lut;  // global copy of the rank LUT (ort::rank_lut_entry), 8 x 256 bytes
     int2* hit;        // per path: {entry (-1 miss), t bits}
     int* defer_list;
     int* sync;        // [0] deferred count, [1] work cursor of the persistent trace
@@ -282,6 +283,211 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))
     flush_counts<COUNT>(cnt, A.counters);
 }
 
+// Wave-wide OR of v (every lane of the wave must be executing): DPP prefix-OR inside each
+// row of 16 lanes, then the row broadcasts; lane 63 ends up with the OR of all 64.
+__device__ inline uint32_t wave_or(uint32_t v) {
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);   // row_shr:1
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);   // row_shr:2
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);   // row_shr:4
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true);   // row_shr:8
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+// Camera rays, wave-level ("packet") walk of the compact layout.
+//
+// A wave is an 8x8 pixel block; when all its fast-path rays share the sign vector (hence the
+// traversal order), the wave walks the tree ONCE, in that order, visiting the union of the
+// nodes its rays visit.  Each lane keeps its own rank-reversed level masks (the children ITS
+// walk pushed) and is active at a node iff that node is in its own set, so every lane sees
+// exactly its own node sequence (a DFS in a fixed child order, restricted to an
+// ancestor-closed subset, is that subset's DFS) and stops after its first hitting leaf, as
+// the per-lane walk does.  What moves to the scalar side: the node record, split planes and
+// leaf spheres are wave-uniform loads (s_load), the union masks and the cell/level
+// bookkeeping live in SGPRs, and the per-level children offsets in one VGPR indexed by level
+// (v_writelane/v_readlane).  The per-lane work per visit is the slab math of the active
+// lanes only.  Waves whose rays do not share one order take the per-lane walk.
+//
+// tools/wave_stats.py prices it: at C3 the union visits 1.41x the internal nodes of one ray,
+// while the per-lane loop ran a ~46-VALU pop for every lane every iteration.
+template <bool COUNT, bool DEEP>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) ort_trace_packet(PipeArgs A) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    using Masks = typename std::conditional<DEEP, ort::Masks96, ort::Masks64>::type;
+    const ort::KScene& S = A.S;
+    const int k = blockIdx.x * kBlock + threadIdx.x;
+    bool alive;
+    const ort::Ray ray = slot_ray<true>(A, k, alive);
+    const ort::V3 inv = ort::mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
+    const bool fast = alive && !A.exact_only && ort::fast_path_ok(ray, inv, 0.001f, ORT_MAXFLOAT);
+    ort::Counters cnt;
+    for (int q = 0; q < 6; ++q) cnt.v[q] = 0;
+    if (COUNT && fast) cnt.v[5] += 1;
+    const uint32_t mL = ((uint32_t)(ray.d.z < 0.0f) << 2) | ((uint32_t)(ray.d.x < 0.0f) << 1) | (uint32_t)(ray.d.y < 0.0f);
+    const uint64_t fastMask = __ballot(fast);
+    int entry = -1;
+    float tHit = 0.0f;
+    bool hit = false;
+    if (fastMask) {
+        const int lead = __builtin_ctzll(fastMask);
+        const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)mL, lead);
+        if (__ballot(fast && mL != m) == 0) {
+            // ---- packet walk: every lane of the wave executes this block ----
+            const int D = S.depth;
+            const int top = 1 << D;
+            const int P1 = top + 1;
+            const bool swap = (m >> 1) & 1u;
+            const uint32_t gA = swap ? (m & 1u) : ((m >> 1) & 1u), gB = swap ? ((m >> 1) & 1u) : (m & 1u),
+                           gC = (m >> 2) & 1u;
+            const float* pA = S.planes + (swap ? P1 : 0) + (gA ? top : 0);
+            const float* pB = S.planes + (swap ? 0 : P1) + (gB ? top : 0);
+            const float* pC = S.planes + 2 * P1 + (gC ? top : 0);
+            const int sA = gA ? -1 : 1, sB = gB ? -1 : 1, sC = gC ? -1 : 1;
+            uint32_t otab = 0;
+            for (uint32_t r = 0; r < 8; ++r) otab |= ort::rank_perm(r, m) << (4 * r);
+            const uint8_t* lutRow = A.lut + m * 256u;
+            const float oA = swap ? ray.o.y : ray.o.x, oB = swap ? ray.o.x : ray.o.y, oC = ray.o.z;
+            const float iA = swap ? inv.y : inv.x, iB = swap ? inv.x : inv.y, iC = inv.z;
+            const float a = ort::dot(ray.d, ray.d);
+            const float ya = 1.0f / a;
+            const float tmin0 = 0.001f, tmax0 = ORT_MAXFLOAT;
+            float closest = tmax0;
+            // root (glsl:296-311): lanes whose ray hits the root box start active
+            bool active;
+            {
+                const float tNA = iA * (pA[0] - oA), tFA = iA * (pA[sA * top] - oA);
+                const float tNB = iB * (pB[0] - oB), tFB = iB * (pB[sB * top] - oB);
+                const float tNC = iC * (pC[0] - oC), tFC = iC * (pC[sC * top] - oC);
+                active = fast && ort::fmin3(tFA, tFB, tFC) >= ort::fmax3(tNA, tNB, tNC);
+            }
+            Masks lm;     // this lane's pending children (rank-reversed level bytes)
+            lm.clear();
+            Masks um;     // wave union of lm (uniform)
+            um.clear();
+            int coLanes = 0;  // lane L holds the children offset of the walk's level-L ancestor
+            const int laneId = (int)(threadIdx.x & 63u);
+            int node = 0, depth = 0, cA = 0, cB = 0, cC = 0, w = top;  // uniform
+            bool more = __ballot(active) != 0;
+            while (more) {
+                // (readfirstlane: keeps the compiler's uniformity analysis from losing these)
+                node = __builtin_amdgcn_readfirstlane(node);
+                depth = __builtin_amdgcn_readfirstlane(depth);
+                cA = __builtin_amdgcn_readfirstlane(cA);
+                cB = __builtin_amdgcn_readfirstlane(cB);
+                cC = __builtin_amdgcn_readfirstlane(cC);
+                w = __builtin_amdgcn_readfirstlane(w);
+                um.uniform();
+                const uint2 rec = S.node[node];  // uniform: s_load
+                const float pnA = pA[sA * cA], pfA = pA[sA * (cA + w)];
+                const float pnB = pB[sB * cB], pfB = pB[sB * (cB + w)];
+                const float pnC = pC[sC * cC], pfC = pC[sC * (cC + w)];
+                // the wave-uniform node-type branch must not share its join with a divergent
+                // branch (or the compiler treats everything merged there as divergent)
+                const bool internal = (rec.y & ORT_INTERNAL_FLAG) != 0;
+                if (internal) {
+                    const int co = (int)rec.x;
+                    const int h = w >> 1;
+                    const float pmA = pA[sA * (cA + h)], pmB = pB[sB * (cB + h)], pmC = pC[sC * (cC + h)];
+                    const uint32_t rcm = lutRow[rec.y & 0xffu];
+                    uint32_t rm = 0;
+                    if (active) {
+                        if (COUNT) {
+                            cnt.v[0] += 1;
+                            const long long rem = (long long)S.n_nodes - (long long)co;
+                            cnt.v[1] += (unsigned long long)(rem >= 8 ? 8 : (rem > 0 ? rem : 0));
+                        }
+                        const float tNA = iA * (pnA - oA), tFA = iA * (pfA - oA), tMA = iA * (pmA - oA);
+                        const float tNB = iB * (pnB - oB), tFB = iB * (pfB - oB), tMB = iB * (pmB - oB);
+                        const float tNC = iC * (pnC - oC), tFC = iC * (pfC - oC), tMC = iC * (pmC - oC);
+                        const float e00 = ort::fmax2(tNA, tNB), e01 = ort::fmax2(tNA, tMB);
+                        const float e10 = ort::fmax2(tMA, tNB), e11 = ort::fmax2(tMA, tMB);
+                        const float x00 = ort::fmin2(tMA, tMB), x01 = ort::fmin2(tMA, tFB);
+                        const float x10 = ort::fmin2(tFA, tMB), x11 = ort::fmin2(tFA, tFB);
+                        const float nN = ort::fmax2(tNC, tmin0), nF = ort::fmax2(tMC, tmin0);
+                        const float cN = ort::fmin2(tMC, tmax0), cF = ort::fmin2(tFC, tmax0);
+                        uint32_t drop = 0;
+#define ORT_CHILD(EAB, XAB, EC, XC) drop = (drop << 1) | (ort::f2u(ort::fmin2(XAB, XC) - ort::fmax2(EAB, EC)) >> 31);
+                        ORT_CHILD(e00, x00, nN, cN)
+                        ORT_CHILD(e01, x01, nN, cN)
+                        ORT_CHILD(e10, x10, nN, cN)
+                        ORT_CHILD(e11, x11, nN, cN)
+                        ORT_CHILD(e00, x00, nF, cF)
+                        ORT_CHILD(e01, x01, nF, cF)
+                        ORT_CHILD(e10, x10, nF, cF)
+                        ORT_CHILD(e11, x11, nF, cF)
+#undef ORT_CHILD
+                        rm = rcm & ~drop;
+                        lm.put(depth, rm);
+                    }
+                    um.put(depth, wave_or(rm));
+                    coLanes = (laneId == depth) ? co : coLanes;  // v_writelane without the builtin
+                }
+                if (!internal && active) {
+                    if (COUNT) cnt.v[0] += 1;
+                    const int off = (int)rec.x;
+                    const int n = (int)rec.y;
+                    const float tNA = iA * (pnA - oA), tNB = iB * (pnB - oB), tNC = iC * (pnC - oC);
+                    const float ntmin = depth == 0 ? tmin0 : ort::fmax2(ort::fmax3(tNA, tNB, tNC), tmin0);
+                    for (int i = 0; i < n; ++i) {
+                        const float4 sp = S.leaf_sph[off + i];  // uniform: s_load
+                        if (COUNT) cnt.v[2] += 1;
+                        float t;
+                        if (ort::sphere_hit_fast(ray, a, ya, sp, ntmin, closest, t)) {
+                            hit = true;
+                            closest = t;
+                            entry = off + i;
+                            if (COUNT) cnt.v[3] += 1;
+                        }
+                    }
+                    if (hit) lm.clear();  // glsl:336: this lane's walk ends after this leaf
+                }
+                // next node: deepest level, lowest rank that some lane still wants
+                int hb = -1;
+                active = false;
+                um.uniform();
+                while (!um.empty()) {
+                    const int c = um.pop();
+                    active = lm.take(c);
+                    if (__ballot(active)) {
+                        hb = c;
+                        break;
+                    }
+                }
+                more = hb >= 0;
+                if (more) {
+                    const int L = hb >> 3;
+                    const uint32_t rk = (uint32_t)(~hb) & 7u;
+                    const int wc = 1 << (D - 1 - L);
+                    const int keep = -2 * wc;
+                    cA = (cA & keep) | (((rk >> 1) & 1u) ? wc : 0);
+                    cB = (cB & keep) | ((rk & 1u) ? wc : 0);
+                    cC = (cC & keep) | (((rk >> 2) & 1u) ? wc : 0);
+                    w = wc;
+                    depth = L + 1;
+                    node = __builtin_amdgcn_readlane(coLanes, L) + (int)((otab >> (4 * rk)) & 15u);
+                }
+            }
+            tHit = hit ? closest : 0.0f;
+        } else if (fast) {
+            // ---- mixed orders: per-lane walk ----
+            ort::LdsFrames fr;
+            fr.co = reinterpret_cast<int*>(smem);
+            fr.tm = nullptr;
+            fr.stride = kBlock;
+            fr.lane = threadIdx.x;
+            hit = ort::traverse_fast_t<COUNT, Masks>(S, S.planes, A.lut, ray, inv, 0.001f, ORT_MAXFLOAT, entry, tHit,
+                                                     fr, cnt);
+        }
+    }
+    if (alive && !fast) {
+        A.defer_list[atomicAdd(A.sync, 1)] = k;
+    } else if (alive) {
+        A.hit[k] = make_int2(hit ? entry : -1, __float_as_int(tHit));
+    }
+    flush_counts<COUNT>(cnt, A.counters);
+}
+
 // One-ray-per-lane trace for the explicit layout (MODE 1) and brute force (MODE 2).
 template <int MODE, bool COUNT, bool PRIMARY>
 __global__ void __launch_bounds__(kBlock) ort_trace_kernel(PipeArgs A) {
@@ -439,6 +645,8 @@ struct ort_ctx {
     int exact_only = 0;
     int refill = 16;
     int persistent = 0;
+    int packet = 0;     // ORT_OPT_PACKET: wave-level walk for camera rays (SALU-bound so far: off)
+    DevBuf lut;         // rank LUT (global copy, for the packet kernel)
     bool has_scene = false;
     int layout = ORT_LAYOUT_EXPLICIT;
     int depth = 0;
@@ -621,8 +829,13 @@ int ensure(ort_ctx* ctx, DevBuf& b, size_t bytes) {
 }
 
 template <bool COUNT, bool PRIMARY>
-hipError_t launch_trace_p(int mode, const PipeArgs& a, int blocks, int pblocks, size_t lds, hipStream_t s) {
+hipError_t launch_trace_p(int mode, const PipeArgs& a, int blocks, int pblocks, size_t lds, hipStream_t s, bool packet) {
     if (mode == 0 && pblocks > 0) hipLaunchKernelGGL((ort_trace_persistent<COUNT>), dim3(pblocks), dim3(kBlock), lds, s, a);
+    else if (mode == 0 && PRIMARY && packet) {
+        const size_t flds = (size_t)std::max(a.S.depth, 1) * kBlock * sizeof(int);  // per-lane fallback frames
+        if (a.S.depth > 8) hipLaunchKernelGGL((ort_trace_packet<COUNT, true>), dim3(blocks), dim3(kBlock), flds, s, a);
+        else hipLaunchKernelGGL((ort_trace_packet<COUNT, false>), dim3(blocks), dim3(kBlock), flds, s, a);
+    }
     else if (mode == 0 && a.S.depth > 8)
         hipLaunchKernelGGL((ort_trace_compact<COUNT, PRIMARY, true>), dim3(blocks), dim3(kBlock), lds, s, a);
     else if (mode == 0) hipLaunchKernelGGL((ort_trace_compact<COUNT, PRIMARY, false>), dim3(blocks), dim3(kBlock), lds, s, a);
@@ -632,9 +845,10 @@ hipError_t launch_trace_p(int mode, const PipeArgs& a, int blocks, int pblocks, 
 }
 
 template <bool COUNT>
-hipError_t launch_trace(int mode, bool primary, const PipeArgs& a, int blocks, int pblocks, size_t lds, hipStream_t s) {
-    return primary ? launch_trace_p<COUNT, true>(mode, a, blocks, pblocks, lds, s)
-                   : launch_trace_p<COUNT, false>(mode, a, blocks, pblocks, lds, s);
+hipError_t launch_trace(int mode, bool primary, const PipeArgs& a, int blocks, int pblocks, size_t lds, hipStream_t s,
+                        bool packet) {
+    return primary ? launch_trace_p<COUNT, true>(mode, a, blocks, pblocks, lds, s, packet)
+                   : launch_trace_p<COUNT, false>(mode, a, blocks, pblocks, lds, s, packet);
 }
 
 template <int MODE>
@@ -706,6 +920,7 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     a.total = (int)slots;
     a.exact_only = ctx->exact_only || !ctx->ordered;
     a.refill = ctx->refill;
+    a.lut = (const uint8_t*)ctx->lut.p;
     a.hit = (int2*)ctx->hit.p;
     a.defer_list = (int*)ctx->defer_list.p;
     a.sync = (int*)ctx->defer_count.p;
@@ -739,8 +954,8 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                 const int slot = (int)(ctx->frames % ort_ctx::kRing);
                 if (first_trace) HIPCHK(ctx, hipEventRecord(ctx->tr0[slot], s));
                 const bool prim = (b == 0) && pblocks == 0;
-                e = dcounters ? launch_trace<true>(mode, prim, a, (int)blocks, pblocks, lds, s)
-                              : launch_trace<false>(mode, prim, a, (int)blocks, pblocks, lds, s);
+                e = dcounters ? launch_trace<true>(mode, prim, a, (int)blocks, pblocks, lds, s, ctx->packet != 0)
+                              : launch_trace<false>(mode, prim, a, (int)blocks, pblocks, lds, s, ctx->packet != 0);
                 if (e != hipSuccess) return hip_fail(ctx, e, "trace kernel launch");
                 if (first_trace) {
                     HIPCHK(ctx, hipEventRecord(ctx->tr1[slot], s));
@@ -804,6 +1019,18 @@ int ort_create(int device, ort_ctx** out) {
             return rc;
         }
     }
+    {
+        std::vector<uint8_t> lut(kRankLutBytes);
+        for (size_t i = 0; i < lut.size(); ++i) lut[i] = ort::rank_lut_entry((uint32_t)i >> 8, (uint32_t)i & 255u);
+        const int rc = upload(c, c->lut, lut.data(), lut.size());
+        if (rc == ORT_OK) e = hipStreamSynchronize(c->stream);
+        if (rc != ORT_OK || e != hipSuccess) {
+            const int rc2 = rc != ORT_OK ? rc : hip_fail(nullptr, e, "ort_create: lut");
+            ort::set_thread_error(c->err);
+            ort_destroy(c);
+            return rc2;
+        }
+    }
     *out = c;
     return ORT_OK;
 }
@@ -815,6 +1042,7 @@ int ort_destroy(ort_ctx* ctx) {
     free_scene(ctx);
     free_buf(ctx->scratch_out);
     free_buf(ctx->counters);
+    free_buf(ctx->lut);
     DevBuf* pipe[] = {&ctx->hit, &ctx->defer_list, &ctx->defer_count, &ctx->po, &ctx->pd, &ctx->pc, &ctx->prng, &ctx->pcol};
     for (DevBuf* b : pipe) free_buf(*b);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
@@ -839,6 +1067,10 @@ int ort_set_option(ort_ctx* ctx, int option, int value) {
     }
     if (option == ORT_OPT_PERSISTENT) {
         ctx->persistent = value ? 1 : 0;
+        return ORT_OK;
+    }
+    if (option == ORT_OPT_PACKET) {
+        ctx->packet = value ? 1 : 0;
         return ORT_OK;
     }
     if (option == ORT_OPT_REFILL) {
@@ -1052,6 +1284,112 @@ int ort_debug_emulate_render(const float* cr, const float* ma, const float* fr, 
             }
         }
         if (counts) for (int k = 0; k < 6; ++k) counts[k] = total.v[k];
+        return ORT_OK;
+    } catch (const std::exception& ex) {
+        return fail(nullptr, ORT_ERR_INTERNAL, ex.what());
+    }
+}
+
+
+// ANALYSIS-ONLY (tools/wave_stats.py): walks sampled 8x8 pixel blocks (one wave each) of
+// the primary-ray frame with the kernel's fast walk on the host and reports how the lanes'
+// visited-node sets overlap, to price wave-level (packet) traversal against the per-lane
+// loop.  stats: see tools/wave_stats.py for the field order.
+int ort_debug_wave_stats(const float* cr, const float* ma, const float* fr, int32_t n_spheres,
+                         const float* node_min, const float* node_max, const int32_t* co, const int32_t* oo,
+                         const int32_t* cnt, int32_t n_nodes, const int32_t* idx, int64_t n_indices,
+                         const ort_params* p, int32_t block_step, double* stats, int32_t n_stats) {
+    try {
+        if (n_stats < 16 || block_step < 1) return fail(nullptr, ORT_ERR_INVALID_ARG, "bad stats args");
+        ort::SceneInput in{cr, ma, fr, n_spheres, node_min, node_max, co, oo, cnt, n_nodes, idx, n_indices};
+        ort::CompactLayout cl;
+        std::string why;
+        if (!ort::buildCompactLayout(in, ORT_COMPACT_MAX_DEPTH, cl, why)) return fail(nullptr, ORT_ERR_UNSUPPORTED, why);
+        ort::KScene S;
+        std::memset(&S, 0, sizeof(S));
+        S.n_spheres = n_spheres;
+        S.n_nodes = n_nodes;
+        S.node = (const uint2*)cl.node.data();
+        S.leaf_sph = (const float4*)cl.leaf_sph.data();
+        S.leaf_idx = cl.leaf_idx.data();
+        S.planes = cl.planes.data();
+        S.depth = cl.depth;
+        std::vector<uint8_t> lut(kRankLutBytes);
+        for (size_t i = 0; i < lut.size(); ++i) lut[i] = ort::rank_lut_entry((uint32_t)i >> 8, (uint32_t)i & 255u);
+        const ort::PixelParams pp = pixel_params(p);
+        ort::LocalFrames lf;
+        ort::Counters cc;
+        for (int k = 0; k < 6; ++k) cc.v[k] = 0;
+        for (int k = 0; k < n_stats; ++k) stats[k] = 0.0;
+        const int bw = (p->width + 7) / 8, bh = (p->height + 7) / 8;
+        std::vector<std::vector<int>> seq(64);
+        std::vector<int> all;
+        for (int b = 0; b < bw * bh; b += block_step) {
+            const int bx = b % bw, by = b / bw;
+            bool uniform = true;
+            int m0 = -1, lanes = 0;
+            size_t maxlen = 0;
+            for (int l = 0; l < 64; ++l) {
+                seq[l].clear();
+                const int px = bx * 8 + (l & 7), py = by * 8 + (l >> 3);
+                if (px >= p->width || py >= p->height) continue;
+                ort_rng st;
+                ort::pixel_rng_init(pp, px, py, st);
+                const ort::Ray ray = ort::primary_ray(pp, px, py, 0, st);
+                const ort::V3 inv = ort::mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
+                if (!ort::fast_path_ok(ray, inv, 0.001f, ORT_MAXFLOAT)) { uniform = false; continue; }
+                lanes++;
+                const int m = ((ray.d.z < 0.0f) << 2) | ((ray.d.x < 0.0f) << 1) | (ray.d.y < 0.0f);
+                if (m0 < 0) m0 = m;
+                else if (m != m0) uniform = false;
+                ort::FastStateT<ort::Masks96> fs;
+                if (!ort::fast_begin(S, S.planes, ray, inv, 0.001f, ORT_MAXFLOAT, fs)) continue;
+                for (;;) {
+                    seq[l].push_back(fs.node);
+                    if (ort::fast_step<false>(S, lut.data(), fs, lf, cc)) break;
+                }
+                maxlen = std::max(maxlen, seq[l].size());
+            }
+            stats[0] += 1;                  // waves
+            stats[1] += uniform ? 0 : 1;    // waves with mixed order / non-fast lanes
+            stats[2] += lanes;
+            all.clear();
+            for (int l = 0; l < 64; ++l)
+                for (int nd : seq[l]) {
+                    const bool leaf = !(cl.node[2 * (size_t)nd + 1] & ORT_INTERNAL_FLAG);
+                    stats[leaf ? 4 : 3] += 1;  // individual internal / leaf visits
+                    if (leaf) stats[5] += cl.node[2 * (size_t)nd + 1];  // individual sphere tests
+                    all.push_back(nd);
+                }
+            std::sort(all.begin(), all.end());
+            all.erase(std::unique(all.begin(), all.end()), all.end());
+            for (int nd : all) {
+                const bool leaf = !(cl.node[2 * (size_t)nd + 1] & ORT_INTERNAL_FLAG);
+                stats[leaf ? 7 : 6] += 1;  // union internal / leaf visits
+                if (leaf) stats[8] += cl.node[2 * (size_t)nd + 1];
+            }
+            // lockstep per-lane loop (the current kernel): iteration k runs the internal
+            // block if any lane's k-th node is internal, the leaf block (max spheres) if any
+            // is a leaf, and the pop for every lane still walking
+            for (size_t k = 0; k < maxlen; ++k) {
+                bool anyI = false, anyL = false;
+                uint32_t maxS = 0;
+                int act = 0;
+                for (int l = 0; l < 64; ++l) {
+                    if (k >= seq[l].size()) continue;
+                    act++;
+                    const uint32_t y = cl.node[2 * (size_t)seq[l][k] + 1];
+                    if (y & ORT_INTERNAL_FLAG) anyI = true;
+                    else { anyL = true; maxS = std::max(maxS, y); }
+                }
+                stats[9] += 1;            // lockstep iterations
+                stats[10] += anyI;        // iterations running the internal block
+                stats[11] += anyL;        // iterations running the leaf block
+                stats[12] += maxS;        // sphere-loop trips
+                stats[13] += act;         // lane-iterations
+            }
+            stats[14] += (double)maxlen;
+        }
         return ORT_OK;
     } catch (const std::exception& ex) {
         return fail(nullptr, ORT_ERR_INTERNAL, ex.what());

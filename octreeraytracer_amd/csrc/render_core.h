@@ -491,6 +491,11 @@ ORT_FN float4 fetch_sphere(const KScene& S, int e) {
 #endif
 }
 
+// Plane idx of a ray-order table: base + s4*idx bytes (s4 = +-4): one v_mad_i32_i24.
+ORT_FN float plane_at(const float* base, int s4, int idx) {
+    return *(const float*)((const char*)base + imul24(s4, idx));
+}
+
 // Rank-reversed level masks (see above).  pop() returns hb = 8L + 7 - rank.
 struct Masks64 {  // levels 0..7: trees of depth <= 8
     uint64_t m;
@@ -501,6 +506,19 @@ struct Masks64 {  // levels 0..7: trees of depth <= 8
         const int hb = 63 - __builtin_clzll(m);
         m ^= (uint64_t)1 << hb;
         return hb;
+    }
+    // clears bit hb (= 8L + 7 - rank) and returns whether it was set
+    ORT_FN bool take(int hb) {
+        const uint64_t b = (uint64_t)1 << hb;
+        const bool t = (m & b) != 0;
+        m &= ~b;
+        return t;
+    }    // device: re-assert wave-uniformity (the value is uniform; this only helps the compiler)
+    ORT_FN void uniform() {
+#if defined(__HIP_DEVICE_COMPILE__)
+        m = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(m >> 32)) << 32) |
+            (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)m);
+#endif
     }
 };
 struct Masks96 {  // levels 0..11
@@ -522,6 +540,24 @@ struct Masks96 {  // levels 0..11
         lo ^= (uint64_t)1 << hb;
         return hb;
     }
+    ORT_FN bool take(int hb) {
+        if (hb >= 64) {
+            const uint32_t b = 1u << (hb - 64);
+            const bool t = (hi & b) != 0;
+            hi &= ~b;
+            return t;
+        }
+        const uint64_t b = (uint64_t)1 << hb;
+        const bool t = (lo & b) != 0;
+        lo &= ~b;
+        return t;
+    }    ORT_FN void uniform() {
+#if defined(__HIP_DEVICE_COMPILE__)
+        lo = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(lo >> 32)) << 32) |
+             (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)lo);
+        hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)hi);
+#endif
+    }
 };
 
 // Resumable per-lane state of the fast walk (so a persistent kernel can interleave rays).
@@ -531,10 +567,11 @@ struct FastStateT {
     float a;         // dot(d, d)
     float ya;        // RN(1 / a)
     float oA, oB, oC, iA, iB, iC;  // role-axis origin / 1/d
-    const float* pA;  // ray-order plane table of each role axis: plane(i) = pA[sA * i]
+    const float* pA;  // ray-order plane table of each role axis: plane(i) = *(pA + sA*i bytes)
     const float* pB;
     const float* pC;
-    int sA, sB, sC;
+    int sA, sB, sC;   // +-4: byte stride along the ray
+    int h;            // half the current node's width, in plane steps (0 at depth D)
     float tNA, tFA, tNB, tFB, tNC, tFC;  // near/far plane t of the current node's box
     int cA, cB, cC;  // ray-order index of the current node's near plane
     uint32_t otab;   // nibble r = octant of rank r
@@ -570,19 +607,20 @@ ORT_FN bool fast_begin(const KScene& S, const float* planes, const Ray& r, V3 in
     st.pA = planes + (swap ? P1 : 0) + (gA ? top : 0);
     st.pB = planes + (swap ? 0 : P1) + (gB ? top : 0);
     st.pC = planes + 2 * P1 + (gC ? top : 0);
-    st.sA = gA ? -1 : 1;
-    st.sB = gB ? -1 : 1;
-    st.sC = gC ? -1 : 1;
+    st.sA = gA ? -4 : 4;
+    st.sB = gB ? -4 : 4;
+    st.sC = gC ? -4 : 4;
+    st.h = top >> 1;
     uint32_t ot = 0;
     for (uint32_t k = 0; k < 8; ++k) ot |= rank_perm(k, m) << (4 * k);
     st.otab = ot;
     st.m = m;
     st.tNA = st.iA * (st.pA[0] - st.oA);
-    st.tFA = st.iA * (st.pA[st.sA * top] - st.oA);
+    st.tFA = st.iA * (plane_at(st.pA, st.sA, top) - st.oA);
     st.tNB = st.iB * (st.pB[0] - st.oB);
-    st.tFB = st.iB * (st.pB[st.sB * top] - st.oB);
+    st.tFB = st.iB * (plane_at(st.pB, st.sB, top) - st.oB);
     st.tNC = st.iC * (st.pC[0] - st.oC);
-    st.tFC = st.iC * (st.pC[st.sC * top] - st.oC);
+    st.tFC = st.iC * (plane_at(st.pC, st.sC, top) - st.oC);
     st.cA = st.cB = st.cC = 0;
     st.node = 0;
     st.depth = 0;
@@ -608,10 +646,10 @@ ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks
             cnt.v[1] += (unsigned long long)(rem >= 8 ? 8 : (rem > 0 ? rem : 0));
         }
         const uint32_t rcm = rank_lut[st.m * 256u + (rec.y & 0xffu)];
-        const int h = (1 << (D - st.depth)) >> 1;  // half the node width, in plane steps
-        const float tMA = st.iA * (st.pA[imul24(st.sA, st.cA + h)] - st.oA);
-        const float tMB = st.iB * (st.pB[imul24(st.sB, st.cB + h)] - st.oB);
-        const float tMC = st.iC * (st.pC[imul24(st.sC, st.cC + h)] - st.oC);
+        const int h = st.h;
+        const float tMA = st.iA * (plane_at(st.pA, st.sA, st.cA + h) - st.oA);
+        const float tMB = st.iB * (plane_at(st.pB, st.sB, st.cB + h) - st.oB);
+        const float tMC = st.iC * (plane_at(st.pC, st.sC, st.cC + h) - st.oC);
         const float tNA = st.tNA, tNB = st.tNB, tNC = st.tNC, tFA = st.tFA, tFB = st.tFB, tFC = st.tFC;
         // entry: near child (rank bit clear) enters at tN, far child at tM; exit: tM / tF
         const float e00 = fmax2(tNA, tNB), e01 = fmax2(tNA, tMB), e10 = fmax2(tMA, tNB), e11 = fmax2(tMA, tMB);
@@ -665,13 +703,14 @@ ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks
     st.cB = (st.cB & keep) | ((rk & 1) ? w : 0);
     st.cC = (st.cC & keep) | (((rk >> 2) & 1) ? w : 0);
     st.depth = L + 1;
+    st.h = w >> 1;
     st.node = fr.getCo(L) + (int)((st.otab >> (4 * rk)) & 15u);
-    st.tNA = st.iA * (st.pA[imul24(st.sA, st.cA)] - st.oA);
-    st.tFA = st.iA * (st.pA[imul24(st.sA, st.cA + w)] - st.oA);
-    st.tNB = st.iB * (st.pB[imul24(st.sB, st.cB)] - st.oB);
-    st.tFB = st.iB * (st.pB[imul24(st.sB, st.cB + w)] - st.oB);
-    st.tNC = st.iC * (st.pC[imul24(st.sC, st.cC)] - st.oC);
-    st.tFC = st.iC * (st.pC[imul24(st.sC, st.cC + w)] - st.oC);
+    st.tNA = st.iA * (plane_at(st.pA, st.sA, st.cA) - st.oA);
+    st.tFA = st.iA * (plane_at(st.pA, st.sA, st.cA + w) - st.oA);
+    st.tNB = st.iB * (plane_at(st.pB, st.sB, st.cB) - st.oB);
+    st.tFB = st.iB * (plane_at(st.pB, st.sB, st.cB + w) - st.oB);
+    st.tNC = st.iC * (plane_at(st.pC, st.sC, st.cC) - st.oC);
+    st.tFC = st.iC * (plane_at(st.pC, st.sC, st.cC + w) - st.oC);
     return false;
 }
 

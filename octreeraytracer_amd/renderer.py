@@ -114,6 +114,10 @@ class Renderer:
         """Disable (True) / enable the sign-specialised fast walk; pixels are identical either way."""
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_EXACT_TRAVERSAL, int(bool(on))))
 
+    def set_packet(self, on: bool):
+        """Wave-level (packet) walk for camera rays (default off: SALU-bound); same pixels."""
+        self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_PACKET, int(bool(on))))
+
     def set_persistent(self, on: bool):
         """Use the persistent trace kernel with per-lane ray refill (default: one ray per lane)."""
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_PERSISTENT, int(bool(on))))
@@ -152,7 +156,8 @@ class Renderer:
         """Render a tile.  out: None (returns a new (rows, width, 3) float32 numpy array),
         a numpy array, or a device pointer (int) / torch CUDA tensor on this device.
         stream: None (synchronous) or a hipStream_t handle (int), e.g.
-        torch.cuda.current_stream().cuda_stream."""
+        torch.cuda.Stream().cuda_stream.  The null stream (handle 0, torch's default
+        stream) cannot be told apart from "no stream": it renders synchronously."""
         tile = tile or Tile.full(params)
         p, t = params.to_c(), tile.to_c()
         s = C.c_void_p(int(stream)) if stream else None

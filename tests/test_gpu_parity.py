@@ -98,10 +98,19 @@ def test_device_output_and_stream(ort, renderer, scene_c1):
     p = ort.FrameParams.default_camera(96, 64)
     host = renderer.render(p)
     dev = torch.empty((64, 96, 3), dtype=torch.float32, device="cuda:0")
-    renderer.render(p, out=dev, stream=torch.cuda.current_stream().cuda_stream)
+    renderer.render(p, out=dev, stream=torch.cuda.current_stream().cuda_stream)  # null stream: synchronous
     torch.cuda.synchronize()
     assert np.array_equal(dev.cpu().numpy(), host)
     assert renderer.last_kernel_ms() > 0
+    # stream-ordered on a caller stream: several frames queued back to back, then one sync
+    st = torch.cuda.Stream()
+    outs = [torch.full((64, 96, 3), -1.0, dtype=torch.float32, device="cuda:0") for _ in range(4)]
+    with torch.cuda.stream(st):
+        for o in outs:
+            renderer.render(p, out=o, stream=st.cuda_stream)
+    st.synchronize()
+    for o in outs:
+        assert np.array_equal(o.cpu().numpy(), host)
 
 
 def test_errors(ort, renderer, scene_c1):
@@ -120,16 +129,18 @@ def test_errors(ort, renderer, scene_c1):
     fresh.close()
 
 
-@pytest.mark.parametrize("persistent,exact,refill", [(False, False, 16), (False, True, 16), (True, False, 1),
-                                                     (True, False, 16), (True, True, 64)])
-def test_kernel_variants_identical(ort, oracle, renderer, scene_c2, persistent, exact, refill):
-    """Every trace-kernel variant (one ray per lane / persistent with refill, fast / exact
-    walk) produces the oracle's pixels, also with several samples and bounces."""
+@pytest.mark.parametrize("persistent,exact,refill,packet", [
+    (False, False, 16, True), (False, False, 16, False), (False, True, 16, True), (True, False, 1, False),
+    (True, False, 16, False), (True, True, 64, False)])
+def test_kernel_variants_identical(ort, oracle, renderer, scene_c2, persistent, exact, refill, packet):
+    """Every trace-kernel variant (packet walk / one ray per lane / persistent with refill,
+    fast / exact walk) produces the oracle's pixels, also with several samples and bounces."""
     s, t = scene_c2
     renderer.upload(s, t)
     renderer.set_persistent(persistent)
     renderer.set_exact_traversal(exact)
     renderer.set_refill(refill)
+    renderer.set_packet(packet)
     try:
         p = ort.FrameParams.default_camera(1920, 1080, num_samples=2, max_depth=3)
         tile = ort.Tile(700, 200, 300, 120)
@@ -142,6 +153,7 @@ def test_kernel_variants_identical(ort, oracle, renderer, scene_c2, persistent, 
         renderer.set_persistent(False)
         renderer.set_exact_traversal(False)
         renderer.set_refill(16)
+        renderer.set_packet(False)
 
 
 @pytest.fixture(scope="module")
@@ -164,6 +176,12 @@ def test_c3_full_frame_bit_exact(ort, oracle, renderer, scene_c3):
     from octreeraytracer_amd.distributed import assemble, rank_tile
     parts = [renderer.render(p, rank_tile(3840, 2160, r, 8)) for r in range(8)]
     assert np.array_equal(assemble(np.stack(parts), 2160, 8), img)
+    # the wave-level (packet) walk gives the same frame
+    renderer.set_packet(True)
+    try:
+        assert_same(renderer.render(p), img, "C3 packet walk")
+    finally:
+        renderer.set_packet(False)
 
 
 def test_c3_counters_match_oracle_on_rows(ort, oracle, renderer, scene_c3):

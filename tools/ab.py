@@ -1,5 +1,5 @@
 """Interleaved A/B timing of kernel variants in one process (cdna_hip_programming.md 5.4
-rule 24).  Variants: exact walk, and persistent-trace refill thresholds.
+rule 24).  Variants: exact walk, per-lane walk, packet walk, persistent-trace refill thresholds.
 usage: python tools/ab.py [config] [rounds] [refill,refill,...]"""
 import sys
 from pathlib import Path
@@ -22,12 +22,15 @@ r = ort.Renderer(0)
 r.upload(s, t)
 out = np.empty((H, W, 3), np.float32)
 ref = None
-variants = [("exact", True, 0), ("lane", False, 0)] + [(f"refill{f}", False, f) for f in refills]
+# (name, exact walk, persistent refill threshold or 0, packet walk for camera rays)
+variants = [("exact", True, 0, False), ("lane", False, 0, False), ("packet", False, 0, True)] + \
+    [(f"refill{f}", False, f, False) for f in refills]
 res = {v[0]: [] for v in variants}
 tr = {v[0]: [] for v in variants}
 for k in range(rounds):
-    for name, exact, f in variants:
+    for name, exact, f, pk in variants:
         r.set_exact_traversal(exact)
+        r.set_packet(pk)
         r.set_persistent(f > 0)
         if f > 0:
             r.set_refill(f)

@@ -17,6 +17,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="c3")
 ap.add_argument("--frames", type=int, default=3)
 ap.add_argument("--layout", type=int, default=-1)
+ap.add_argument("--both", action="store_true", help="also render the frames with the packet walk off")
 a = ap.parse_args()
 W, H, N, D, M, NS, MD = bench.CONFIGS[a.config]
 s = ort.random_spheres(N, 42)
@@ -31,3 +32,10 @@ for _ in range(a.frames):
     r.render(p, out=out)
     ms.append(r.last_kernel_ms())
 print(f"{a.config} layout={r.info()['layout']} kernel ms: {['%.3f' % m for m in ms]}", flush=True)
+if a.both:
+    r.set_packet(False)
+    ms = []
+    for _ in range(a.frames):
+        r.render(p, out=out)
+        ms.append(r.last_kernel_ms())
+    print(f"{a.config} per-lane walk kernel ms: {['%.3f' % m for m in ms]}", flush=True)
