@@ -128,6 +128,23 @@ int ort_upload_octree_nodes(ort_ctx* ctx,
 
 int ort_scene_get_info(const ort_ctx* ctx, ort_scene_info* info);
 
+/* Build the octree ON THE GPU and make it ctx's scene: replaces Octree::build + setGPUData
+ * (src/octree.cpp:47-95, 189-229, 231-242, 268-312) followed by ort_upload_scene, without the
+ * host tree.  Same tree, byte for byte: root box from the sphere bounds, midpoint octants,
+ * sphereIntersectsBox distribution, BFS numbering, objectIndices in BFS leaf order
+ * (level-synchronous build, octreeraytracer_amd/csrc/gpu_build.hip).  n_spheres == 0 fails
+ * with ORT_ERR_INVALID_ARG "Sphere list is empty" like the reference's std::invalid_argument.
+ * keep_tree != 0 keeps the reference-layout arrays on the device for ort_scene_export_octree. */
+int ort_build_scene(ort_ctx* ctx, const float* sphere_center_radius, const float* sphere_mat_albedo,
+                    const float* sphere_fuzz_ri, int32_t n_spheres, int32_t max_depth, int32_t max_spheres_per_node,
+                    int32_t keep_tree);
+/* Copy the kept GPU-built tree to host arrays (sizes: ort_scene_get_info n_nodes x 3 floats /
+ * n_nodes ints / n_indices ints): the Octree::flattenedTree fields and objectIndices. */
+int ort_scene_export_octree(ort_ctx* ctx, float* node_min, float* node_max, int32_t* children_offset,
+                            int32_t* objects_offset, int32_t* object_count, int32_t* object_indices);
+/* Device time of the last ort_build_scene (HIP events; the reference's Octree::buildTime). */
+int ort_last_build_ms(const ort_ctx* ctx, float* ms);
+
 /* Render the tile; rgb_out receives tile->rows * tile->width RGB float triples, row-major,
  * output row 0 first.  out_is_device != 0: rgb_out is a device pointer on ctx's device.
  * stream: a hipStream_t on ctx's device (stream-ordered, returns at once), or NULL for the

@@ -1,0 +1,56 @@
+// gpu_build.h -- the reference octree builder on the GPU (see gpu_build.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace ort {
+
+// The reference flattened tree (Octree::flattenedTree + objectIndices, src/octree.cpp:268-312)
+// in device memory, SoA.  Owned by the caller of gpuBuildOctree (freeGpuTree).
+struct GpuTree {
+    int32_t n_nodes = 0;
+    int64_t n_indices = 0;
+    int depth = 0;                      // deepest node level (root = 0)
+    std::vector<int64_t> level_start;   // BFS index of the first node of each level (+ end)
+    float* node_min = nullptr;          // 3 per node
+    float* node_max = nullptr;
+    int32_t* co = nullptr;              // childrenOffset (-1 for leaves)
+    int32_t* oo = nullptr;              // objectsOffset (-1 unless a leaf with objects)
+    int32_t* cnt = nullptr;             // objectCount
+    int32_t* idx = nullptr;             // objectIndices
+    uint32_t* cell = nullptr;           // node cell, 10 bits per axis (x | y << 10 | z << 20)
+    bool ordered = true;                // every box has min <= max (no NaN)
+    double seconds = 0.0;               // device build time (events)
+};
+
+void freeGpuTree(GpuTree& t);
+
+// Builds the tree of `spheres` (n x float4 center.xyz, radius; device memory) exactly as
+// Octree::build(maxDepth, maxSpheresPerNode) does.  Synchronous on `s`.  Returns "" or an error.
+std::string gpuBuildOctree(const float4* spheres, int32_t n, int32_t maxDepth, int32_t maxSpheresPerNode, hipStream_t s,
+                           GpuTree& out);
+
+// Device-side conversions of a built tree into the kernel layouts (ort_kernel.hip).  The
+// caller owns the outputs (hipMalloc'd here).  Compact: returns false with `why` when the
+// tree does not fit the compact layout (depth, 4 GiB offsets, plane check).
+struct CompactDev {
+    uint2* node = nullptr;
+    float4* leaf_sph = nullptr;
+    int32_t* leaf_idx = nullptr;
+    float* planes = nullptr;
+    size_t node_bytes = 0, leaf_bytes = 0, idx_bytes = 0, plane_bytes = 0;
+};
+bool gpuCompactLayout(const GpuTree& t, const float4* spheres, int maxDepth, hipStream_t s, CompactDev& out,
+                      std::string& why);
+struct ExplicitDev {
+    float4* nodeA = nullptr;
+    float4* nodeB = nullptr;
+    int32_t* cnt = nullptr;
+    int32_t* indices = nullptr;
+};
+std::string gpuExplicitLayout(const GpuTree& t, hipStream_t s, ExplicitDev& out);
+
+}  // namespace ort

@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "camera.h"
+#include "gpu_build.h"
 #include "layout.h"
 #include "ort_internal.h"
 #include "render_core.h"
@@ -647,6 +648,8 @@ struct ort_ctx {
     int persistent = 0;
     int packet = 0;     // ORT_OPT_PACKET: wave-level walk for camera rays (SALU-bound so far: off)
     DevBuf lut;         // rank LUT (global copy, for the packet kernel)
+    ort::GpuTree tree;  // reference-layout tree of the last ort_build_scene(keep_tree)
+    float build_ms = 0.0f;
     bool has_scene = false;
     int layout = ORT_LAYOUT_EXPLICIT;
     int depth = 0;
@@ -690,6 +693,7 @@ void free_scene(ort_ctx* c) {
     DevBuf* all[] = {&c->sph_cr, &c->sph_ma, &c->sph_fr, &c->node, &c->leaf_sph, &c->leaf_idx,
                      &c->planes, &c->nodeA, &c->nodeB, &c->cnt, &c->indices};
     for (DevBuf* b : all) free_buf(*b);
+    ort::freeGpuTree(c->tree);
     c->has_scene = false;
 }
 
@@ -702,22 +706,83 @@ int upload(ort_ctx* ctx, DevBuf& b, const void* src, size_t bytes) {
     return ORT_OK;
 }
 
+// Spheres -> device (bindings 0, 1 and the .xy of binding 2).
+int upload_spheres(ort_ctx* ctx, const float* cr, const float* ma, const float* fr, int32_t n) {
+    std::vector<float> fr2((size_t)n * 2);
+    for (int32_t i = 0; i < n; ++i) {
+        fr2[2 * (size_t)i] = fr[4 * (size_t)i];
+        fr2[2 * (size_t)i + 1] = fr[4 * (size_t)i + 1];
+    }
+    int rc;
+    if ((rc = upload(ctx, ctx->sph_cr, cr, 16 * (size_t)n))) return rc;
+    if ((rc = upload(ctx, ctx->sph_ma, ma, 16 * (size_t)n))) return rc;
+    if ((rc = upload(ctx, ctx->sph_fr, fr2.data(), 8 * (size_t)n))) return rc;
+    ctx->n_spheres = n;
+    return ORT_OK;
+}
+
+// ort_build_scene: GPU octree build (gpu_build.hip) straight into the kernel layout.
+int build_impl(ort_ctx* ctx, const float* cr, const float* ma, const float* fr, int32_t n, int32_t max_depth,
+               int32_t max_per_node, int32_t keep_tree) {
+    if (n <= 0) return fail(ctx, ORT_ERR_INVALID_ARG, "ort_build_scene: Sphere list is empty");
+    if (!cr || !ma || !fr) return fail(ctx, ORT_ERR_INVALID_ARG, "ort_build_scene: null sphere array");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    free_scene(ctx);
+    int rc;
+    if ((rc = upload_spheres(ctx, cr, ma, fr, n))) return rc;
+    ort::GpuTree t;
+    const std::string e = ort::gpuBuildOctree((const float4*)ctx->sph_cr.p, n, max_depth, max_per_node, ctx->stream, t);
+    if (!e.empty()) {
+        ort::freeGpuTree(t);
+        return fail(ctx, e.find("out of memory") != std::string::npos ? ORT_ERR_OUT_OF_MEMORY : ORT_ERR_INTERNAL,
+                    "ort_build_scene: " + e);
+    }
+    ctx->n_nodes = t.n_nodes;
+    ctx->n_indices = t.n_indices;
+    ctx->depth = t.depth;
+    ctx->ordered = t.ordered;
+    ctx->build_ms = (float)(t.seconds * 1e3);
+    std::string why;
+    ort::CompactDev cd;
+    const bool compact_ok = ctx->force_layout != ORT_LAYOUT_EXPLICIT &&
+                            ort::gpuCompactLayout(t, (const float4*)ctx->sph_cr.p, ORT_COMPACT_MAX_DEPTH, ctx->stream, cd, why);
+    if (compact_ok) {
+        ctx->layout = ORT_LAYOUT_COMPACT;
+        ctx->node = {cd.node, cd.node_bytes};
+        ctx->leaf_sph = {cd.leaf_sph, cd.leaf_bytes};
+        ctx->leaf_idx = {cd.leaf_idx, cd.idx_bytes};
+        ctx->planes = {cd.planes, cd.plane_bytes};
+    } else {
+        if (ctx->force_layout == ORT_LAYOUT_COMPACT) {
+            ort::freeGpuTree(t);
+            return fail(ctx, ORT_ERR_UNSUPPORTED, "compact layout forced but not possible: " + why);
+        }
+        ort::ExplicitDev ed;
+        const std::string ee = ort::gpuExplicitLayout(t, ctx->stream, ed);
+        ctx->nodeA = {ed.nodeA, 16 * (size_t)std::max(t.n_nodes, 1)};
+        ctx->nodeB = {ed.nodeB, 16 * (size_t)std::max(t.n_nodes, 1)};
+        ctx->cnt = {ed.cnt, 4 * (size_t)std::max(t.n_nodes, 1)};
+        ctx->indices = {ed.indices, 4 * (size_t)std::max<int64_t>(t.n_indices, 1)};
+        if (!ee.empty()) {
+            ort::freeGpuTree(t);
+            free_scene(ctx);
+            return fail(ctx, ORT_ERR_HIP, "ort_build_scene: " + ee);
+        }
+        ctx->layout = ORT_LAYOUT_EXPLICIT;
+    }
+    if (keep_tree) ctx->tree = t;
+    else ort::freeGpuTree(t);
+    ctx->has_scene = true;
+    return ORT_OK;
+}
+
 int upload_impl(ort_ctx* ctx, const ort::SceneInput& in) {
     const std::string bad = ort::validateScene(in);
     if (!bad.empty()) return fail(ctx, ORT_ERR_INVALID_ARG, "ort_upload_scene: " + bad);
     HIPCHK(ctx, hipSetDevice(ctx->device));
     free_scene(ctx);
-    // spheres: binding 0, 1 and the .xy of binding 2
-    std::vector<float> fr2((size_t)in.n_spheres * 2);
-    for (int32_t i = 0; i < in.n_spheres; ++i) {
-        fr2[2 * (size_t)i] = in.sph_fr[4 * (size_t)i];
-        fr2[2 * (size_t)i + 1] = in.sph_fr[4 * (size_t)i + 1];
-    }
     int rc;
-    if ((rc = upload(ctx, ctx->sph_cr, in.sph_cr, 16 * (size_t)in.n_spheres))) return rc;
-    if ((rc = upload(ctx, ctx->sph_ma, in.sph_ma, 16 * (size_t)in.n_spheres))) return rc;
-    if ((rc = upload(ctx, ctx->sph_fr, fr2.data(), 8 * (size_t)in.n_spheres))) return rc;
-    ctx->n_spheres = in.n_spheres;
+    if ((rc = upload_spheres(ctx, in.sph_cr, in.sph_ma, in.sph_fr, in.n_spheres))) return rc;
     ctx->n_nodes = in.n_nodes;
     ctx->n_indices = in.n_indices;
     ctx->layout = ORT_LAYOUT_EXPLICIT;
@@ -1138,6 +1203,43 @@ int ort_scene_get_info(const ort_ctx* ctx, ort_scene_info* info) {
     int64_t b = 0;
     for (const DevBuf* d : all) b += (int64_t)d->bytes;
     info->device_bytes = b;
+    return ORT_OK;
+}
+
+int ort_build_scene(ort_ctx* ctx, const float* sphere_center_radius, const float* sphere_mat_albedo,
+                    const float* sphere_fuzz_ri, int32_t n_spheres, int32_t max_depth, int32_t max_spheres_per_node,
+                    int32_t keep_tree) {
+    if (!ctx) return fail(nullptr, ORT_ERR_INVALID_ARG, "ort_build_scene: null ctx");
+    try {
+        return build_impl(ctx, sphere_center_radius, sphere_mat_albedo, sphere_fuzz_ri, n_spheres, max_depth,
+                          max_spheres_per_node, keep_tree);
+    } catch (const std::exception& ex) {
+        return fail(ctx, ORT_ERR_INTERNAL, std::string("ort_build_scene: ") + ex.what());
+    }
+}
+
+int ort_scene_export_octree(ort_ctx* ctx, float* node_min, float* node_max, int32_t* children_offset,
+                            int32_t* objects_offset, int32_t* object_count, int32_t* object_indices) {
+    if (!ctx) return fail(nullptr, ORT_ERR_INVALID_ARG, "ort_scene_export_octree: null ctx");
+    const ort::GpuTree& t = ctx->tree;
+    if (!ctx->has_scene || !t.co)
+        return fail(ctx, ORT_ERR_NO_SCENE, "ort_scene_export_octree: no GPU-built tree kept (ort_build_scene keep_tree)");
+    if (!node_min || !node_max || !children_offset || !objects_offset || !object_count || (!object_indices && t.n_indices))
+        return fail(ctx, ORT_ERR_INVALID_ARG, "ort_scene_export_octree: null output");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    const size_t n = (size_t)t.n_nodes;
+    HIPCHK(ctx, hipMemcpy(node_min, t.node_min, 12 * n, hipMemcpyDeviceToHost));
+    HIPCHK(ctx, hipMemcpy(node_max, t.node_max, 12 * n, hipMemcpyDeviceToHost));
+    HIPCHK(ctx, hipMemcpy(children_offset, t.co, 4 * n, hipMemcpyDeviceToHost));
+    HIPCHK(ctx, hipMemcpy(objects_offset, t.oo, 4 * n, hipMemcpyDeviceToHost));
+    HIPCHK(ctx, hipMemcpy(object_count, t.cnt, 4 * n, hipMemcpyDeviceToHost));
+    if (t.n_indices) HIPCHK(ctx, hipMemcpy(object_indices, t.idx, 4 * (size_t)t.n_indices, hipMemcpyDeviceToHost));
+    return ORT_OK;
+}
+
+int ort_last_build_ms(const ort_ctx* ctx, float* ms) {
+    if (!ctx || !ms) return fail(nullptr, ORT_ERR_INVALID_ARG, "ort_last_build_ms: null argument");
+    *ms = ctx->build_ms;
     return ORT_OK;
 }
 

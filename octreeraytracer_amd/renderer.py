@@ -144,6 +144,35 @@ class Renderer:
                                                L.fptr(nmin), L.fptr(nmax), L.iptr(co), L.iptr(oo), L.iptr(cnt),
                                                tree.n_nodes, L.iptr(idx), tree.n_indices))
 
+    def build_scene(self, spheres: SphereSet, max_depth: int, max_spheres_per_node: int, keep_tree: bool = False):
+        """Build the octree on the GPU (ort_build_scene: the reference builder's exact output)
+        and make it this renderer's scene.  keep_tree: keep the reference-layout tree on the
+        device for export_octree()."""
+        cr = np.ascontiguousarray(spheres.center_radius, np.float32)
+        ma = np.ascontiguousarray(spheres.mat_albedo, np.float32)
+        fr = np.ascontiguousarray(spheres.fuzz_ri, np.float32)
+        self._check(self._lib.ort_build_scene(self._ctx, L.fptr(cr), L.fptr(ma), L.fptr(fr), spheres.n,
+                                              int(max_depth), int(max_spheres_per_node), int(bool(keep_tree))))
+
+    def export_octree(self) -> FlatOctree:
+        """The kept GPU-built tree (build_scene(keep_tree=True)) as a host FlatOctree."""
+        i = self.info()
+        n, k = i["n_nodes"], i["n_indices"]
+        nmin = np.empty((n, 3), np.float32)
+        nmax = np.empty((n, 3), np.float32)
+        co = np.empty(n, np.int32)
+        oo = np.empty(n, np.int32)
+        cnt = np.empty(n, np.int32)
+        idx = np.empty(max(k, 1), np.int32)
+        self._check(self._lib.ort_scene_export_octree(self._ctx, L.fptr(nmin), L.fptr(nmax), L.iptr(co), L.iptr(oo),
+                                                      L.iptr(cnt), L.iptr(idx)))
+        return FlatOctree(nmin, nmax, co, oo, cnt, idx[:k])
+
+    def last_build_ms(self) -> float:
+        ms = C.c_float()
+        self._check(self._lib.ort_last_build_ms(self._ctx, C.byref(ms)))
+        return ms.value
+
     def info(self) -> dict:
         i = L.OrtSceneInfo()
         self._check(self._lib.ort_scene_get_info(self._ctx, C.byref(i)))
