@@ -3,7 +3,9 @@
 
 One step = one frame of primary rays (numSamples=1, maxDepth=1 -> one traversal per pixel)
 over the seeded synthetic sphere cloud, rendered by the gfx950 kernel with the scene
-already resident in HBM.  With N GPUs (one process per GPU, torchrun) the frame is
+already resident in HBM (octree built on the GPU by ort_build_scene, byte-identical to the
+reference builder; --host-build uses the host builder + upload instead).  `value` counts
+traced rays (octree traversals) per second, which for primary-only configs is W*H/s.  With N GPUs (one process per GPU, torchrun) the frame is
 partitioned into 16-row bands dealt round-robin to the ranks; each rank renders its bands
 into device memory and the bands are gathered to rank 0 over RCCL and de-interleaved into
 the final frame -- the gather is inside the timed region.  Total work per step is one
@@ -49,6 +51,8 @@ def parse():
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--host-build", action="store_true", help="build the octree on the host and upload it "
+                    "(default: ort_build_scene, the GPU builder)")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"),
                     help="PMC-measured HBM bytes per launch (written by tools/pmc_traffic.py)")
     ap.add_argument("--save", default="", help="rank 0: save the assembled frame (.pfm/.png)")
@@ -73,14 +77,22 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    t0 = time.time()
     spheres = ort.random_spheres(NSPH, args.seed)
-    tree = ort.build_octree(spheres, DEPTH, MPN)
-    t_build = time.time() - t0
     r = ort.Renderer(local)
-    t0 = time.time()
-    r.upload(spheres, tree)
-    t_upload = time.time() - t0
+    setup = {}
+    tree = None
+    if args.host_build:  # the reference's CPU builder (restated) + upload
+        t0 = time.time()
+        tree = ort.build_octree(spheres, DEPTH, MPN)
+        setup["host_octree_build_s"] = round(time.time() - t0, 3)
+        t0 = time.time()
+        r.upload(spheres, tree)
+        setup["upload_s"] = round(time.time() - t0, 3)
+    else:  # GPU octree builder, same tree byte for byte (tests/test_gpu_build.py)
+        t0 = time.time()
+        r.build_scene(spheres, DEPTH, MPN)
+        setup["gpu_octree_build_ms"] = round(r.last_build_ms(), 2)
+        setup["build_scene_wall_s"] = round(time.time() - t0, 3)
     info = r.info()
     p = ort.FrameParams.default_camera(W, H, num_samples=NS, max_depth=MAXD)
 
@@ -123,12 +135,16 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
 
-    # algorithmic traffic of this rank's launch (counting variant, untimed)
+    # algorithmic traffic of this rank's launch (counting variant, untimed); the traced rays
+    # of a step = traversals summed over the ranks (W*H*spp for primary-only configs)
     counts = r.count_traffic(p, tile)
     alg_bytes = ort.algorithmic_bytes(counts)
     kern_avg_ms = float(np.mean(kern_ms))
     trace_avg_ms = float(np.mean(trace_ms))
-    rays_per_frame = W * H * NS
+    trav = torch.tensor([counts["traversals"]], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(trav)
+    rays_per_frame = int(trav.item())
 
     result = None
     if rank == 0:
@@ -158,12 +174,13 @@ def main():
             "dtype": "f32",
             "data": "synthetic (seeded generateRandomSpheres restatement, mt19937 seed %d)" % args.seed,
             "config": {
-                "workload": f"{args.config}: {W}x{H} primary rays (spp={NS}, bounces={MAXD}), {NSPH} spheres, "
+                "workload": f"{args.config}: {W}x{H} camera rays (spp={NS}, bounces={MAXD}), {NSPH} spheres, "
                             f"octree depth {DEPTH}, maxSpheresPerNode {MPN}",
                 "width": W, "height": H, "spheres": NSPH, "octree_depth": DEPTH, "max_spheres_per_node": MPN,
                 "num_samples": NS, "max_bounces": MAXD, "nodes": info["n_nodes"], "indices": info["n_indices"],
                 "layout": info["layout"], "partition": "16-row bands round-robin + RCCL gather" if world > 1
-                else "full frame", "rays_per_step": rays_per_frame,
+                else "full frame", "rays_per_step": rays_per_frame, "rays": "traced rays (octree traversals), "
+                "all bounces and ranks",
             },
             "frame_gpu_ms_avg": round(kern_avg_ms, 4),
             "trace_kernel_ms_avg": round(trace_avg_ms, 4),
@@ -183,9 +200,13 @@ def main():
                         "frame / trace-kernel time; this kernel reads far fewer bytes (compact layout, L2/MALL "
                         "residency) and is instruction-issue bound -- see traffic and DESIGN.md",
             },
-            "setup_s": {"scene_build": round(t_build, 3), "upload": round(t_upload, 3)},
+            "setup": setup,
         }
         if world == 1 and not args.no_cpu_baseline:
+            if tree is None:
+                t0 = time.time()
+                tree = ort.build_octree(spheres, DEPTH, MPN)  # the oracle walks the host tree
+                setup["host_octree_build_s"] = round(time.time() - t0, 3)
             result["cpu_baseline"] = cpu_baseline(spheres, tree, p, args.cpu_seconds)
         if args.save:
             img = frame.cpu().numpy()
@@ -215,7 +236,7 @@ def cpu_baseline(spheres, tree, p, budget_s):
     dt, stride = run(n)
     rays = n * p.width * p.num_samples
     return {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": f"{n} of {p.height} rows (every {stride}th), {rays} primary rays, {dt:.1f} s wall; "
+            "sample": f"{n} of {p.height} rows (every {stride}th), {rays} camera rays, {dt:.1f} s wall; "
                       f"oracle/ort_oracle.c -O3, OpenMP dynamic over rows"}
 
 

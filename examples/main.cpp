@@ -30,6 +30,7 @@ int main(int argc, char** argv) {
         else if (!std::strcmp(argv[i], "--no-octree")) cfg.useOctree = 0;
         else if (!std::strcmp(argv[i], "--prebuilt")) cfg.usePrebuilt = 1;
         else if (!std::strcmp(argv[i], "--debug")) cfg.debug = 1;
+        else if (!std::strcmp(argv[i], "--gpu-build")) cfg.gpuBuild = true;
         else if (!std::strcmp(argv[i], "--seed")) cfg.seed = (uint32_t)std::strtoul(next(), nullptr, 10);
         else if (!std::strcmp(argv[i], "--device")) cfg.device = std::atoi(next());
         else if (!std::strcmp(argv[i], "--stats")) { cfg.collectStats = true; cfg.outputFile = next(); }

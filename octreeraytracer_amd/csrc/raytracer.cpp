@@ -54,6 +54,7 @@ void Raytracer::setupScene() {
     const int maxDepth = cfg.debug ? cfg.debugDepth : cfg.maxDepth;
     const int maxSpheresPerNode = cfg.debug ? cfg.debugSpheresPerNode : cfg.maxSpheresPerNode;
     octree = Octree(maxDepth, maxSpheresPerNode);
+    if (cfg.gpuBuild && !cfg.debug) return;  // setupBuffers builds it on the device
     octree.build(spheres, cfg.debug);
     if (cfg.debug) octree.printFlattenedTree();
 }
@@ -62,9 +63,18 @@ void Raytracer::setupBuffers() {
     // SoA packing of src/raytracer.cpp:87-101, then one upload (replaces 7x glBufferData)
     std::vector<float> cr(4 * spheres.size()), ma(4 * spheres.size()), fr(4 * spheres.size());
     ort::packSpheres(spheres, cr.data(), ma.data(), fr.data());
-    const int rc = ort_upload_octree_nodes(ctx, cr.data(), ma.data(), fr.data(), (int32_t)spheres.size(),
-                                           octree.flattenedTree.data(), (int32_t)octree.flattenedTree.size(),
-                                           octree.objectIndices.data(), (int64_t)octree.objectIndices.size());
+    int rc;
+    if (cfg.gpuBuild && !cfg.debug) {
+        rc = ort_build_scene(ctx, cr.data(), ma.data(), fr.data(), (int32_t)spheres.size(), octree.getMaxDepth(),
+                             octree.getMaxSpheresPerNode(), 0);
+        float ms = 0.0f;
+        if (rc == ORT_OK) ort_last_build_ms(ctx, &ms);
+        gpuBuildSeconds = ms * 1e-3;
+    } else {
+        rc = ort_upload_octree_nodes(ctx, cr.data(), ma.data(), fr.data(), (int32_t)spheres.size(),
+                                     octree.flattenedTree.data(), (int32_t)octree.flattenedTree.size(),
+                                     octree.objectIndices.data(), (int64_t)octree.objectIndices.size());
+    }
     if (rc != ORT_OK) std::cerr << "scene upload failed: " << ort_last_error(ctx) << std::endl;
     sceneReady = rc == ORT_OK;
 }
@@ -177,5 +187,6 @@ void Raytracer::saveStats() {
     const double fpsAvg = fpsTotal / clean.size();
     outFile << cfg.useOctree << ";" << cfg.numSpheres << ";" << cfg.maxDepth << ";" << cfg.maxSpheresPerNode << ";"
             << cfg.numSamples << ";" << cfg.maxRaysDepth << ";" << cfg.width << ";" << cfg.height << ";" << mn << ";" << mx
-            << ";" << avg << ";" << 1.0 / mx << ";" << 1.0 / mn << ";" << fpsAvg << ";" << octree.buildTime << std::endl;
+            << ";" << avg << ";" << 1.0 / mx << ";" << 1.0 / mn << ";" << fpsAvg << ";"
+            << ((cfg.gpuBuild && !cfg.debug) ? gpuBuildSeconds : octree.buildTime) << std::endl;
 }

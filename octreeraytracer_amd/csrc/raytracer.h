@@ -39,6 +39,8 @@ struct RaytracerConfig {
     int device = 0;                // HIP device of the context
     int frames = 50;               // frames of run() (the reference stops after 50 with stats)
     int warmupFrames = 15;         // src/raytracer.cpp:455
+    bool gpuBuild = false;         // build the octree on the GPU (ort_build_scene, same tree) instead
+                                   // of Octree::build on the host; getOctree() then stays empty
 };
 
 class Raytracer {
@@ -78,6 +80,7 @@ private:
     int frameCount;
     std::vector<double> renderTimes;
     std::vector<float> frame;
+    double gpuBuildSeconds = 0.0;
 
     void setupScene();
     void setupBuffers();
