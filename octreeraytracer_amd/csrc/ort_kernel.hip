@@ -52,6 +52,8 @@ struct PipeArgs {
     int refill;       // persistent trace: refill a wave when at least this many lanes idle
     int rays_stored;  // bounce-0 rays were written by ort_raygen_kernel (persistent pipeline)
     const uint8_t* lut;  // global copy of the rank LUT (ort::rank_lut_entry), 8 x 256 bytes
+    const int* qlist;    // bounce >= 1: the alive path slots (compacted, increasing), or null = all
+    const int* qcount;   // their number (device)
     int2* hit;        // per path: {entry (-1 miss), t bits}
     int* defer_list;
     int* sync;        // [0] deferred count, [1] work cursor of the persistent trace
@@ -228,6 +230,14 @@ __global__ void __launch_bounds__(kBlock) ort_trace_persistent(PipeArgs A) {
     flush_counts<COUNT>(cnt, A.counters);
 }
 
+// Bounce >= 1 with a compacted list: thread index -> alive path slot (false past the list).
+__device__ inline bool list_slot(const PipeArgs& A, int& k) {
+    if (!A.qlist) return true;
+    if (k >= *A.qcount) return false;
+    k = A.qlist[k];
+    return true;
+}
+
 // Path-slot ray for the trace kernels: bounce 0 generates the sample's camera ray here
 // (main() up to radiance()'s first line; the shade kernel regenerates it identically),
 // later bounces read the ray the previous shade kernel stored.
@@ -262,8 +272,10 @@ __device__ inline ort::Ray slot_ray(const PipeArgs& A, int k, bool& alive) {
 template <bool COUNT, bool PRIMARY, bool DEEP>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) ort_trace_compact(PipeArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    if (!PRIMARY && A.qlist && (int)(blockIdx.x * kBlock) >= *A.qcount) return;  // whole block past the list
     LdsView L = setup_lds<true>(smem, A.S);
-    const int k = blockIdx.x * kBlock + threadIdx.x;
+    int k = blockIdx.x * kBlock + threadIdx.x;
+    if (!PRIMARY && !list_slot(A, k)) return;
     bool alive;
     const ort::Ray ray = slot_ray<PRIMARY>(A, k, alive);
     if (!alive) return;
@@ -492,7 +504,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))
 // One-ray-per-lane trace for the explicit layout (MODE 1) and brute force (MODE 2).
 template <int MODE, bool COUNT, bool PRIMARY>
 __global__ void __launch_bounds__(kBlock) ort_trace_kernel(PipeArgs A) {
-    const int k = blockIdx.x * kBlock + threadIdx.x;
+    int k = blockIdx.x * kBlock + threadIdx.x;
+    if (!PRIMARY && !list_slot(A, k)) return;
     bool alive;
     const ort::Ray ray = slot_ray<PRIMARY>(A, k, alive);
     if (!alive) return;
@@ -537,16 +550,18 @@ __global__ void __launch_bounds__(kBlock) ort_trace_exact(PipeArgs A) {
 // DIRECT (1 sample, 1 bounce): writes the final pixel.
 template <int MODE, bool FIRST, bool DIRECT>
 __global__ void __launch_bounds__(kBlock) ort_shade_kernel(PipeArgs A) {
-    const int k = blockIdx.x * kBlock + threadIdx.x;
+    int k = blockIdx.x * kBlock + threadIdx.x;
+    if (!FIRST && !list_slot(A, k)) return;
     int col, row;
-    if (!slot_coords(A, k, col, row)) return;
-    const int y = tile_row_to_y(A.tm, row);
+    const bool in_tile = slot_coords(A, k, col, row);
+    const int y = in_tile ? tile_row_to_y(A.tm, row) : 0;
     const size_t p = (size_t)row * A.tm.tw + col;
-    if (y >= A.pp.H) {
-        if (DIRECT) {
+    if (!in_tile || y >= A.pp.H) {
+        if (DIRECT && in_tile) {
             float* o = A.out + 3 * p;
             o[0] = 0.0f; o[1] = 0.0f; o[2] = 0.0f;
         }
+        if (FIRST && !DIRECT) A.pd[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // never alive (compaction)
         return;
     }
     bool alive = true;
@@ -662,6 +677,7 @@ struct ort_ctx {
     DevBuf scratch_out, counters;
     // wavefront pipeline state, sized for the largest tile rendered so far
     DevBuf hit, defer_list, defer_count, po, pd, pc, prng, pcol;
+    DevBuf qlist, qcount, qtemp;  // bounce >= 1 path compaction
 };
 
 namespace {
@@ -976,6 +992,14 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
             (rc = ensure(ctx, ctx->pcol, 16 * slots)))
             return rc;
     }
+    const bool compact = !direct && !ctx->persistent && p->max_depth > 1;
+    size_t qtemp_bytes = 0;
+    if (compact) {
+        qtemp_bytes = ort::selectAliveTempBytes((int)slots);
+        if ((rc = ensure(ctx, ctx->qlist, 4 * slots)) || (rc = ensure(ctx, ctx->qcount, 64)) ||
+            (rc = ensure(ctx, ctx->qtemp, std::max<size_t>(qtemp_bytes, 16))))
+            return rc;
+    }
     PipeArgs a;
     std::memset(&a, 0, sizeof(a));
     a.pp = pixel_params(p);
@@ -1006,6 +1030,8 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     for (int smp = 0; smp < ns; ++smp) {
         a.sample = smp;
         a.rays_stored = pblocks > 0;
+        a.qlist = nullptr;  // bounce 0: every slot
+        a.qcount = nullptr;
         if (pblocks > 0) {  // the persistent kernel refills lanes from stored rays
             hipLaunchKernelGGL(ort_raygen_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, s, a);
             if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "ort_raygen_kernel launch");
@@ -1038,6 +1064,13 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
             }
             e = launch_shade(mode, b == 0, direct, a, (int)blocks, s);
             if (e != hipSuccess) return hip_fail(ctx, e, "ort_shade_kernel launch");
+            if (compact && !a.nobounce && b + 1 < bounces) {  // the next bounce walks only the alive paths
+                e = ort::selectAlive(ctx->qtemp.p, qtemp_bytes, (const float4*)ctx->pd.p, (int)slots, (int*)ctx->qlist.p,
+                                     (int*)ctx->qcount.p, s);
+                if (e != hipSuccess) return hip_fail(ctx, e, "path compaction");
+                a.qlist = (const int*)ctx->qlist.p;
+                a.qcount = (const int*)ctx->qcount.p;
+            }
         }
     }
     if (!direct) {
@@ -1108,7 +1141,8 @@ int ort_destroy(ort_ctx* ctx) {
     free_buf(ctx->scratch_out);
     free_buf(ctx->counters);
     free_buf(ctx->lut);
-    DevBuf* pipe[] = {&ctx->hit, &ctx->defer_list, &ctx->defer_count, &ctx->po, &ctx->pd, &ctx->pc, &ctx->prng, &ctx->pcol};
+    DevBuf* pipe[] = {&ctx->hit, &ctx->defer_list, &ctx->defer_count, &ctx->po, &ctx->pd, &ctx->pc, &ctx->prng, &ctx->pcol,
+                      &ctx->qlist, &ctx->qcount, &ctx->qtemp};
     for (DevBuf* b : pipe) free_buf(*b);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);

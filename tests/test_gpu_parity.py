@@ -191,3 +191,18 @@ def test_c3_counters_match_oracle_on_rows(ort, oracle, renderer, scene_c3):
     tile = ort.Tile(0, 3840, 7, 16 * 4, 4, 135)  # 64 rows spread over the frame
     _, want = oracle.render(s, t, p, 0, 7, 3840, 64, band_height=4, band_stride=135, counts=True)
     assert renderer.count_traffic(p, tile) == want
+
+
+def test_bounce_compaction_after_larger_frames(ort, oracle, renderer, scene_c2):
+    """Bounces >= 1 walk only the alive paths (compacted list).  Slots a previous, larger
+    render left alive must never leak into a later, smaller tile."""
+    s, t = scene_c2
+    renderer.upload(s, t)
+    big = ort.FrameParams.default_camera(1920, 1080, num_samples=1, max_depth=4)
+    renderer.render(big, ort.Tile(0, 1920, 0, 256))
+    p = ort.FrameParams.default_camera(1920, 1080, num_samples=2, max_depth=5)
+    for tile in (ort.Tile(900, 70, 500, 30), ort.Tile(0, 1920, 3, 40, 8, 27)):
+        got = renderer.render(p, tile)
+        ref = oracle.render(s, t, p, tile.x0, tile.y0, tile.width, tile.rows, band_height=tile.band_height,
+                            band_stride=tile.band_stride)
+        assert_same(got, ref, f"compaction tile {tile}")
