@@ -86,6 +86,8 @@ typedef struct ort_scene_info {
 #define ORT_OPT_REFILL 3           /* persistent trace: refill a wave when >= value of its 64 lanes idle (16) */
 #define ORT_OPT_PERSISTENT 4       /* 1: persistent trace kernel with per-lane ray refill (default 0) */
 #define ORT_OPT_PACKET 5           /* 1: wave-level walk for camera rays; 0 (default): per-lane walk (same pixels) */
+#define ORT_OPT_SORT_PATHS 6       /* 1 (default): sort the alive paths by direction octant + origin cell between
+                                      bounces (coherence; same pixels); 0: keep them in slot order */
 
 /* Traffic counters (ort_count_traffic), in the REFERENCE layout's terms. */
 #define ORT_COUNT_NODES_POPPED 0

@@ -61,3 +61,18 @@ namespace ort {
 size_t selectAliveTempBytes(int n);
 hipError_t selectAlive(void* temp, size_t temp_bytes, const float4* pd, int n, int* out, int* count, hipStream_t s);
 }  // namespace ort
+
+namespace ort {
+// Coherence sort of the alive paths (ORT_OPT_SORT_PATHS): key = direction octant (3 bits) |
+// Morton code of the origin in the root box (9 bits per axis); dead slots get the largest
+// key, so the sorted values are the alive slots first, *count of them (device).
+struct SortBuffers {
+    uint32_t* keys_in;
+    uint32_t* keys_out;
+    int* vals_in;
+    int* vals_out;  // = the list the next bounce walks
+};
+size_t sortAliveTempBytes(int n);
+hipError_t sortAlive(void* temp, size_t temp_bytes, const float4* po, const float4* pd, int n, const float* root_lo,
+                     const float* root_hi, const SortBuffers& b, int* count, hipStream_t s);
+}  // namespace ort

@@ -656,4 +656,65 @@ hipError_t selectAlive(void* temp, size_t temp_bytes, const float4* pd, int n, i
     return rocprim::select(temp, temp_bytes, rocprim::counting_iterator<int>(0), flags, out, count, (size_t)n, s);
 }
 
+namespace {
+__device__ __forceinline__ uint32_t spread3(uint32_t v) {  // 9 bits -> every third bit
+    v &= 0x1ffu;
+    v = (v | (v << 16)) & 0x030000ffu;
+    v = (v | (v << 8)) & 0x0300f00fu;
+    v = (v | (v << 4)) & 0x030c30c3u;
+    v = (v | (v << 2)) & 0x09249249u;
+    return v;
+}
+__device__ __forceinline__ uint32_t quant9(float x, float lo, float scale) {
+    const float q = (x - lo) * scale;
+    return q <= 0.0f ? 0u : (q >= 511.0f ? 511u : (uint32_t)q);  // NaN -> 0
+}
+__global__ void k_path_keys(const float4* po, const float4* pd, int n, float3 lo, float3 sc, uint32_t* keys, int* vals,
+                            int* count) {
+    const int k = blockIdx.x * kB + threadIdx.x;
+    if (k >= n) return;
+    const float4 d = pd[k];
+    const bool alive = d.w != 0.0f;
+    uint32_t key = 0xffffffffu;
+    if (alive) {
+        const float4 o = po[k];
+        const uint32_t m = ((uint32_t)(d.z < 0.0f) << 2) | ((uint32_t)(d.x < 0.0f) << 1) | (uint32_t)(d.y < 0.0f);
+        key = (m << 27) | (spread3(quant9(o.x, lo.x, sc.x)) << 2) | (spread3(quant9(o.y, lo.y, sc.y)) << 1) |
+              spread3(quant9(o.z, lo.z, sc.z));
+    }
+    keys[k] = key;
+    vals[k] = k;
+    const unsigned long long m = __ballot(alive);
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(count, __popcll(m));
+}
+}  // namespace
+
+size_t sortAliveTempBytes(int n) {
+    size_t tb = 0;
+    (void)rocprim::radix_sort_pairs(nullptr, tb, (uint32_t*)nullptr, (uint32_t*)nullptr, (int*)nullptr, (int*)nullptr,
+                                    (size_t)std::max(n, 1), 0, 31);
+    return tb;
+}
+
+hipError_t sortAlive(void* temp, size_t temp_bytes, const float4* po, const float4* pd, int n, const float* root_lo,
+                     const float* root_hi, const SortBuffers& b, int* count, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(count, 0, sizeof(int), s);
+    if (e != hipSuccess) return e;
+    float3 lo, sc;
+    float l[3], c[3];
+    for (int a = 0; a < 3; ++a) {
+        const float ext = root_hi[a] - root_lo[a];
+        l[a] = root_lo[a];
+        c[a] = (ext > 0.0f && ext < 3.0e38f) ? 512.0f / ext : 0.0f;
+    }
+    lo = make_float3(l[0], l[1], l[2]);
+    sc = make_float3(c[0], c[1], c[2]);
+    hipLaunchKernelGGL(k_path_keys, dim3((n + kB - 1) / kB), dim3(kB), 0, s, po, pd, n, lo, sc, b.keys_in, b.vals_in,
+                       count);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    // alive keys are < 2^30, dead keys 0xffffffff: on bits [0, 31) every dead key sorts after
+    // every alive one
+    return rocprim::radix_sort_pairs(temp, temp_bytes, b.keys_in, b.keys_out, b.vals_in, b.vals_out, (size_t)n, 0, 31, s);
+}
+
 }  // namespace ort

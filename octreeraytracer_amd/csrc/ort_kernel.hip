@@ -662,6 +662,8 @@ struct ort_ctx {
     int refill = 16;
     int persistent = 0;
     int packet = 0;     // ORT_OPT_PACKET: wave-level walk for camera rays (SALU-bound so far: off)
+    int sort_paths = 1; // ORT_OPT_SORT_PATHS: coherence-sort the alive paths between bounces
+    float root_lo[3] = {0, 0, 0}, root_hi[3] = {0, 0, 0};  // root box (coherence-sort key)
     DevBuf lut;         // rank LUT (global copy, for the packet kernel)
     ort::GpuTree tree;  // reference-layout tree of the last ort_build_scene(keep_tree)
     float build_ms = 0.0f;
@@ -678,6 +680,7 @@ struct ort_ctx {
     // wavefront pipeline state, sized for the largest tile rendered so far
     DevBuf hit, defer_list, defer_count, po, pd, pc, prng, pcol;
     DevBuf qlist, qcount, qtemp;  // bounce >= 1 path compaction
+    DevBuf skeys, skeys2, svals;  // coherence sort
 };
 
 namespace {
@@ -722,6 +725,28 @@ int upload(ort_ctx* ctx, DevBuf& b, const void* src, size_t bytes) {
     return ORT_OK;
 }
 
+// Root box for the coherence-sort key: the tree's root node, or the spheres' bounds when
+// there is no tree (brute force).  Only orders work; never affects pixels.
+void set_root_box(ort_ctx* ctx, const float* nmin, const float* nmax, const float* cr, int32_t n) {
+    for (int a = 0; a < 3; ++a) {
+        ctx->root_lo[a] = 0.0f;
+        ctx->root_hi[a] = 0.0f;
+    }
+    if (nmin && nmax) {
+        for (int a = 0; a < 3; ++a) {
+            ctx->root_lo[a] = nmin[a];
+            ctx->root_hi[a] = nmax[a];
+        }
+        return;
+    }
+    for (int32_t i = 0; i < n && cr; ++i)
+        for (int a = 0; a < 3; ++a) {
+            const float lo = cr[4 * (size_t)i + a] - cr[4 * (size_t)i + 3], hi = cr[4 * (size_t)i + a] + cr[4 * (size_t)i + 3];
+            if (i == 0 || lo < ctx->root_lo[a]) ctx->root_lo[a] = lo;
+            if (i == 0 || hi > ctx->root_hi[a]) ctx->root_hi[a] = hi;
+        }
+}
+
 // Spheres -> device (bindings 0, 1 and the .xy of binding 2).
 int upload_spheres(ort_ctx* ctx, const float* cr, const float* ma, const float* fr, int32_t n) {
     std::vector<float> fr2((size_t)n * 2);
@@ -757,6 +782,12 @@ int build_impl(ort_ctx* ctx, const float* cr, const float* ma, const float* fr, 
     ctx->n_indices = t.n_indices;
     ctx->depth = t.depth;
     ctx->ordered = t.ordered;
+    {
+        float lo[3], hi[3];
+        if (hipMemcpy(lo, t.node_min, 12, hipMemcpyDeviceToHost) == hipSuccess &&
+            hipMemcpy(hi, t.node_max, 12, hipMemcpyDeviceToHost) == hipSuccess)
+            set_root_box(ctx, lo, hi, nullptr, 0);
+    }
     ctx->build_ms = (float)(t.seconds * 1e3);
     std::string why;
     ort::CompactDev cd;
@@ -803,6 +834,8 @@ int upload_impl(ort_ctx* ctx, const ort::SceneInput& in) {
     ctx->n_indices = in.n_indices;
     ctx->layout = ORT_LAYOUT_EXPLICIT;
     ctx->depth = 0;
+    set_root_box(ctx, in.n_nodes > 0 ? in.node_min : nullptr, in.n_nodes > 0 ? in.node_max : nullptr, in.sph_cr,
+                 in.n_spheres);
     if (in.n_nodes > 0) {
         ort::CompactLayout cl;
         std::string why;
@@ -993,11 +1026,15 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
             return rc;
     }
     const bool compact = !direct && !ctx->persistent && p->max_depth > 1;
+    const bool sorted = compact && ctx->sort_paths;
     size_t qtemp_bytes = 0;
     if (compact) {
-        qtemp_bytes = ort::selectAliveTempBytes((int)slots);
+        qtemp_bytes = sorted ? ort::sortAliveTempBytes((int)slots) : ort::selectAliveTempBytes((int)slots);
         if ((rc = ensure(ctx, ctx->qlist, 4 * slots)) || (rc = ensure(ctx, ctx->qcount, 64)) ||
             (rc = ensure(ctx, ctx->qtemp, std::max<size_t>(qtemp_bytes, 16))))
+            return rc;
+        if (sorted && ((rc = ensure(ctx, ctx->skeys, 4 * slots)) || (rc = ensure(ctx, ctx->skeys2, 4 * slots)) ||
+                       (rc = ensure(ctx, ctx->svals, 4 * slots))))
             return rc;
     }
     PipeArgs a;
@@ -1065,8 +1102,15 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
             e = launch_shade(mode, b == 0, direct, a, (int)blocks, s);
             if (e != hipSuccess) return hip_fail(ctx, e, "ort_shade_kernel launch");
             if (compact && !a.nobounce && b + 1 < bounces) {  // the next bounce walks only the alive paths
-                e = ort::selectAlive(ctx->qtemp.p, qtemp_bytes, (const float4*)ctx->pd.p, (int)slots, (int*)ctx->qlist.p,
-                                     (int*)ctx->qcount.p, s);
+                if (sorted) {
+                    const ort::SortBuffers sb{(uint32_t*)ctx->skeys.p, (uint32_t*)ctx->skeys2.p, (int*)ctx->svals.p,
+                                              (int*)ctx->qlist.p};
+                    e = ort::sortAlive(ctx->qtemp.p, qtemp_bytes, (const float4*)ctx->po.p, (const float4*)ctx->pd.p,
+                                       (int)slots, ctx->root_lo, ctx->root_hi, sb, (int*)ctx->qcount.p, s);
+                } else {
+                    e = ort::selectAlive(ctx->qtemp.p, qtemp_bytes, (const float4*)ctx->pd.p, (int)slots,
+                                         (int*)ctx->qlist.p, (int*)ctx->qcount.p, s);
+                }
                 if (e != hipSuccess) return hip_fail(ctx, e, "path compaction");
                 a.qlist = (const int*)ctx->qlist.p;
                 a.qcount = (const int*)ctx->qcount.p;
@@ -1142,7 +1186,7 @@ int ort_destroy(ort_ctx* ctx) {
     free_buf(ctx->counters);
     free_buf(ctx->lut);
     DevBuf* pipe[] = {&ctx->hit, &ctx->defer_list, &ctx->defer_count, &ctx->po, &ctx->pd, &ctx->pc, &ctx->prng, &ctx->pcol,
-                      &ctx->qlist, &ctx->qcount, &ctx->qtemp};
+                      &ctx->qlist, &ctx->qcount, &ctx->qtemp, &ctx->skeys, &ctx->skeys2, &ctx->svals};
     for (DevBuf* b : pipe) free_buf(*b);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
@@ -1170,6 +1214,10 @@ int ort_set_option(ort_ctx* ctx, int option, int value) {
     }
     if (option == ORT_OPT_PACKET) {
         ctx->packet = value ? 1 : 0;
+        return ORT_OK;
+    }
+    if (option == ORT_OPT_SORT_PATHS) {
+        ctx->sort_paths = value ? 1 : 0;
         return ORT_OK;
     }
     if (option == ORT_OPT_REFILL) {

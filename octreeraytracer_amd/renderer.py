@@ -118,6 +118,10 @@ class Renderer:
         """Wave-level (packet) walk for camera rays (default off: SALU-bound); same pixels."""
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_PACKET, int(bool(on))))
 
+    def set_sort_paths(self, on: bool):
+        """Coherence-sort the alive paths between bounces (default on); same pixels."""
+        self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_SORT_PATHS, int(bool(on))))
+
     def set_persistent(self, on: bool):
         """Use the persistent trace kernel with per-lane ray refill (default: one ray per lane)."""
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_PERSISTENT, int(bool(on))))
