@@ -99,19 +99,36 @@ def main():
     # partition: 16-row bands dealt round-robin; every rank renders the same number of rows
     from octreeraytracer_amd.distributed import FrameGather, rank_tile
     tile = rank_tile(W, H, rank, world)
-    out = torch.empty((tile.rows, W, 3), dtype=torch.float32, device="cuda")
-    gather = FrameGather(dist, W, H, world, rank, "cuda")
+    # two band tiles per rank: frame k's gather/assembly overlaps frame k+1's render
+    outs = [torch.empty((tile.rows, W, 3), dtype=torch.float32, device="cuda") for _ in range(2)]
+    out = outs[0]
+    gather = FrameGather(dist, W, H, world, rank, "cuda", depth=2)
     # a dedicated stream: torch's default stream is the HIP null stream (handle 0), which the
     # C ABI reads as "no stream" and then renders synchronously on the context's stream
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
 
-    def step():
-        r.render(p, tile, out=out, stream=stream.cuda_stream)
-        return gather(out)
+    pending = []
 
-    for _ in range(args.warmup):
-        step()
+    def drain(keep):
+        frame = None
+        while len(pending) > keep:
+            frame = gather.finish(pending.pop(0))
+        return frame
+
+    def step(k, ev=None):
+        slot = k % 2
+        drain(1)  # the previous use of this slot's tile has been gathered
+        if ev is not None:
+            ev[0].record(stream)
+        r.render(p, tile, out=outs[slot], stream=stream.cuda_stream)
+        if ev is not None:
+            ev[1].record(stream)
+        pending.append(gather.submit(outs[slot], slot))
+
+    for k in range(args.warmup):
+        step(k)
+    drain(0)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -119,10 +136,8 @@ def main():
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     t0 = time.perf_counter()
     for k in range(args.steps):
-        evs[k][0].record(stream)
-        r.render(p, tile, out=out, stream=stream.cuda_stream)
-        evs[k][1].record(stream)
-        frame = gather(out)
+        step(k, evs[k])
+    frame = drain(0)  # every frame gathered and assembled inside the timed region
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -178,7 +193,8 @@ def main():
                             f"octree depth {DEPTH}, maxSpheresPerNode {MPN}",
                 "width": W, "height": H, "spheres": NSPH, "octree_depth": DEPTH, "max_spheres_per_node": MPN,
                 "num_samples": NS, "max_bounces": MAXD, "nodes": info["n_nodes"], "indices": info["n_indices"],
-                "layout": info["layout"], "partition": "16-row bands round-robin + RCCL gather" if world > 1
+                "layout": info["layout"], "partition": "16-row bands round-robin + RCCL gather (async, "
+                "overlapping the next frame's render)" if world > 1
                 else "full frame", "rays_per_step": rays_per_frame, "rays": "traced rays (octree traversals), "
                 "all bounces and ranks",
             },

@@ -54,13 +54,22 @@ def assemble(gathered, height: int, world: int, band: int = BAND, out=None):
 
 
 class FrameGather:
-    """Gather every rank's band tile to rank 0 and assemble the frame (torch.distributed)."""
+    """Gather every rank's band tile to rank 0 and assemble the frame (torch.distributed).
 
-    def __init__(self, dist, width: int, height: int, world: int, rank: int, device, band: int = BAND):
+    __call__ is synchronous.  submit()/finish() pipeline frames: submit issues the gather of a
+    tile asynchronously into receive slot `slot` (depth slots), finish waits for it (a stream
+    wait for RCCL, no host block) and assembles the frame on rank 0 -- so frame k's gather
+    and assembly overlap frame k+1's render.  A rank must not overwrite a submitted tile
+    before finish() of that submission (bench.py double-buffers its tiles)."""
+
+    def __init__(self, dist, width: int, height: int, world: int, rank: int, device, band: int = BAND,
+                 depth: int = 1):
         import torch
         self.dist, self.world, self.rank, self.height, self.band = dist, world, rank, height, band
         rows = rank_tile(width, height, rank, world, band).rows
-        self.gathered = torch.empty((world, rows, width, 3), dtype=torch.float32, device=device) if rank == 0 else None
+        self.slots = [torch.empty((world, rows, width, 3), dtype=torch.float32, device=device)
+                      for _ in range(depth)] if rank == 0 and world > 1 else None
+        self.gathered = self.slots[0] if self.slots else None
         self.frame = torch.empty((height, width, 3), dtype=torch.float32, device=device) if rank == 0 else None
 
     def __call__(self, local):
@@ -69,5 +78,23 @@ class FrameGather:
         self.dist.gather(local, list(self.gathered.unbind(0)) if self.rank == 0 else None, dst=0)
         if self.rank == 0:
             assemble(self.gathered, self.height, self.world, self.band, out=self.frame)
+            return self.frame
+        return None
+
+    def submit(self, local, slot: int = 0):
+        """Start gathering `local` (async); returns a handle for finish()."""
+        if self.world == 1:
+            return (None, slot, local)
+        dst = list(self.slots[slot].unbind(0)) if self.rank == 0 else None
+        return (self.dist.gather(local, dst, dst=0, async_op=True), slot, local)
+
+    def finish(self, handle):
+        """Complete a submit(): returns the assembled frame on rank 0 (None elsewhere)."""
+        work, slot, local = handle
+        if self.world == 1:
+            return local[:self.height]  # nothing to gather: the tile is the frame
+        work.wait()
+        if self.rank == 0:
+            assemble(self.slots[slot], self.height, self.world, self.band, out=self.frame)
             return self.frame
         return None

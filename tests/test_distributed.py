@@ -38,6 +38,51 @@ def worker(rank, world, port, W, H, q):
     dist.destroy_process_group()
 
 
+def worker_pipelined(rank, world, port, W, H, q):
+    """bench.py's pipeline: two frames in flight (double-buffered tiles, async gathers)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import octreeraytracer_amd as ort
+    from octreeraytracer_amd.distributed import FrameGather, rank_tile
+    from octreeraytracer_amd.renderer import emulate_render_host
+    s = ort.random_spheres(100, 42)
+    t = ort.build_octree(s, 4, 0)
+    tile = rank_tile(W, H, rank, world)
+    g = FrameGather(dist, W, H, world, rank, "cpu", depth=2)
+    handles = []
+    for slot, yaw in enumerate((-90.0, -80.0)):
+        p = ort.FrameParams.default_camera(W, H, yaw=yaw)
+        local, _ = emulate_render_host(s, t, p, tile)
+        handles.append(g.submit(torch.from_numpy(local), slot))
+    frames = []
+    for h in handles:  # finish() assembles into one frame buffer: copy each frame out
+        f = g.finish(h)
+        if rank == 0:
+            frames.append(f.numpy().copy())
+    if rank == 0:
+        q.put(frames)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_pipelined_gather_two_frames_in_flight(ort, oracle):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    W, H, world = 48, 40, 2
+    procs = [ctx.Process(target=worker_pipelined, args=(r, world, port, W, H, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    frames = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    s = ort.random_spheres(100, 42)
+    t = ort.build_octree(s, 4, 0)
+    for f, yaw in zip(frames, (-90.0, -80.0)):
+        assert np.array_equal(f, oracle.render(s, t, ort.FrameParams.default_camera(W, H, yaw=yaw)))
+
+
 @pytest.mark.parametrize("world,W,H", [(2, 64, 72), (3, 40, 100)])
 def test_gather_assembles_full_frame(ort, oracle, world, W, H):
     ctx = mp.get_context("spawn")
