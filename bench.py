@@ -211,7 +211,7 @@ def main():
                 "algorithmic_bytes_per_launch": int(alg_bytes),
                 "bytes_per_ray": round(alg_bytes / max(1, counts["pixels"]), 1),
                 "counts": counts,
-                "kernel": "ort_trace_compact<false,true,false> (camera rays + octree walk)",
+                "kernel": "ort_trace_compact<false,true> (camera rays + octree walk)",
                 "note": "achieved = reference-layout record bytes (SURVEY.md 8(d)) the reference walk reads per "
                         "frame / trace-kernel time; this kernel reads far fewer bytes (compact layout, L2/MALL "
                         "residency) and is instruction-issue bound -- see traffic and DESIGN.md",

@@ -234,13 +234,15 @@ __global__ void k_compact_nodes(const int32_t* co, const int32_t* oo, const int3
         const int32_t c = co[i];
         if (c != -1) {
             uint32_t mask = 0;
+            bool leafkids = true;
             for (int k = 0; k < 8; ++k) {
                 const int64_t j = (int64_t)c + k;
                 if (j >= n) continue;
+                if (co[j] != -1) leafkids = false;
                 if (co[j] == -1 && oo[j] == -1) continue;  // empty leaf, glsl:467
                 mask |= 1u << k;
             }
-            node[i] = make_uint2((uint32_t)c, 0x80000000u | mask);
+            node[i] = make_uint2((uint32_t)c, 0x80000000u | (leafkids ? 0x40000000u : 0u) | mask);
         } else {
             const int32_t v = cnt[i] > 0 ? cnt[i] : 0;
             node[i] = make_uint2(v > 0 ? (uint32_t)oo[i] : 0u, (uint32_t)v);

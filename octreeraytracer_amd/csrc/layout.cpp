@@ -127,14 +127,16 @@ bool buildCompactLayout(const SceneInput& in, int maxDepth, CompactLayout& out, 
         const int32_t co = in.co[i];
         if (co != -1) {
             uint32_t mask = 0;
+            bool leafkids = true;
             for (int k = 0; k < 8; ++k) {
                 const int64_t c = (int64_t)co + k;
                 if (c >= n) continue;
+                if (in.co[c] != -1) leafkids = false;
                 if (in.co[c] == -1 && in.oo[c] == -1) continue;  // empty leaf, glsl:467
                 mask |= 1u << k;
             }
             out.node[2 * (size_t)i] = (uint32_t)co;
-            out.node[2 * (size_t)i + 1] = ORT_INTERNAL_FLAG_HOST | mask;
+            out.node[2 * (size_t)i + 1] = ORT_INTERNAL_FLAG_HOST | (leafkids ? ORT_LEAFKIDS_FLAG_HOST : 0u) | mask;
         } else {
             const int32_t cntv = in.cnt[i] > 0 ? in.cnt[i] : 0;
             out.node[2 * (size_t)i] = cntv > 0 ? (uint32_t)in.oo[i] : 0u;

@@ -167,6 +167,14 @@ __global__ void __launch_bounds__(kBlock) ort_raygen_kernel(PipeArgs A) {
 // chunk, MI355X_MICROARCH.md 'dequeue') and hands the next slots of its chunk to lanes
 // that finished, so the wave stays full until the queue drains.  Rays the fast walk
 // cannot take are appended to the defer list for ort_trace_exact.
+// Waves per SIMD of the per-lane trace kernel: 7 (72 VGPRs) -- at 8 (64 VGPRs) the walk with
+// inline leaf children spills ~5 registers per iteration and runs 1.6x slower (tools/ab_libs.py).
+#ifndef ORT_TRACE_WAVES
+#define ORT_TRACE_WAVES 7
+#endif
+#ifndef ORT_TRACE_WAVES_DEEP  // 96-bit masks, no inline leaf children: 64 VGPRs, spill-free
+#define ORT_TRACE_WAVES_DEEP 8
+#endif
 constexpr int kChunk = 256;
 
 template <bool COUNT>
@@ -268,10 +276,9 @@ __device__ inline ort::Ray slot_ray(const PipeArgs& A, int k, bool& alive) {
 
 // One ray per lane over the compact layout (default): the tile-block order of the path
 // slots keeps each wave on an 8x8 pixel block, whose rays walk nearly the same nodes.
-// DEEP: trees deeper than 8 levels need the 96-bit level masks.
+// DEEP: trees deeper than 8 levels need the 96-bit level masks (ort_trace_compact_deep).
 template <bool COUNT, bool PRIMARY, bool DEEP>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) ort_trace_compact(PipeArgs A) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+__device__ __forceinline__ void trace_compact_body(PipeArgs& A, unsigned char* smem) {
     if (!PRIMARY && A.qlist && (int)(blockIdx.x * kBlock) >= *A.qcount) return;  // whole block past the list
     LdsView L = setup_lds<true>(smem, A.S);
     int k = blockIdx.x * kBlock + threadIdx.x;
@@ -294,6 +301,18 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))
                                                         L.fr, cnt);
     A.hit[k] = make_int2(hit ? entry : -1, __float_as_int(t));
     flush_counts<COUNT>(cnt, A.counters);
+}
+
+template <bool COUNT, bool PRIMARY>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ORT_TRACE_WAVES))) ort_trace_compact(PipeArgs A) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    trace_compact_body<COUNT, PRIMARY, false>(A, smem);
+}
+template <bool COUNT, bool PRIMARY>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ORT_TRACE_WAVES_DEEP)))
+ort_trace_compact_deep(PipeArgs A) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    trace_compact_body<COUNT, PRIMARY, true>(A, smem);
 }
 
 // Wave-wide OR of v (every lane of the wave must be executing): DPP prefix-OR inside each
@@ -951,8 +970,8 @@ hipError_t launch_trace_p(int mode, const PipeArgs& a, int blocks, int pblocks, 
         else hipLaunchKernelGGL((ort_trace_packet<COUNT, false>), dim3(blocks), dim3(kBlock), flds, s, a);
     }
     else if (mode == 0 && a.S.depth > 8)
-        hipLaunchKernelGGL((ort_trace_compact<COUNT, PRIMARY, true>), dim3(blocks), dim3(kBlock), lds, s, a);
-    else if (mode == 0) hipLaunchKernelGGL((ort_trace_compact<COUNT, PRIMARY, false>), dim3(blocks), dim3(kBlock), lds, s, a);
+        hipLaunchKernelGGL((ort_trace_compact_deep<COUNT, PRIMARY>), dim3(blocks), dim3(kBlock), lds, s, a);
+    else if (mode == 0) hipLaunchKernelGGL((ort_trace_compact<COUNT, PRIMARY>), dim3(blocks), dim3(kBlock), lds, s, a);
     else if (mode == 1) hipLaunchKernelGGL((ort_trace_kernel<1, COUNT, PRIMARY>), dim3(blocks), dim3(kBlock), 0, s, a);
     else hipLaunchKernelGGL((ort_trace_kernel<2, COUNT, PRIMARY>), dim3(blocks), dim3(kBlock), 0, s, a);
     return hipGetLastError();

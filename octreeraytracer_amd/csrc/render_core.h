@@ -43,6 +43,7 @@
 #define ORT_COMPACT_MAX_DEPTH 10
 #define ORT_MAX_STACK 200
 #define ORT_INTERNAL_FLAG 0x80000000u
+#define ORT_LEAFKIDS_FLAG 0x40000000u  // internal node whose existing children are all leaves
 #define ORT_MAXFLOAT 3.402823466e+38f
 
 namespace ort {
@@ -498,6 +499,9 @@ ORT_FN float plane_at(const float* base, int s4, int idx) {
 
 // Rank-reversed level masks (see above).  pop() returns hb = 8L + 7 - rank.
 struct Masks64 {  // levels 0..7: trees of depth <= 8
+    // test the leaf children of a LEAFKIDS node inline (fast_step); pays for its registers on
+    // depth <= 8 trees (all leaves at the bottom level with maxSpheresPerNode 0), not deeper
+    static constexpr bool kInlineLeaves = true;
     uint64_t m;
     ORT_FN void clear() { m = 0; }
     ORT_FN bool empty() const { return m == 0; }
@@ -522,6 +526,7 @@ struct Masks64 {  // levels 0..7: trees of depth <= 8
     }
 };
 struct Masks96 {  // levels 0..11
+    static constexpr bool kInlineLeaves = false;
     uint64_t lo;
     uint32_t hi;
     ORT_FN void clear() { lo = 0; hi = 0; }
@@ -632,6 +637,24 @@ ORT_FN bool fast_begin(const KScene& S, const float* planes, const Ray& r, V3 in
     return fmin3(st.tFA, st.tFB, st.tFC) >= fmax3(st.tNA, st.tNB, st.tNC);
 }
 
+// Sphere_hit over one leaf's objects (glsl:327-338) in the range (ntmin, closest); returns
+// true if one was accepted (the walk then ends after this leaf).
+template <bool COUNT, class Masks>
+ORT_FN bool leaf_tests(const KScene& S, FastStateT<Masks>& st, int off, int n, float ntmin, Counters& cnt) {
+    for (int i = 0; i < n; ++i) {
+        const float4 sp = fetch_sphere(S, off + i);
+        if (COUNT) cnt.v[2] += 1;
+        float t;
+        if (sphere_hit_fast(st.r, st.a, st.ya, sp, ntmin, st.closest, t)) {
+            st.hit = true;
+            st.closest = t;
+            st.hitEntry = off + i;
+            if (COUNT) cnt.v[3] += 1;
+        }
+    }
+    return st.hit;
+}
+
 // One node of the walk: visit st.node (push its surviving children, or test its spheres),
 // then pop the next node.  Returns true when the walk is over (hit found, or stack empty).
 template <bool COUNT, class Masks, class Frames>
@@ -651,46 +674,50 @@ ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks
         const float tMB = st.iB * (plane_at(st.pB, st.sB, st.cB + h) - st.oB);
         const float tMC = st.iC * (plane_at(st.pC, st.sC, st.cC + h) - st.oC);
         const float tNA = st.tNA, tNB = st.tNB, tNC = st.tNC, tFA = st.tFA, tFB = st.tFB, tFC = st.tFC;
-        // entry: near child (rank bit clear) enters at tN, far child at tM; exit: tM / tF
-        const float e00 = fmax2(tNA, tNB), e01 = fmax2(tNA, tMB), e10 = fmax2(tMA, tNB), e11 = fmax2(tMA, tMB);
-        const float x00 = fmin2(tMA, tMB), x01 = fmin2(tMA, tFB), x10 = fmin2(tFA, tMB), x11 = fmin2(tFA, tFB);
+        // child R enters at max3 of its axis entries (near half: tN, far half: tM) and exits at
+        // min3 of its exits (tM / tF); t_min and t_max are folded into the C axis.
         const float nN = fmax2(tNC, st.tmin0), nF = fmax2(tMC, st.tmin0);
         const float cN = fmin2(tMC, st.closest), cF = fmin2(tFC, st.closest);  // closest == t_max here
         // keep child R <=> exit >= entry, with entry >= t_min > 0 and exit <= t_max finite, so
         // exit - entry is never NaN and is +0 when equal: its sign bit is "drop".  The drop
         // bits are shifted in rank order (rank 0 ends at bit 7: the reversed layout) -- one
-        // v_sub + one v_alignbit per child, no compare/select.
+        // v_max3 + v_min3 + v_sub + v_alignbit per child, no compare/select.
         uint32_t drop = 0;
-#define ORT_CHILD(R, EAB, XAB, EC, XC) drop = (drop << 1) | (f2u(fmin2(XAB, XC) - fmax2(EAB, EC)) >> 31);
-        ORT_CHILD(0, e00, x00, nN, cN)
-        ORT_CHILD(1, e01, x01, nN, cN)
-        ORT_CHILD(2, e10, x10, nN, cN)
-        ORT_CHILD(3, e11, x11, nN, cN)
-        ORT_CHILD(4, e00, x00, nF, cF)
-        ORT_CHILD(5, e01, x01, nF, cF)
-        ORT_CHILD(6, e10, x10, nF, cF)
-        ORT_CHILD(7, e11, x11, nF, cF)
+#define ORT_CHILD(EA, EB, EC, XA, XB, XC) drop = (drop << 1) | (f2u(fmin3(XA, XB, XC) - fmax3(EA, EB, EC)) >> 31);
+        ORT_CHILD(tNA, tNB, nN, tMA, tMB, cN)  // rank 0: A near, B near, C near
+        ORT_CHILD(tNA, tMB, nN, tMA, tFB, cN)  // rank 1: B far
+        ORT_CHILD(tMA, tNB, nN, tFA, tMB, cN)  // rank 2: A far
+        ORT_CHILD(tMA, tMB, nN, tFA, tFB, cN)  // rank 3
+        ORT_CHILD(tNA, tNB, nF, tMA, tMB, cF)  // ranks 4-7: C far
+        ORT_CHILD(tNA, tMB, nF, tMA, tFB, cF)
+        ORT_CHILD(tMA, tNB, nF, tFA, tMB, cF)
+        ORT_CHILD(tMA, tMB, nF, tFA, tFB, cF)
 #undef ORT_CHILD
-        // level depth holds nothing yet (every deeper level is empty), so both writes are
-        // harmless when no child survives
-        st.masks.put(st.depth, rcm & ~drop);
-        fr.setCo(st.depth, co);
-    } else {
-        const int off = (int)rec.x;
-        const int n = (int)rec.y;
-        const float ntmin = st.depth == 0 ? st.tmin0 : fmax2(fmax3(st.tNA, st.tNB, st.tNC), st.tmin0);
-        for (int i = 0; i < n; ++i) {
-            const float4 sp = fetch_sphere(S, off + i);
-            if (COUNT) cnt.v[2] += 1;
-            float t;
-            if (sphere_hit_fast(st.r, st.a, st.ya, sp, ntmin, st.closest, t)) {
-                st.hit = true;
-                st.closest = t;
-                st.hitEntry = off + i;
-                if (COUNT) cnt.v[3] += 1;
+        const uint32_t keep = rcm & ~drop & 0xffu;
+        if (Masks::kInlineLeaves && (rec.y & ORT_LEAFKIDS_FLAG)) {
+            // Every existing child is a leaf, so the reference pops the surviving ones next,
+            // consecutively in rank order (a leaf pushes nothing): test them right here, with
+            // the tmin the reference pushed for each (max(max3(child entries), t_min)).
+            uint32_t todo = keep;
+            while (todo) {
+                const int hb = 31 - __builtin_clz(todo);
+                todo ^= 1u << hb;
+                const uint32_t R = 7u - (uint32_t)hb;
+                const uint2 lrec = fetch_node(S, co + (int)((st.otab >> (4 * R)) & 15u));
+                if (COUNT) cnt.v[0] += 1;
+                const float eA = (R & 2u) ? tMA : tNA, eB = (R & 1u) ? tMB : tNB, eC = (R & 4u) ? tMC : tNC;
+                if (leaf_tests<COUNT>(S, st, (int)lrec.x, (int)lrec.y, fmax2(fmax3(eA, eB, eC), st.tmin0), cnt))
+                    return true;  // glsl:336
             }
+        } else {
+            // level depth holds nothing yet (every deeper level is empty), so both writes are
+            // harmless when no child survives
+            st.masks.put(st.depth, keep);
+            fr.setCo(st.depth, co);
         }
-        if (st.hit) return true;  // glsl:336: the walk ends after the leaf that produced a hit
+    } else {
+        const float ntmin = st.depth == 0 ? st.tmin0 : fmax2(fmax3(st.tNA, st.tNB, st.tNC), st.tmin0);
+        if (leaf_tests<COUNT>(S, st, (int)rec.x, (int)rec.y, ntmin, cnt)) return true;  // glsl:336
     }
     if (st.masks.empty()) return true;
     // next node: lowest remaining rank of the deepest level with one left
