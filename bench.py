@@ -211,7 +211,7 @@ def main():
                 "algorithmic_bytes_per_launch": int(alg_bytes),
                 "bytes_per_ray": round(alg_bytes / max(1, counts["pixels"]), 1),
                 "counts": counts,
-                "kernel": "ort_trace_compact<false,true> (camera rays + octree walk)",
+                "kernel": "ort_trace_compact<false,true,true> (camera rays + octree walk + shading)",
                 "note": "achieved = reference-layout record bytes (SURVEY.md 8(d)) the reference walk reads per "
                         "frame / trace-kernel time; this kernel reads far fewer bytes (compact layout, L2/MALL "
                         "residency) and is instruction-issue bound -- see traffic and DESIGN.md",
@@ -251,9 +251,18 @@ def cpu_baseline(spheres, tree, p, budget_s):
     n = int(max(n, min(p.height, n * budget_s / max(dt, 1e-3))))
     dt, stride = run(n)
     rays = n * p.width * p.num_samples
+    # one core (report all cores and 1 core), a smaller row sample
+    n1 = max(2, min(p.height, int(n * 0.25 * budget_s / max(dt * threads, 1e-3))))
+    stride1 = max(1, p.height // n1)
+    t0 = time.perf_counter()
+    oracle.render(spheres, tree, p, 0, stride1 // 2, p.width, n1, band_height=1, band_stride=stride1, threads=1)
+    dt1 = time.perf_counter() - t0
+    rays1 = n1 * p.width * p.num_samples
     return {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
             "sample": f"{n} of {p.height} rows (every {stride}th), {rays} camera rays, {dt:.1f} s wall; "
-                      f"oracle/ort_oracle.c -O3, OpenMP dynamic over rows"}
+                      f"oracle/ort_oracle.c -O3, OpenMP dynamic over rows",
+            "value_1core": round(rays1 / dt1 / 1e6, 3),
+            "sample_1core": f"{n1} rows (every {stride1}th), {rays1} camera rays, {dt1:.1f} s wall, 1 thread"}
 
 
 if __name__ == "__main__":

@@ -219,7 +219,7 @@ __global__ void __launch_bounds__(kBlock) ort_trace_persistent(PipeArgs A) {
                             A.defer_list[atomicAdd(A.sync, 1)] = cand;
                         } else {
                             if (COUNT) cnt.v[5] += 1;
-                            if (ort::fast_begin(A.S, L.planes, ray, inv, 0.001f, ORT_MAXFLOAT, st)) k = cand;
+                            if (ort::fast_begin(A.S, L.planes, lut, ray, inv, 0.001f, ORT_MAXFLOAT, st)) k = cand;
                             else A.hit[cand] = make_int2(-1, 0);
                         }
                     }
@@ -229,7 +229,7 @@ __global__ void __launch_bounds__(kBlock) ort_trace_persistent(PipeArgs A) {
             continue;
         }
         if (k >= 0) {
-            if (ort::fast_step<COUNT>(A.S, lut, st, L.fr, cnt)) {
+            if (ort::fast_step<COUNT>(A.S, st, L.fr, cnt)) {
                 A.hit[k] = make_int2(st.hit ? st.hitEntry : -1, __float_as_int(st.closest));
                 k = -1;
             }
@@ -250,7 +250,7 @@ __device__ inline bool list_slot(const PipeArgs& A, int& k) {
 // (main() up to radiance()'s first line; the shade kernel regenerates it identically),
 // later bounces read the ray the previous shade kernel stored.
 template <bool PRIMARY>
-__device__ inline ort::Ray slot_ray(const PipeArgs& A, int k, bool& alive) {
+__device__ inline ort::Ray slot_ray(const PipeArgs& A, int k, bool& alive, ort_rng* st_out = nullptr) {
     if constexpr (PRIMARY) {
         int col, row;
         alive = slot_coords(A, k, col, row);
@@ -268,16 +268,44 @@ __device__ inline ort::Ray slot_ray(const PipeArgs& A, int k, bool& alive) {
             st.x = v.x;
             st.y = v.y;
         }
-        return ort::primary_ray(A.pp, A.tm.x0 + col, y, A.sample, st);
+        const ort::Ray r = ort::primary_ray(A.pp, A.tm.x0 + col, y, A.sample, st);
+        if (st_out) *st_out = st;
+        return r;
     } else {
         return load_ray(A, k, alive);
     }
 }
 
+// 1 sample, 1 bounce (the primary-ray benchmark mode): the trace kernels shade their own
+// rays -- exactly ort_shade_kernel<0, true, true> -- instead of writing hit records for it.
+__device__ inline void shade_direct(const PipeArgs& A, int k, ort::Ray ray, ort_rng st, bool hit, int entry, float t) {
+    int col, row;
+    (void)slot_coords(A, k, col, row);
+    ort::V3 c = ort::mk(1.0f, 1.0f, 1.0f);
+    float importance = 1.0f;
+    ort::HitRec rec;
+    if (hit) rec = ort::hit_record<0>(A.S, ray, t, entry);
+    (void)ort::shade_bounce(hit, rec, ray, c, importance, st);
+    const ort::V3 v = ort::finish_pixel(ort::add(ort::mk(0.0f, 0.0f, 0.0f), c), 1);
+    float* o = A.out + 3 * ((size_t)row * A.tm.tw + col);
+    o[0] = v.x;
+    o[1] = v.y;
+    o[2] = v.z;
+}
+// Tile rows past the frame (band padding) are written as zeros, as the shade kernel does.
+__device__ inline void shade_direct_padding(const PipeArgs& A, int k) {
+    int col, row;
+    if (!slot_coords(A, k, col, row) || tile_row_to_y(A.tm, row) < A.pp.H) return;
+    float* o = A.out + 3 * ((size_t)row * A.tm.tw + col);
+    o[0] = 0.0f;
+    o[1] = 0.0f;
+    o[2] = 0.0f;
+}
+
 // One ray per lane over the compact layout (default): the tile-block order of the path
 // slots keeps each wave on an 8x8 pixel block, whose rays walk nearly the same nodes.
 // DEEP: trees deeper than 8 levels need the 96-bit level masks (ort_trace_compact_deep).
-template <bool COUNT, bool PRIMARY, bool DEEP>
+template <bool COUNT, bool PRIMARY, bool DEEP, bool FUSE>
 __device__ __forceinline__ void trace_compact_body(PipeArgs& A, unsigned char* smem) {
     if (!PRIMARY && A.qlist && (int)(blockIdx.x * kBlock) >= *A.qcount) return;  // whole block past the list
     LdsView L = setup_lds<true>(smem, A.S);
@@ -285,12 +313,15 @@ __device__ __forceinline__ void trace_compact_body(PipeArgs& A, unsigned char* s
     if (!PRIMARY && !list_slot(A, k)) return;
     bool alive;
     const ort::Ray ray = slot_ray<PRIMARY>(A, k, alive);
-    if (!alive) return;
+    if (!alive) {
+        if (FUSE) shade_direct_padding(A, k);
+        return;
+    }
     ort::Counters cnt;
     for (int q = 0; q < 6; ++q) cnt.v[q] = 0;
     const ort::V3 inv = ort::mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
     if (A.exact_only || !ort::fast_path_ok(ray, inv, 0.001f, ORT_MAXFLOAT)) {
-        A.defer_list[atomicAdd(A.sync, 1)] = k;
+        A.defer_list[atomicAdd(A.sync, 1)] = k;  // ort_trace_exact walks (and, FUSE, shades) it
         return;
     }
     if (COUNT) cnt.v[5] += 1;
@@ -299,20 +330,43 @@ __device__ __forceinline__ void trace_compact_body(PipeArgs& A, unsigned char* s
     using Masks = typename std::conditional<DEEP, ort::Masks96, ort::Masks64>::type;
     const bool hit = ort::traverse_fast_t<COUNT, Masks>(A.S, L.planes, L.lut, ray, inv, 0.001f, ORT_MAXFLOAT, entry, t,
                                                         L.fr, cnt);
-    A.hit[k] = make_int2(hit ? entry : -1, __float_as_int(t));
+    if (FUSE) {
+        // regenerate the camera ray and its RNG state (a few hundred ALU ops once per ray)
+        // rather than keep 8 registers live across the walk; the empty asm hides that it is
+        // the same slot, so the compiler cannot just reuse the values from before the loop
+        // (the kernel arguments are re-read through a laundered pointer too: held across the
+        // walk they overflow the SGPRs)
+        int k2 = k;
+        asm volatile("" : "+v"(k2));
+#if defined(__HIP_DEVICE_COMPILE__)
+        typedef __attribute__((address_space(4))) const PipeArgs KernArgs;  // the kernarg segment
+        KernArgs* kp = (KernArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(kp));
+        const PipeArgs A2 = *kp;
+#else
+        const PipeArgs& A2 = A;
+#endif
+        bool alive2;
+        ort_rng rng;
+        const ort::Ray ray2 = slot_ray<PRIMARY>(A2, k2, alive2, &rng);
+        shade_direct(A2, k2, ray2, rng, hit, entry, t);
+    } else {
+        A.hit[k] = make_int2(hit ? entry : -1, __float_as_int(t));
+    }
     flush_counts<COUNT>(cnt, A.counters);
 }
 
-template <bool COUNT, bool PRIMARY>
+// FUSE: 1 sample, 1 bounce -- the kernel also shades (shade_direct), no hit records.
+template <bool COUNT, bool PRIMARY, bool FUSE>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ORT_TRACE_WAVES))) ort_trace_compact(PipeArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    trace_compact_body<COUNT, PRIMARY, false>(A, smem);
+    trace_compact_body<COUNT, PRIMARY, false, FUSE>(A, smem);
 }
-template <bool COUNT, bool PRIMARY>
+template <bool COUNT, bool PRIMARY, bool FUSE>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ORT_TRACE_WAVES_DEEP)))
 ort_trace_compact_deep(PipeArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    trace_compact_body<COUNT, PRIMARY, true>(A, smem);
+    trace_compact_body<COUNT, PRIMARY, true, FUSE>(A, smem);
 }
 
 // Wave-wide OR of v (every lane of the wave must be executing): DPP prefix-OR inside each
@@ -546,7 +600,7 @@ __global__ void __launch_bounds__(kBlock) ort_trace_kernel(PipeArgs A) {
 }
 
 // Exact compact walk (traverse_compact) for the deferred rays; grid-stride loop.
-template <bool COUNT, bool PRIMARY>
+template <bool COUNT, bool PRIMARY, bool FUSE>
 __global__ void __launch_bounds__(kBlock) ort_trace_exact(PipeArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     LdsView L = setup_lds<false>(smem, A.S);
@@ -556,11 +610,13 @@ __global__ void __launch_bounds__(kBlock) ort_trace_exact(PipeArgs A) {
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
         const int k = A.defer_list[i];
         bool alive;
-        const ort::Ray ray = slot_ray<PRIMARY>(A, k, alive);
+        ort_rng rng;
+        const ort::Ray ray = slot_ray<PRIMARY>(A, k, alive, FUSE ? &rng : nullptr);
         float t;
         int entry;
         const int st = ort::trace_ray<0, COUNT>(A.S, L.planes, nullptr, ray, false, t, entry, L.fr, nullptr, nullptr, cnt);
-        A.hit[k] = make_int2(st == ORT_TRACE_HIT ? entry : -1, __float_as_int(t));
+        if (FUSE) shade_direct(A, k, ray, rng, st == ORT_TRACE_HIT, entry, t);
+        else A.hit[k] = make_int2(st == ORT_TRACE_HIT ? entry : -1, __float_as_int(t));
     }
     flush_counts<COUNT>(cnt, A.counters);
 }
@@ -962,7 +1018,8 @@ int ensure(ort_ctx* ctx, DevBuf& b, size_t bytes) {
 }
 
 template <bool COUNT, bool PRIMARY>
-hipError_t launch_trace_p(int mode, const PipeArgs& a, int blocks, int pblocks, size_t lds, hipStream_t s, bool packet) {
+hipError_t launch_trace_p(int mode, const PipeArgs& a, int blocks, int pblocks, size_t lds, hipStream_t s, bool packet,
+                          bool fuse) {
     if (mode == 0 && pblocks > 0) hipLaunchKernelGGL((ort_trace_persistent<COUNT>), dim3(pblocks), dim3(kBlock), lds, s, a);
     else if (mode == 0 && PRIMARY && packet) {
         const size_t flds = (size_t)std::max(a.S.depth, 1) * kBlock * sizeof(int);  // per-lane fallback frames
@@ -970,8 +1027,13 @@ hipError_t launch_trace_p(int mode, const PipeArgs& a, int blocks, int pblocks, 
         else hipLaunchKernelGGL((ort_trace_packet<COUNT, false>), dim3(blocks), dim3(kBlock), flds, s, a);
     }
     else if (mode == 0 && a.S.depth > 8)
-        hipLaunchKernelGGL((ort_trace_compact_deep<COUNT, PRIMARY>), dim3(blocks), dim3(kBlock), lds, s, a);
-    else if (mode == 0) hipLaunchKernelGGL((ort_trace_compact<COUNT, PRIMARY>), dim3(blocks), dim3(kBlock), lds, s, a);
+    {
+        if (fuse) hipLaunchKernelGGL((ort_trace_compact_deep<COUNT, PRIMARY, true>), dim3(blocks), dim3(kBlock), lds, s, a);
+        else hipLaunchKernelGGL((ort_trace_compact_deep<COUNT, PRIMARY, false>), dim3(blocks), dim3(kBlock), lds, s, a);
+    }
+    else if (mode == 0 && fuse)
+        hipLaunchKernelGGL((ort_trace_compact<COUNT, PRIMARY, true>), dim3(blocks), dim3(kBlock), lds, s, a);
+    else if (mode == 0) hipLaunchKernelGGL((ort_trace_compact<COUNT, PRIMARY, false>), dim3(blocks), dim3(kBlock), lds, s, a);
     else if (mode == 1) hipLaunchKernelGGL((ort_trace_kernel<1, COUNT, PRIMARY>), dim3(blocks), dim3(kBlock), 0, s, a);
     else hipLaunchKernelGGL((ort_trace_kernel<2, COUNT, PRIMARY>), dim3(blocks), dim3(kBlock), 0, s, a);
     return hipGetLastError();
@@ -979,9 +1041,9 @@ hipError_t launch_trace_p(int mode, const PipeArgs& a, int blocks, int pblocks, 
 
 template <bool COUNT>
 hipError_t launch_trace(int mode, bool primary, const PipeArgs& a, int blocks, int pblocks, size_t lds, hipStream_t s,
-                        bool packet) {
-    return primary ? launch_trace_p<COUNT, true>(mode, a, blocks, pblocks, lds, s, packet)
-                   : launch_trace_p<COUNT, false>(mode, a, blocks, pblocks, lds, s, packet);
+                        bool packet, bool fuse) {
+    return primary ? launch_trace_p<COUNT, true>(mode, a, blocks, pblocks, lds, s, packet, fuse)
+                   : launch_trace_p<COUNT, false>(mode, a, blocks, pblocks, lds, s, packet, false);
 }
 
 template <int MODE>
@@ -1045,6 +1107,8 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
             return rc;
     }
     const bool compact = !direct && !ctx->persistent && p->max_depth > 1;
+    // primary-ray mode (1 sample, 1 bounce) on the compact layout: the trace kernels shade
+    const bool fuse = direct && mode == 0 && !ctx->persistent && !ctx->packet;
     const bool sorted = compact && ctx->sort_paths;
     size_t qtemp_bytes = 0;
     if (compact) {
@@ -1101,8 +1165,8 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                 const int slot = (int)(ctx->frames % ort_ctx::kRing);
                 if (first_trace) HIPCHK(ctx, hipEventRecord(ctx->tr0[slot], s));
                 const bool prim = (b == 0) && pblocks == 0;
-                e = dcounters ? launch_trace<true>(mode, prim, a, (int)blocks, pblocks, lds, s, ctx->packet != 0)
-                              : launch_trace<false>(mode, prim, a, (int)blocks, pblocks, lds, s, ctx->packet != 0);
+                e = dcounters ? launch_trace<true>(mode, prim, a, (int)blocks, pblocks, lds, s, ctx->packet != 0, fuse)
+                              : launch_trace<false>(mode, prim, a, (int)blocks, pblocks, lds, s, ctx->packet != 0, fuse);
                 if (e != hipSuccess) return hip_fail(ctx, e, "trace kernel launch");
                 if (first_trace) {
                     HIPCHK(ctx, hipEventRecord(ctx->tr1[slot], s));
@@ -1111,15 +1175,20 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                 }
                 if (mode == 0) {
                     const bool prim = (b == 0) && pblocks == 0;
-                    if (dcounters && prim) hipLaunchKernelGGL((ort_trace_exact<true, true>), dim3(exact_blocks), dim3(kBlock), lds_exact, s, a);
-                    else if (dcounters) hipLaunchKernelGGL((ort_trace_exact<true, false>), dim3(exact_blocks), dim3(kBlock), lds_exact, s, a);
-                    else if (prim) hipLaunchKernelGGL((ort_trace_exact<false, true>), dim3(exact_blocks), dim3(kBlock), lds_exact, s, a);
-                    else hipLaunchKernelGGL((ort_trace_exact<false, false>), dim3(exact_blocks), dim3(kBlock), lds_exact, s, a);
+                    const dim3 g(exact_blocks), t(kBlock);
+                    if (dcounters && fuse) hipLaunchKernelGGL((ort_trace_exact<true, true, true>), g, t, lds_exact, s, a);
+                    else if (dcounters && prim) hipLaunchKernelGGL((ort_trace_exact<true, true, false>), g, t, lds_exact, s, a);
+                    else if (dcounters) hipLaunchKernelGGL((ort_trace_exact<true, false, false>), g, t, lds_exact, s, a);
+                    else if (fuse) hipLaunchKernelGGL((ort_trace_exact<false, true, true>), g, t, lds_exact, s, a);
+                    else if (prim) hipLaunchKernelGGL((ort_trace_exact<false, true, false>), g, t, lds_exact, s, a);
+                    else hipLaunchKernelGGL((ort_trace_exact<false, false, false>), g, t, lds_exact, s, a);
                     if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "ort_trace_exact launch");
                 }
             }
-            e = launch_shade(mode, b == 0, direct, a, (int)blocks, s);
-            if (e != hipSuccess) return hip_fail(ctx, e, "ort_shade_kernel launch");
+            if (!fuse) {
+                e = launch_shade(mode, b == 0, direct, a, (int)blocks, s);
+                if (e != hipSuccess) return hip_fail(ctx, e, "ort_shade_kernel launch");
+            }
             if (compact && !a.nobounce && b + 1 < bounces) {  // the next bounce walks only the alive paths
                 if (sorted) {
                     const ort::SortBuffers sb{(uint32_t*)ctx->skeys.p, (uint32_t*)ctx->skeys2.p, (int*)ctx->svals.p,
@@ -1546,10 +1615,10 @@ int ort_debug_wave_stats(const float* cr, const float* ma, const float* fr, int3
                 if (m0 < 0) m0 = m;
                 else if (m != m0) uniform = false;
                 ort::FastStateT<ort::Masks96> fs;
-                if (!ort::fast_begin(S, S.planes, ray, inv, 0.001f, ORT_MAXFLOAT, fs)) continue;
+                if (!ort::fast_begin(S, S.planes, lut.data(), ray, inv, 0.001f, ORT_MAXFLOAT, fs)) continue;
                 for (;;) {
                     seq[l].push_back(fs.node);
-                    if (ort::fast_step<false>(S, lut.data(), fs, lf, cc)) break;
+                    if (ort::fast_step<false>(S, fs, lf, cc)) break;
                 }
                 maxlen = std::max(maxlen, seq[l].size());
             }

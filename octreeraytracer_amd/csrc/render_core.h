@@ -580,7 +580,7 @@ struct FastStateT {
     float tNA, tFA, tNB, tFB, tNC, tFC;  // near/far plane t of the current node's box
     int cA, cB, cC;  // ray-order index of the current node's near plane
     uint32_t otab;   // nibble r = octant of rank r
-    uint32_t m;      // order xor (rank LUT row)
+    const uint8_t* lut_row;  // rank LUT row of this ray's order xor m
     int node, depth;
     float tmin0, closest;
     int hitEntry;
@@ -591,8 +591,8 @@ using FastState = FastStateT<Masks96>;
 
 // Root test and state setup (glsl:296-311).  Returns false when the root box is missed.
 template <class Masks>
-ORT_FN bool fast_begin(const KScene& S, const float* planes, const Ray& r, V3 inv, float t_min, float t_max,
-                       FastStateT<Masks>& st) {
+ORT_FN bool fast_begin(const KScene& S, const float* planes, const uint8_t* rank_lut, const Ray& r, V3 inv, float t_min,
+                       float t_max, FastStateT<Masks>& st) {
     const int D = S.depth;
     const int top = 1 << D;
     const int P1 = top + 1;
@@ -619,7 +619,7 @@ ORT_FN bool fast_begin(const KScene& S, const float* planes, const Ray& r, V3 in
     uint32_t ot = 0;
     for (uint32_t k = 0; k < 8; ++k) ot |= rank_perm(k, m) << (4 * k);
     st.otab = ot;
-    st.m = m;
+    st.lut_row = rank_lut + m * 256u;
     st.tNA = st.iA * (st.pA[0] - st.oA);
     st.tFA = st.iA * (plane_at(st.pA, st.sA, top) - st.oA);
     st.tNB = st.iB * (st.pB[0] - st.oB);
@@ -658,7 +658,7 @@ ORT_FN bool leaf_tests(const KScene& S, FastStateT<Masks>& st, int off, int n, f
 // One node of the walk: visit st.node (push its surviving children, or test its spheres),
 // then pop the next node.  Returns true when the walk is over (hit found, or stack empty).
 template <bool COUNT, class Masks, class Frames>
-ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks>& st, Frames& fr, Counters& cnt) {
+ORT_FN bool fast_step(const KScene& S, FastStateT<Masks>& st, Frames& fr, Counters& cnt) {
     const int D = S.depth;
     const uint2 rec = fetch_node(S, st.node);
     if (COUNT) cnt.v[0] += 1;
@@ -668,7 +668,7 @@ ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks
             const long long rem = (long long)S.n_nodes - (long long)co;
             cnt.v[1] += (unsigned long long)(rem >= 8 ? 8 : (rem > 0 ? rem : 0));
         }
-        const uint32_t rcm = rank_lut[st.m * 256u + (rec.y & 0xffu)];
+        const uint32_t rcm = st.lut_row[rec.y & 0xffu];
         const int h = st.h;
         const float tMA = st.iA * (plane_at(st.pA, st.sA, st.cA + h) - st.oA);
         const float tMB = st.iB * (plane_at(st.pB, st.sB, st.cB + h) - st.oB);
@@ -745,8 +745,8 @@ template <bool COUNT, class Masks, class Frames>
 ORT_FN bool traverse_fast_t(const KScene& S, const float* planes, const uint8_t* rank_lut, const Ray& r, V3 inv,
                             float t_min, float t_max, int& hitEntry, float& hitT, Frames& fr, Counters& cnt) {
     FastStateT<Masks> st;
-    if (!fast_begin(S, planes, r, inv, t_min, t_max, st)) return false;
-    while (!fast_step<COUNT>(S, rank_lut, st, fr, cnt)) {
+    if (!fast_begin(S, planes, rank_lut, r, inv, t_min, t_max, st)) return false;
+    while (!fast_step<COUNT>(S, st, fr, cnt)) {
     }
     hitEntry = st.hitEntry;
     hitT = st.closest;

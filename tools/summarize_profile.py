@@ -7,7 +7,7 @@ from collections import defaultdict
 from pathlib import Path
 
 src, dst = Path(sys.argv[1]), Path(sys.argv[2])
-KERNEL = sys.argv[3] if len(sys.argv) > 3 else "ort_trace_compact<false, true>"
+KERNEL = sys.argv[3] if len(sys.argv) > 3 else "ort_trace_compact<false, true, true>"
 
 stats = {}
 ks = next(src.glob("trace/*kernel_stats.csv"), None)
