@@ -21,10 +21,9 @@ ap.add_argument("--both", action="store_true", help="also render the frames with
 a = ap.parse_args()
 W, H, N, D, M, NS, MD = bench.CONFIGS[a.config]
 s = ort.random_spheres(N, 42)
-t = ort.build_octree(s, D, M)
 r = ort.Renderer(0)
 r.set_layout(a.layout)
-r.upload(s, t)
+r.build_scene(s, D, M)  # GPU octree builder (same tree as the host builder)
 p = ort.FrameParams.default_camera(W, H, num_samples=NS, max_depth=MD)
 out = np.empty((H, W, 3), np.float32)
 ms = []
