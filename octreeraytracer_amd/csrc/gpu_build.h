@@ -64,7 +64,8 @@ hipError_t selectAlive(void* temp, size_t temp_bytes, const float4* pd, int n, i
 
 namespace ort {
 // Coherence sort of the alive paths (ORT_OPT_SORT_PATHS): key = direction octant (3 bits) |
-// Morton code of the origin in the root box (9 bits per axis); dead slots get the largest
+// Morton code of the origin in the root box (7 bits per axis) | 2 bits per axis of the
+// normalised direction magnitude; dead slots get the largest
 // key, so the sorted values are the alive slots first, *count of them (device).
 struct SortBuffers {
     uint32_t* keys_in;

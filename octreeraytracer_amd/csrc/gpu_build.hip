@@ -658,6 +658,9 @@ hipError_t selectAlive(void* temp, size_t temp_bytes, const float4* pd, int n, i
     return rocprim::select(temp, temp_bytes, rocprim::counting_iterator<int>(0), flags, out, count, (size_t)n, s);
 }
 
+#ifndef ORT_SORT_KEY
+#define ORT_SORT_KEY 2  // 1: octant | origin Morton (9 bits/axis); 2: + direction bits (C5: 2% faster)
+#endif
 namespace {
 __device__ __forceinline__ uint32_t spread3(uint32_t v) {  // 9 bits -> every third bit
     v &= 0x1ffu;
@@ -684,8 +687,17 @@ __global__ void k_path_keys(const float4* po, const float4* pd, int n, float3 lo
         if (alive) {
             const float4 o = po[k];
             const uint32_t m = ((uint32_t)(d.z < 0.0f) << 2) | ((uint32_t)(d.x < 0.0f) << 1) | (uint32_t)(d.y < 0.0f);
+#if ORT_SORT_KEY == 2
+            // octant | origin Morton (7 bits per axis) | direction (2 bits per axis of |d|/max|d|)
+            const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
+            const float inv = 3.999f / fmaxf(fmaxf(ax, ay), fmaxf(az, 1e-30f));
+            const uint32_t dq = ((uint32_t)(ax * inv) << 4) | ((uint32_t)(ay * inv) << 2) | (uint32_t)(az * inv);
+            key = (m << 27) | ((spread3(quant9(o.x, lo.x, sc.x) >> 2) << 2 | spread3(quant9(o.y, lo.y, sc.y) >> 2) << 1 |
+                               spread3(quant9(o.z, lo.z, sc.z) >> 2)) << 6) | dq;
+#else
             key = (m << 27) | (spread3(quant9(o.x, lo.x, sc.x)) << 2) | (spread3(quant9(o.y, lo.y, sc.y)) << 1) |
                   spread3(quant9(o.z, lo.z, sc.z));
+#endif
         }
         keys[k] = key;
         vals[k] = k;
