@@ -398,10 +398,13 @@ __device__ inline uint32_t wave_or(uint32_t v) {
 // tools/wave_stats.py prices it: at C3 the union visits 1.41x the internal nodes of one ray,
 // while the per-lane loop ran a ~46-VALU pop for every lane every iteration.
 template <bool COUNT, bool DEEP>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) ort_trace_packet(PipeArgs A) {
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ORT_TRACE_WAVES))) ort_trace_packet(PipeArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     using Masks = typename std::conditional<DEEP, ort::Masks96, ort::Masks64>::type;
     const ort::KScene& S = A.S;
+    // planes and rank LUT in LDS: wave-uniform reads are LDS broadcasts addressed by one VALU
+    // op, instead of scalar loads whose 64-bit address arithmetic saturated the scalar unit
+    LdsView LV = setup_lds<true>(smem, A.S);
     const int k = blockIdx.x * kBlock + threadIdx.x;
     bool alive;
     const ort::Ray ray = slot_ray<true>(A, k, alive);
@@ -426,13 +429,13 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))
             const bool swap = (m >> 1) & 1u;
             const uint32_t gA = swap ? (m & 1u) : ((m >> 1) & 1u), gB = swap ? ((m >> 1) & 1u) : (m & 1u),
                            gC = (m >> 2) & 1u;
-            const float* pA = S.planes + (swap ? P1 : 0) + (gA ? top : 0);
-            const float* pB = S.planes + (swap ? 0 : P1) + (gB ? top : 0);
-            const float* pC = S.planes + 2 * P1 + (gC ? top : 0);
+            const float* pA = LV.planes + (swap ? P1 : 0) + (gA ? top : 0);
+            const float* pB = LV.planes + (swap ? 0 : P1) + (gB ? top : 0);
+            const float* pC = LV.planes + 2 * P1 + (gC ? top : 0);
             const int sA = gA ? -1 : 1, sB = gB ? -1 : 1, sC = gC ? -1 : 1;
             uint32_t otab = 0;
             for (uint32_t r = 0; r < 8; ++r) otab |= ort::rank_perm(r, m) << (4 * r);
-            const uint8_t* lutRow = A.lut + m * 256u;
+            const uint8_t* lutRow = LV.lut + m * 256u;
             const float oA = swap ? ray.o.y : ray.o.x, oB = swap ? ray.o.x : ray.o.y, oC = ray.o.z;
             const float iA = swap ? inv.y : inv.x, iB = swap ? inv.x : inv.y, iC = inv.z;
             const float a = ort::dot(ray.d, ray.d);
@@ -557,13 +560,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))
             tHit = hit ? closest : 0.0f;
         } else if (fast) {
             // ---- mixed orders: per-lane walk ----
-            ort::LdsFrames fr;
-            fr.co = reinterpret_cast<int*>(smem);
-            fr.tm = nullptr;
-            fr.stride = kBlock;
-            fr.lane = threadIdx.x;
-            hit = ort::traverse_fast_t<COUNT, Masks>(S, S.planes, A.lut, ray, inv, 0.001f, ORT_MAXFLOAT, entry, tHit,
-                                                     fr, cnt);
+            hit = ort::traverse_fast_t<COUNT, Masks>(S, LV.planes, LV.lut, ray, inv, 0.001f, ORT_MAXFLOAT, entry, tHit,
+                                                     LV.fr, cnt);
         }
     }
     if (alive && !fast) {
@@ -1022,9 +1020,8 @@ hipError_t launch_trace_p(int mode, const PipeArgs& a, int blocks, int pblocks, 
                           bool fuse) {
     if (mode == 0 && pblocks > 0) hipLaunchKernelGGL((ort_trace_persistent<COUNT>), dim3(pblocks), dim3(kBlock), lds, s, a);
     else if (mode == 0 && PRIMARY && packet) {
-        const size_t flds = (size_t)std::max(a.S.depth, 1) * kBlock * sizeof(int);  // per-lane fallback frames
-        if (a.S.depth > 8) hipLaunchKernelGGL((ort_trace_packet<COUNT, true>), dim3(blocks), dim3(kBlock), flds, s, a);
-        else hipLaunchKernelGGL((ort_trace_packet<COUNT, false>), dim3(blocks), dim3(kBlock), flds, s, a);
+        if (a.S.depth > 8) hipLaunchKernelGGL((ort_trace_packet<COUNT, true>), dim3(blocks), dim3(kBlock), lds, s, a);
+        else hipLaunchKernelGGL((ort_trace_packet<COUNT, false>), dim3(blocks), dim3(kBlock), lds, s, a);
     }
     else if (mode == 0 && a.S.depth > 8)
     {

@@ -17,7 +17,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="c3")
 ap.add_argument("--frames", type=int, default=3)
 ap.add_argument("--layout", type=int, default=-1)
-ap.add_argument("--both", action="store_true", help="also render the frames with the packet walk off")
+ap.add_argument("--both", action="store_true", help="render with the packet walk on, then off")
 a = ap.parse_args()
 W, H, N, D, M, NS, MD = bench.CONFIGS[a.config]
 s = ort.random_spheres(N, 42)
@@ -26,6 +26,8 @@ r.set_layout(a.layout)
 r.build_scene(s, D, M)  # GPU octree builder (same tree as the host builder)
 p = ort.FrameParams.default_camera(W, H, num_samples=NS, max_depth=MD)
 out = np.empty((H, W, 3), np.float32)
+if a.both:
+    r.set_packet(True)  # first the wave-level walk, then (below) the per-lane walk
 ms = []
 for _ in range(a.frames):
     r.render(p, out=out)
