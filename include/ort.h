@@ -84,7 +84,9 @@ typedef struct ort_scene_info {
 #define ORT_OPT_FORCE_LAYOUT 1     /* -1 auto (default), or ORT_LAYOUT_* */
 #define ORT_OPT_EXACT_TRAVERSAL 2  /* 1: disable the sign-specialised fast walk (A/B testing; same pixels) */
 #define ORT_OPT_REFILL 3           /* persistent trace: refill a wave when >= value of its 64 lanes idle (16) */
-#define ORT_OPT_PERSISTENT 4       /* 1: persistent trace kernel with per-lane ray refill (default 0) */
+#define ORT_OPT_PERSISTENT 4       /* persistent trace kernel with per-lane ray refill: 0 off, 1 every
+                                      trace, 2 (default) bounce >= 1 traces only: their incoherent
+                                      rays gain from refilling idle lanes (C5 -4.5 %) */
 #define ORT_OPT_PACKET 5           /* 1: wave-level walk for camera rays; 0 (default): per-lane walk (same pixels) */
 #define ORT_OPT_SORT_PATHS 6       /* 1 (default): sort the alive paths by direction octant + origin cell between
                                       bounces (coherence; same pixels); 0: keep them in slot order */

@@ -188,8 +188,10 @@ __global__ void __launch_bounds__(kBlock) ort_trace_persistent(PipeArgs A) {
     for (int q = 0; q < 6; ++q) cnt.v[q] = 0;
     ort::FastState st;
     int k = -1;
-    int next = 0, end = 0;   // wave-uniform: remaining slots [next, end) of the wave's chunk
-    bool drained = false;    // wave-uniform: the global cursor passed A.total
+    int next = 0, end = 0;   // wave-uniform: remaining work items [next, end) of the wave's chunk
+    bool drained = false;    // wave-uniform: the global cursor passed the item count
+    // items: the compacted (sorted) alive-path list of a bounce >= 1, or every slot
+    const int total = A.qlist ? *A.qcount : A.total;
     for (;;) {
         const unsigned long long idle = __ballot(k < 0);
         const int n_idle = __popcll(idle);
@@ -199,18 +201,18 @@ __global__ void __launch_bounds__(kBlock) ort_trace_persistent(PipeArgs A) {
                 int base = 0;
                 if (lane == 0) base = atomicAdd(A.sync + 1, kChunk);
                 base = __shfl(base, 0);
-                if (base >= A.total) {
+                if (base >= total) {
                     drained = true;
                     continue;
                 }
                 next = base;
-                end = min(base + kChunk, A.total);
+                end = min(base + kChunk, total);
             }
             const int take = min(n_idle, end - next);
             if (k < 0) {
                 const int rank = __popcll(idle & below);
                 if (rank < take) {
-                    const int cand = next + rank;
+                    const int cand = A.qlist ? A.qlist[next + rank] : next + rank;
                     bool alive;
                     const ort::Ray ray = load_ray(A, cand, alive);
                     if (alive) {
@@ -733,7 +735,7 @@ struct ort_ctx {
     int force_layout = -1;
     int exact_only = 0;
     int refill = 16;
-    int persistent = 0;
+    int persistent = 2;  // ORT_OPT_PERSISTENT: 0 off, 1 every trace, 2 bounce >= 1 traces (default)
     int packet = 0;     // ORT_OPT_PACKET: wave-level walk for camera rays (SALU-bound so far: off)
     int sort_paths = 1; // ORT_OPT_SORT_PATHS: coherence-sort the alive paths between bounces
     float root_lo[3] = {0, 0, 0}, root_hi[3] = {0, 0, 0};  // root box (coherence-sort key)
@@ -1103,9 +1105,11 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
             (rc = ensure(ctx, ctx->pcol, 16 * slots)))
             return rc;
     }
-    const bool compact = !direct && !ctx->persistent && p->max_depth > 1;
+    const bool pers_all = ctx->persistent == 1;     // every trace persistent (rays stored by raygen)
+    const bool pers_bounce = ctx->persistent == 2;  // persistent only for the bounce >= 1 lists
+    const bool compact = !direct && !pers_all && p->max_depth > 1;
     // primary-ray mode (1 sample, 1 bounce) on the compact layout: the trace kernels shade
-    const bool fuse = direct && mode == 0 && !ctx->persistent && !ctx->packet;
+    const bool fuse = direct && mode == 0 && !pers_all && !ctx->packet;
     const bool sorted = compact && ctx->sort_paths;
     size_t qtemp_bytes = 0;
     if (compact) {
@@ -1146,10 +1150,10 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     bool first_trace = true;
     for (int smp = 0; smp < ns; ++smp) {
         a.sample = smp;
-        a.rays_stored = pblocks > 0;
+        a.rays_stored = pers_all && pblocks > 0;
         a.qlist = nullptr;  // bounce 0: every slot
         a.qcount = nullptr;
-        if (pblocks > 0) {  // the persistent kernel refills lanes from stored rays
+        if (a.rays_stored) {  // the persistent kernel refills lanes from stored rays
             hipLaunchKernelGGL(ort_raygen_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, s, a);
             if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "ort_raygen_kernel launch");
         }
@@ -1161,9 +1165,10 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                 HIPCHK(ctx, hipMemsetAsync(ctx->defer_count.p, 0, 64, s));
                 const int slot = (int)(ctx->frames % ort_ctx::kRing);
                 if (first_trace) HIPCHK(ctx, hipEventRecord(ctx->tr0[slot], s));
-                const bool prim = (b == 0) && pblocks == 0;
-                e = dcounters ? launch_trace<true>(mode, prim, a, (int)blocks, pblocks, lds, s, ctx->packet != 0, fuse)
-                              : launch_trace<false>(mode, prim, a, (int)blocks, pblocks, lds, s, ctx->packet != 0, fuse);
+                const bool prim = (b == 0) && !a.rays_stored;
+                const int pb = (pers_all || (pers_bounce && b > 0)) ? pblocks : 0;
+                e = dcounters ? launch_trace<true>(mode, prim, a, (int)blocks, pb, lds, s, ctx->packet != 0, fuse)
+                              : launch_trace<false>(mode, prim, a, (int)blocks, pb, lds, s, ctx->packet != 0, fuse);
                 if (e != hipSuccess) return hip_fail(ctx, e, "trace kernel launch");
                 if (first_trace) {
                     HIPCHK(ctx, hipEventRecord(ctx->tr1[slot], s));
@@ -1171,7 +1176,7 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                     first_trace = false;
                 }
                 if (mode == 0) {
-                    const bool prim = (b == 0) && pblocks == 0;
+                    const bool prim = (b == 0) && !a.rays_stored;
                     const dim3 g(exact_blocks), t(kBlock);
                     if (dcounters && fuse) hipLaunchKernelGGL((ort_trace_exact<true, true, true>), g, t, lds_exact, s, a);
                     else if (dcounters && prim) hipLaunchKernelGGL((ort_trace_exact<true, true, false>), g, t, lds_exact, s, a);
@@ -1294,7 +1299,8 @@ int ort_set_option(ort_ctx* ctx, int option, int value) {
         return ORT_OK;
     }
     if (option == ORT_OPT_PERSISTENT) {
-        ctx->persistent = value ? 1 : 0;
+        if (value < 0 || value > 2) return fail(ctx, ORT_ERR_INVALID_ARG, "persistent must be 0, 1 or 2");
+        ctx->persistent = value;
         return ORT_OK;
     }
     if (option == ORT_OPT_PACKET) {

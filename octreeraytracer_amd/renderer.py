@@ -122,9 +122,10 @@ class Renderer:
         """Coherence-sort the alive paths between bounces (default on); same pixels."""
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_SORT_PATHS, int(bool(on))))
 
-    def set_persistent(self, on: bool):
-        """Use the persistent trace kernel with per-lane ray refill (default: one ray per lane)."""
-        self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_PERSISTENT, int(bool(on))))
+    def set_persistent(self, on):
+        """Persistent trace kernel with lane refill: False/0 off, True/1 every trace, 2 bounce >= 1
+        traces only (same pixels)."""
+        self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_PERSISTENT, int(on)))
 
     def set_refill(self, lanes: int):
         """Persistent trace: refill a wave once at least `lanes` of its 64 lanes are idle."""

@@ -131,7 +131,7 @@ def test_errors(ort, renderer, scene_c1):
 
 @pytest.mark.parametrize("persistent,exact,refill,packet", [
     (False, False, 16, True), (False, False, 16, False), (False, True, 16, True), (True, False, 1, False),
-    (True, False, 16, False), (True, True, 64, False)])
+    (True, False, 16, False), (True, True, 64, False), (2, False, 8, False), (2, True, 32, False)])
 def test_kernel_variants_identical(ort, oracle, renderer, scene_c2, persistent, exact, refill, packet):
     """Every trace-kernel variant (packet walk / one ray per lane / persistent with refill,
     fast / exact walk) produces the oracle's pixels, also with several samples and bounces."""
@@ -150,7 +150,7 @@ def test_kernel_variants_identical(ort, oracle, renderer, scene_c2, persistent, 
         p1 = ort.FrameParams.default_camera(1920, 1080)
         assert_same(renderer.render(p1, tile), oracle.render(s, t, p1, 700, 300, 200, 120), "primary")
     finally:
-        renderer.set_persistent(False)
+        renderer.set_persistent(2)  # the default
         renderer.set_exact_traversal(False)
         renderer.set_refill(16)
         renderer.set_packet(False)
@@ -206,3 +206,21 @@ def test_bounce_compaction_after_larger_frames(ort, oracle, renderer, scene_c2):
         ref = oracle.render(s, t, p, tile.x0, tile.y0, tile.width, tile.rows, band_height=tile.band_height,
                             band_stride=tile.band_stride)
         assert_same(got, ref, f"compaction tile {tile}")
+
+
+@pytest.mark.parametrize("depth,mspn", [(9, 0), (10, 1)])
+def test_deep_tree_kernel_bit_exact(ort, oracle, renderer, depth, mspn):
+    """Depth 9-10 trees take ort_trace_compact_deep (96-bit level masks): primary frame and
+    multi-bounce tiles (path compaction + coherence sort) against the oracle."""
+    s = ort.random_spheres(20_000, 7)
+    t = ort.build_octree(s, depth, mspn)
+    renderer.build_scene(s, depth, mspn)
+    assert renderer.info()["layout"] == "compact" and renderer.info()["tree_depth"] == depth
+    p = ort.FrameParams.default_camera(640, 360)
+    assert_same(renderer.render(p), oracle.render(s, t, p), f"deep d{depth} primary")
+    pb = ort.FrameParams.default_camera(1280, 720, num_samples=2, max_depth=4)
+    for tile in (ort.Tile(300, 160, 200, 96), ort.Tile(0, 1280, 5, 48, 8, 90)):
+        got = renderer.render(pb, tile)
+        ref = oracle.render(s, t, pb, tile.x0, tile.y0, tile.width, tile.rows, band_height=tile.band_height,
+                            band_stride=tile.band_stride)
+        assert_same(got, ref, f"deep d{depth} bounces {tile}")

@@ -1,9 +1,10 @@
 """Interleaved A/B timing of kernel variants in one process (cdna_hip_programming.md 5.4
 rule 24): frames of the variants alternate, and every variant must produce the same pixels.
 usage: python tools/ab.py [config] [rounds] [variant,variant,...]
-variants: exact (GLSL min/max walk), lane (default per-lane walk), packet (wave-level walk
+variants: exact (GLSL min/max walk), lane (the defaults: per-lane walk for camera rays,
+persistent refill kernel for bounces >= 1), laneonly (per-lane walk everywhere), packet (wave-level walk
 for camera rays), nosort (bounce paths compacted but not coherence-sorted), refillN
-(persistent trace, refill threshold N)."""
+(persistent trace, refill threshold N), bounceN (persistent only for bounces >= 1)."""
 import sys
 from pathlib import Path
 
@@ -20,7 +21,7 @@ names = sys.argv[3].split(",") if len(sys.argv) > 3 else ["exact", "lane", "pack
 
 
 def settings(name):
-    s = {"exact": False, "refill": 0, "packet": False, "sort": True}
+    s = {"exact": False, "refill": 0, "packet": False, "sort": True, "pmode": 1}
     if name == "exact":
         s["exact"] = True
     elif name == "packet":
@@ -29,7 +30,9 @@ def settings(name):
         s["sort"] = False
     elif name.startswith("refill"):
         s["refill"] = int(name[6:])
-    elif name != "lane":
+    elif name.startswith("bounce"):  # persistent kernel for the bounce >= 1 lists only
+        s["refill"], s["pmode"] = int(name[6:]), 2
+    elif name not in ("lane", "laneonly"):
         raise SystemExit(f"unknown variant {name}")
     return s
 
@@ -49,7 +52,7 @@ for k in range(rounds + 1):
         r.set_exact_traversal(v["exact"])
         r.set_packet(v["packet"])
         r.set_sort_paths(v["sort"])
-        r.set_persistent(v["refill"] > 0)
+        r.set_persistent(v["pmode"] if v["refill"] > 0 else (2 if name == "lane" else 0))
         if v["refill"] > 0:
             r.set_refill(v["refill"])
         r.render(p, out=out)
