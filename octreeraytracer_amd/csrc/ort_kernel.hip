@@ -64,6 +64,8 @@ struct PipeArgs {
     float4* pcol;     // running sum of samples
     float* out;
     unsigned long long* counters;
+    ulonglong4* wclock;  // analysis only (ort_debug_wave_clock): per queue block {t0, t1, hw ids, 0}
+    int wclock_n;
 };
 
 __host__ __device__ inline int tile_row_to_y(const TileMap& t, int j) {
@@ -89,6 +91,20 @@ struct LdsView {
     ort::LdsFrames fr;
 };
 template <bool WITH_LUT>
+__device__ inline LdsView lds_view(unsigned char* smem, int D) {
+    const int np = 3 * ((1 << D) + 1);
+    const size_t poff = align16(sizeof(float) * (size_t)np);
+    const size_t foff = poff + kRankLutBytes;
+    LdsView v;
+    v.planes = reinterpret_cast<float*>(smem);
+    v.lut = WITH_LUT ? smem + poff : nullptr;
+    v.fr.co = reinterpret_cast<int*>(smem + foff);
+    v.fr.tm = reinterpret_cast<float*>(smem + foff + (size_t)(D > 0 ? D : 1) * kBlock * sizeof(int));
+    v.fr.stride = kBlock;
+    v.fr.lane = threadIdx.x;
+    return v;
+}
+template <bool WITH_LUT>
 __device__ inline LdsView setup_lds(unsigned char* smem, const ort::KScene& S) {
     const int tid = threadIdx.x;
     const int D = S.depth;
@@ -100,16 +116,8 @@ __device__ inline LdsView setup_lds(unsigned char* smem, const ort::KScene& S) {
     if (WITH_LUT)
         for (int i = tid; i < (int)kRankLutBytes; i += kBlock)
             lut[i] = ort::rank_lut_entry((uint32_t)i >> 8, (uint32_t)i & 255u);
-    const size_t foff = poff + kRankLutBytes;
-    LdsView v;
-    v.planes = lp;
-    v.lut = WITH_LUT ? lut : nullptr;
-    v.fr.co = reinterpret_cast<int*>(smem + foff);
-    v.fr.tm = reinterpret_cast<float*>(smem + foff + (size_t)(D > 0 ? D : 1) * kBlock * sizeof(int));
-    v.fr.stride = kBlock;
-    v.fr.lane = tid;
     __syncthreads();
-    return v;
+    return lds_view<WITH_LUT>(smem, D);
 }
 
 // Path slot k (tile-block order: 256 slots = one 16x16 tile, 64 = one 8x8 wave block)
@@ -175,10 +183,13 @@ __global__ void __launch_bounds__(kBlock) ort_raygen_kernel(PipeArgs A) {
 #ifndef ORT_TRACE_WAVES_DEEP  // 96-bit masks, no inline leaf children: 64 VGPRs, spill-free
 #define ORT_TRACE_WAVES_DEEP 8
 #endif
+#ifndef ORT_PERSISTENT_WAVES
+#define ORT_PERSISTENT_WAVES 5
+#endif
 constexpr int kChunk = 256;
 
 template <bool COUNT>
-__global__ void __launch_bounds__(kBlock) ort_trace_persistent(PipeArgs A) {
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ORT_PERSISTENT_WAVES))) ort_trace_persistent(PipeArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     LdsView L = setup_lds<true>(smem, A.S);
     const uint8_t* lut = L.lut;
@@ -307,20 +318,15 @@ __device__ inline void shade_direct_padding(const PipeArgs& A, int k) {
 // One ray per lane over the compact layout (default): the tile-block order of the path
 // slots keeps each wave on an 8x8 pixel block, whose rays walk nearly the same nodes.
 // DEEP: trees deeper than 8 levels need the 96-bit level masks (ort_trace_compact_deep).
+// One path slot k of the compact-layout trace (the per-lane walk); counts accumulate in cnt.
 template <bool COUNT, bool PRIMARY, bool DEEP, bool FUSE>
-__device__ __forceinline__ void trace_compact_body(PipeArgs& A, unsigned char* smem) {
-    if (!PRIMARY && A.qlist && (int)(blockIdx.x * kBlock) >= *A.qcount) return;  // whole block past the list
-    LdsView L = setup_lds<true>(smem, A.S);
-    int k = blockIdx.x * kBlock + threadIdx.x;
-    if (!PRIMARY && !list_slot(A, k)) return;
+__device__ __forceinline__ void trace_slot(PipeArgs& A, LdsView& L, int k, ort::Counters& cnt) {
     bool alive;
     const ort::Ray ray = slot_ray<PRIMARY>(A, k, alive);
     if (!alive) {
         if (FUSE) shade_direct_padding(A, k);
         return;
     }
-    ort::Counters cnt;
-    for (int q = 0; q < 6; ++q) cnt.v[q] = 0;
     const ort::V3 inv = ort::mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
     if (A.exact_only || !ort::fast_path_ok(ray, inv, 0.001f, ORT_MAXFLOAT)) {
         A.defer_list[atomicAdd(A.sync, 1)] = k;  // ort_trace_exact walks (and, FUSE, shades) it
@@ -355,6 +361,58 @@ __device__ __forceinline__ void trace_compact_body(PipeArgs& A, unsigned char* s
     } else {
         A.hit[k] = make_int2(hit ? entry : -1, __float_as_int(t));
     }
+}
+
+template <bool COUNT, bool PRIMARY, bool DEEP, bool FUSE>
+__device__ __forceinline__ void trace_compact_body(PipeArgs& A, unsigned char* smem) {
+    if (!PRIMARY && A.qlist && (int)(blockIdx.x * kBlock) >= *A.qcount) return;  // whole block past the list
+    LdsView L = setup_lds<true>(smem, A.S);
+    int k = blockIdx.x * kBlock + threadIdx.x;
+    if (!PRIMARY && !list_slot(A, k)) return;
+    ort::Counters cnt;
+    for (int q = 0; q < 6; ++q) cnt.v[q] = 0;
+    trace_slot<COUNT, PRIMARY, DEEP, FUSE>(A, L, k, cnt);
+    flush_counts<COUNT>(cnt, A.counters);
+}
+
+// Wave queue (ORT_OPT_WAVE_QUEUE): resident workgroups whose waves each take the next 64-slot
+// block (an 8x8 pixel block, or 64 entries of a bounce list) with one atomic, as soon as
+// their previous block is done -- no workgroup-level wait and one LDS setup per resident
+// group.  Balances the tail when a GPU has few blocks (a 1/8 band tile of an 8-GPU frame).
+template <bool COUNT, bool PRIMARY, bool DEEP, bool FUSE>
+__device__ __forceinline__ void trace_queue_body(PipeArgs& A, unsigned char* smem) {
+    (void)setup_lds<true>(smem, A.S);
+    const int lane = threadIdx.x & 63;
+    const int items = (!PRIMARY && A.qlist) ? *A.qcount : A.total;
+    const int nblk = (items + 63) >> 6;
+    int* cursor = A.sync + 1;
+    ort::Counters cnt;
+    for (int q = 0; q < 6; ++q) cnt.v[q] = 0;
+    for (;;) {
+        int w = 0;
+        if (lane == 0) w = atomicAdd(cursor, 1);
+        w = __shfl(w, 0);
+        if (w >= nblk) break;
+        int k = w * 64 + lane;
+        // kernel arguments re-read per block through a laundered pointer: hoisted out of the
+        // loop they would stay live across the walk and spill
+#if defined(__HIP_DEVICE_COMPILE__)
+        typedef __attribute__((address_space(4))) const PipeArgs KernArgs;
+        KernArgs* kp = (KernArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(kp));
+        PipeArgs A1 = *kp;
+#else
+        PipeArgs& A1 = A;
+#endif
+        LdsView L = lds_view<true>(smem, A1.S.depth);
+        const unsigned long long t0 = A1.wclock ? __builtin_amdgcn_s_memrealtime() : 0;
+        if (PRIMARY || list_slot(A1, k)) trace_slot<COUNT, PRIMARY, DEEP, FUSE>(A1, L, k, cnt);
+        if (A1.wclock && lane == 0 && w < A1.wclock_n) {
+            const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);     // HW_ID: wave, simd, cu, se
+            const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);   // XCC_ID
+            A1.wclock[w] = make_ulonglong4(t0, __builtin_amdgcn_s_memrealtime(), hw, xcc);
+        }
+    }
     flush_counts<COUNT>(cnt, A.counters);
 }
 
@@ -369,6 +427,17 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ORT
 ort_trace_compact_deep(PipeArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     trace_compact_body<COUNT, PRIMARY, true, FUSE>(A, smem);
+}
+template <bool COUNT, bool PRIMARY, bool FUSE>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ORT_TRACE_WAVES))) ort_trace_compact_q(PipeArgs A) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    trace_queue_body<COUNT, PRIMARY, false, FUSE>(A, smem);
+}
+template <bool COUNT, bool PRIMARY, bool FUSE>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ORT_TRACE_WAVES_DEEP)))
+ort_trace_compact_deep_q(PipeArgs A) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    trace_queue_body<COUNT, PRIMARY, true, FUSE>(A, smem);
 }
 
 // Wave-wide OR of v (every lane of the wave must be executing): DPP prefix-OR inside each
@@ -736,6 +805,9 @@ struct ort_ctx {
     int exact_only = 0;
     int refill = 16;
     int persistent = 2;  // ORT_OPT_PERSISTENT: 0 off, 1 every trace, 2 bounce >= 1 traces (default)
+    void* wclock = nullptr;  // ort_debug_wave_clock
+    long long wclock_n = 0;
+    int wave_queue = 0;  // ORT_OPT_WAVE_QUEUE: per-lane walk from a wave-level block queue (opt-in)
     int packet = 0;     // ORT_OPT_PACKET: wave-level walk for camera rays (SALU-bound so far: off)
     int sort_paths = 1; // ORT_OPT_SORT_PATHS: coherence-sort the alive paths between bounces
     float root_lo[3] = {0, 0, 0}, root_hi[3] = {0, 0, 0};  // root box (coherence-sort key)
@@ -1019,8 +1091,18 @@ int ensure(ort_ctx* ctx, DevBuf& b, size_t bytes) {
 
 template <bool COUNT, bool PRIMARY>
 hipError_t launch_trace_p(int mode, const PipeArgs& a, int blocks, int pblocks, size_t lds, hipStream_t s, bool packet,
-                          bool fuse) {
+                          bool fuse, int qblocks) {
     if (mode == 0 && pblocks > 0) hipLaunchKernelGGL((ort_trace_persistent<COUNT>), dim3(pblocks), dim3(kBlock), lds, s, a);
+    else if (mode == 0 && qblocks > 0 && !(PRIMARY && packet)) {
+        const dim3 g(qblocks), t(kBlock);
+        if (a.S.depth > 8) {
+            if (fuse) hipLaunchKernelGGL((ort_trace_compact_deep_q<COUNT, PRIMARY, true>), g, t, lds, s, a);
+            else hipLaunchKernelGGL((ort_trace_compact_deep_q<COUNT, PRIMARY, false>), g, t, lds, s, a);
+        } else {
+            if (fuse) hipLaunchKernelGGL((ort_trace_compact_q<COUNT, PRIMARY, true>), g, t, lds, s, a);
+            else hipLaunchKernelGGL((ort_trace_compact_q<COUNT, PRIMARY, false>), g, t, lds, s, a);
+        }
+    }
     else if (mode == 0 && PRIMARY && packet) {
         if (a.S.depth > 8) hipLaunchKernelGGL((ort_trace_packet<COUNT, true>), dim3(blocks), dim3(kBlock), lds, s, a);
         else hipLaunchKernelGGL((ort_trace_packet<COUNT, false>), dim3(blocks), dim3(kBlock), lds, s, a);
@@ -1040,9 +1122,9 @@ hipError_t launch_trace_p(int mode, const PipeArgs& a, int blocks, int pblocks, 
 
 template <bool COUNT>
 hipError_t launch_trace(int mode, bool primary, const PipeArgs& a, int blocks, int pblocks, size_t lds, hipStream_t s,
-                        bool packet, bool fuse) {
-    return primary ? launch_trace_p<COUNT, true>(mode, a, blocks, pblocks, lds, s, packet, fuse)
-                   : launch_trace_p<COUNT, false>(mode, a, blocks, pblocks, lds, s, packet, false);
+                        bool packet, bool fuse, int qblocks) {
+    return primary ? launch_trace_p<COUNT, true>(mode, a, blocks, pblocks, lds, s, packet, fuse, qblocks)
+                   : launch_trace_p<COUNT, false>(mode, a, blocks, pblocks, lds, s, packet, false, qblocks);
 }
 
 template <int MODE>
@@ -1057,6 +1139,21 @@ hipError_t launch_shade(int mode, bool first, bool direct, const PipeArgs& a, in
     if (mode == 0) return launch_shade_mode<0>(first, direct, a, blocks, s);
     if (mode == 1) return launch_shade_mode<1>(first, direct, a, blocks, s);
     return launch_shade_mode<2>(first, direct, a, blocks, s);
+}
+
+// Resident workgroups of the wave-queue trace kernels.
+int queue_blocks(ort_ctx* ctx, bool count, size_t lds, long long needed) {
+    int per_cu = 0, cus = 0;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device);
+    const bool deep = ctx->depth > 8;
+    if (count)
+        (void)(deep ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ort_trace_compact_deep_q<true, true, false>, kBlock, lds)
+                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ort_trace_compact_q<true, true, false>, kBlock, lds));
+    else
+        (void)(deep ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ort_trace_compact_deep_q<false, true, true>, kBlock, lds)
+                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ort_trace_compact_q<false, true, true>, kBlock, lds));
+    const long long b = (long long)std::max(per_cu, 1) * std::max(cus, 1);
+    return (int)std::max(1LL, std::min(b, needed));
 }
 
 // Resident workgroups of the persistent trace kernel (a plain launch: extra groups just
@@ -1141,10 +1238,14 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     a.pcol = (float4*)ctx->pcol.p;
     a.out = dout;
     a.counters = dcounters;
+    a.wclock = (ulonglong4*)ctx->wclock;
+    a.wclock_n = (int)ctx->wclock_n;
     const size_t lds = lds_bytes(mode, ctx->depth, false);
     const size_t lds_exact = lds_bytes(mode, ctx->depth, true);
     const int pblocks = (mode == 0 && ctx->persistent) ? persistent_blocks(ctx->device, dcounters != nullptr, lds, blocks) : 0;
     const int exact_blocks = 1024;
+    // wave queue: as many workgroups as are resident (never more than the frame has)
+    const int qblocks = (mode == 0 && ctx->wave_queue) ? queue_blocks(ctx, dcounters != nullptr, lds, blocks) : 0;
     hipError_t e;
     HIPCHK(ctx, hipEventRecord(ctx->ev0, s));
     bool first_trace = true;
@@ -1167,8 +1268,8 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                 if (first_trace) HIPCHK(ctx, hipEventRecord(ctx->tr0[slot], s));
                 const bool prim = (b == 0) && !a.rays_stored;
                 const int pb = (pers_all || (pers_bounce && b > 0)) ? pblocks : 0;
-                e = dcounters ? launch_trace<true>(mode, prim, a, (int)blocks, pb, lds, s, ctx->packet != 0, fuse)
-                              : launch_trace<false>(mode, prim, a, (int)blocks, pb, lds, s, ctx->packet != 0, fuse);
+                e = dcounters ? launch_trace<true>(mode, prim, a, (int)blocks, pb, lds, s, ctx->packet != 0, fuse, qblocks)
+                              : launch_trace<false>(mode, prim, a, (int)blocks, pb, lds, s, ctx->packet != 0, fuse, qblocks);
                 if (e != hipSuccess) return hip_fail(ctx, e, "trace kernel launch");
                 if (first_trace) {
                     HIPCHK(ctx, hipEventRecord(ctx->tr1[slot], s));
@@ -1305,6 +1406,10 @@ int ort_set_option(ort_ctx* ctx, int option, int value) {
     }
     if (option == ORT_OPT_PACKET) {
         ctx->packet = value ? 1 : 0;
+        return ORT_OK;
+    }
+    if (option == ORT_OPT_WAVE_QUEUE) {
+        ctx->wave_queue = value ? 1 : 0;
         return ORT_OK;
     }
     if (option == ORT_OPT_SORT_PATHS) {
@@ -1570,6 +1675,15 @@ int ort_debug_emulate_render(const float* cr, const float* ma, const float* fr, 
 // the primary-ray frame with the kernel's fast walk on the host and reports how the lanes'
 // visited-node sets overlap, to price wave-level (packet) traversal against the per-lane
 // loop.  stats: see tools/wave_stats.py for the field order.
+// Analysis only: the wave-queue trace kernels record, per 64-slot block, {start, end}
+// (s_memrealtime, 100 MHz), HW_ID and XCC_ID into dev (n records of 4 x u64); null = off.
+int ort_debug_wave_clock(ort_ctx* ctx, void* dev, int64_t n) {
+    if (!ctx) return ORT_ERR_INVALID_ARG;
+    ctx->wclock = dev;
+    ctx->wclock_n = dev ? n : 0;
+    return ORT_OK;
+}
+
 int ort_debug_wave_stats(const float* cr, const float* ma, const float* fr, int32_t n_spheres,
                          const float* node_min, const float* node_max, const int32_t* co, const int32_t* oo,
                          const int32_t* cnt, int32_t n_nodes, const int32_t* idx, int64_t n_indices,

@@ -118,6 +118,10 @@ class Renderer:
         """Wave-level (packet) walk for camera rays (default off: SALU-bound); same pixels."""
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_PACKET, int(bool(on))))
 
+    def set_wave_queue(self, on: bool):
+        """Wave-level block queue for the per-lane trace kernels (default on); same pixels."""
+        self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_WAVE_QUEUE, int(bool(on))))
+
     def set_sort_paths(self, on: bool):
         """Coherence-sort the alive paths between bounces (default on); same pixels."""
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_SORT_PATHS, int(bool(on))))

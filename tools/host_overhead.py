@@ -1,5 +1,8 @@
-"""Host-side cost of ort_render (enqueue only) vs GPU time per frame, device output.
-usage: python tools/host_overhead.py [config] [frames]"""
+"""Host-side cost of ort_render (enqueue only) vs GPU time per frame, device output; with a
+world size, rank 0's band tile of an N-GPU run (is the host fast enough to feed a GPU that
+renders 1/N of the frame?).  With inflight > 1, that many renderers (each with its own copy of
+the scene) take frames in turn on their own streams, so one frame's tail overlaps the next.
+usage: python tools/host_overhead.py [config] [frames] [world] [inflight] [torch|hip|prio]"""
 import sys
 import time
 from pathlib import Path
@@ -13,27 +16,51 @@ import octreeraytracer_amd as ort  # noqa: E402
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 100
+world = int(sys.argv[3]) if len(sys.argv) > 3 else 1
+inflight = int(sys.argv[4]) if len(sys.argv) > 4 else 1
+kind = sys.argv[5] if len(sys.argv) > 5 else "torch"
 W, H, N, D, M, NS, MD = bench.CONFIGS[cfg]
 s = ort.random_spheres(N, 42)
-t = ort.build_octree(s, D, M)
-r = ort.Renderer(0)
-r.upload(s, t)
+rs = [ort.Renderer(0) for _ in range(inflight)]
+for r in rs:
+    r.build_scene(s, D, M)
+from octreeraytracer_amd.distributed import rank_tile  # noqa: E402
+tile = rank_tile(W, H, 0, world)
 p = ort.FrameParams.default_camera(W, H, num_samples=NS, max_depth=MD)
-out = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
-st = torch.cuda.Stream()  # not the null stream (handle 0 = synchronous, see bench.py)
+outs = [torch.empty((tile.rows, W, 3), dtype=torch.float32, device="cuda") for _ in rs]
+if kind == "torch":
+    sts = [torch.cuda.Stream() for _ in rs]  # not the null stream (handle 0 = synchronous, see bench.py)
+elif kind == "prio":
+    sts = [torch.cuda.Stream(priority=-(i % 2)) for i in range(inflight)]
+else:  # streams made by HIP itself (one HW queue each, while the runtime has queues free)
+    import ctypes as C
+    hip = C.CDLL("libamdhip64.so")
+    sts = []
+    for _ in rs:
+        h = C.c_void_p()
+        assert hip.hipStreamCreateWithFlags(C.byref(h), 1) == 0
+        sts.append(torch.cuda.ExternalStream(h.value))
+st = sts[0]
 torch.cuda.set_stream(st)
-for _ in range(5):
-    r.render(p, out=out, stream=st.cuda_stream)
+for i in range(5 * inflight):
+    j = i % inflight
+    rs[j].render(p, tile, out=outs[j], stream=sts[j].cuda_stream)
 torch.cuda.synchronize()
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 t0 = time.perf_counter()
 e0.record(st)
-for _ in range(n):
-    r.render(p, out=out, stream=st.cuda_stream)
+for x in sts[1:]:
+    x.wait_stream(st)
+for i in range(n):
+    j = i % inflight
+    rs[j].render(p, tile, out=outs[j], stream=sts[j].cuda_stream)
+for x in sts[1:]:
+    st.wait_stream(x)
 e1.record(st)
 t1 = time.perf_counter()
 torch.cuda.synchronize()
 t2 = time.perf_counter()
-print(f"{cfg}: enqueue {1e3 * (t1 - t0) / n:.3f} ms/frame, wall {1e3 * (t2 - t0) / n:.3f} ms/frame, "
+r = rs[0]
+print(f"{cfg} world={world} inflight={inflight}: enqueue {1e3 * (t1 - t0) / n:.3f} ms/frame, wall {1e3 * (t2 - t0) / n:.3f} ms/frame, "
       f"gpu span {e0.elapsed_time(e1) / n:.3f} ms/frame, last frame pipeline {r.last_kernel_ms():.3f} ms, "
       f"trace {r.last_trace_ms():.3f} ms")
