@@ -55,6 +55,9 @@ def parse():
                     "(default: ort_build_scene, the GPU builder)")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"),
                     help="PMC-measured HBM bytes per launch (written by tools/pmc_traffic.py)")
+    ap.add_argument("--inflight", type=int, default=0,
+                    help="frames in flight, each on its own context and stream (0 = auto: 1 on one GPU, "
+                    "2 with N>1, where a band tile's tail would otherwise idle the GPU)")
     ap.add_argument("--save", default="", help="rank 0: save the assembled frame (.pfm/.png)")
     return ap.parse_args()
 
@@ -67,6 +70,11 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    inflight = args.inflight or (1 if world == 1 else 2)
+    if inflight > 1:
+        # frames in flight only overlap when their streams sit on different hardware queues;
+        # with HIP's default 4 queues per process, RCCL's and torch's streams share them
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, max(8, 4 * inflight)))
 
     import torch
     import torch.distributed as dist
@@ -78,7 +86,8 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     spheres = ort.random_spheres(NSPH, args.seed)
-    r = ort.Renderer(local)
+    rs = [ort.Renderer(local) for _ in range(inflight)]  # one context (scene copy + stream) per frame in flight
+    r = rs[0]
     setup = {}
     tree = None
     if args.host_build:  # the reference's CPU builder (restated) + upload
@@ -86,26 +95,31 @@ def main():
         tree = ort.build_octree(spheres, DEPTH, MPN)
         setup["host_octree_build_s"] = round(time.time() - t0, 3)
         t0 = time.time()
-        r.upload(spheres, tree)
-        setup["upload_s"] = round(time.time() - t0, 3)
+        for x in rs:
+            x.upload(spheres, tree)
+        setup["upload_s"] = round((time.time() - t0) / inflight, 3)
     else:  # GPU octree builder, same tree byte for byte (tests/test_gpu_build.py)
         t0 = time.time()
-        r.build_scene(spheres, DEPTH, MPN)
+        for x in rs:
+            x.build_scene(spheres, DEPTH, MPN)
         setup["gpu_octree_build_ms"] = round(r.last_build_ms(), 2)
-        setup["build_scene_wall_s"] = round(time.time() - t0, 3)
+        setup["build_scene_wall_s"] = round((time.time() - t0) / inflight, 3)
     info = r.info()
     p = ort.FrameParams.default_camera(W, H, num_samples=NS, max_depth=MAXD)
 
     # partition: 16-row bands dealt round-robin; every rank renders the same number of rows
     from octreeraytracer_amd.distributed import FrameGather, rank_tile
     tile = rank_tile(W, H, rank, world)
-    # two band tiles per rank: frame k's gather/assembly overlaps frame k+1's render
-    outs = [torch.empty((tile.rows, W, 3), dtype=torch.float32, device="cuda") for _ in range(2)]
+    # inflight+1 band tiles per rank: frame k's gather/assembly overlaps the next frames'
+    # renders, and frame k+1 (next context, next stream) fills the tail of frame k
+    nslot = inflight + 1
+    outs = [torch.empty((tile.rows, W, 3), dtype=torch.float32, device="cuda") for _ in range(nslot)]
     out = outs[0]
-    gather = FrameGather(dist, W, H, world, rank, "cuda", depth=2)
-    # a dedicated stream: torch's default stream is the HIP null stream (handle 0), which the
-    # C ABI reads as "no stream" and then renders synchronously on the context's stream
-    stream = torch.cuda.Stream()
+    gather = FrameGather(dist, W, H, world, rank, "cuda", depth=nslot)
+    # each context's own stream (never the HIP null stream, handle 0, which the C ABI reads
+    # as "no stream" and renders synchronously)
+    streams = [torch.cuda.ExternalStream(x.stream_handle()) for x in rs]
+    stream = streams[0]
     torch.cuda.set_stream(stream)
 
     pending = []
@@ -117,13 +131,15 @@ def main():
         return frame
 
     def step(k, ev=None):
-        slot = k % 2
-        drain(1)  # the previous use of this slot's tile has been gathered
+        slot, j = k % nslot, k % inflight
+        st = streams[j]
+        torch.cuda.set_stream(st)  # the gather of frame k waits on this stream; finish() waits here
+        drain(nslot - 1)  # the previous use of this slot's tile has been gathered
         if ev is not None:
-            ev[0].record(stream)
-        r.render(p, tile, out=outs[slot], stream=stream.cuda_stream)
+            ev[0].record(st)
+        rs[j].render(p, tile, out=outs[slot], stream=st.cuda_stream)
         if ev is not None:
-            ev[1].record(stream)
+            ev[1].record(st)
         pending.append(gather.submit(outs[slot], slot))
 
     for k in range(args.warmup):
@@ -144,7 +160,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     kern_ms = [a.elapsed_time(b) for a, b in evs]          # whole per-frame pipeline (trace+shade)
-    trace_ms = r.trace_times_ms(min(args.steps, 64))         # the dominant kernel, same frames
+    trace_ms = r.trace_times_ms(min(-(-args.steps // inflight), 64))  # dominant kernel, context 0's timed frames
     t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -195,7 +211,7 @@ def main():
                 "num_samples": NS, "max_bounces": MAXD, "nodes": info["n_nodes"], "indices": info["n_indices"],
                 "layout": info["layout"], "partition": "16-row bands round-robin + RCCL gather (async, "
                 "overlapping the next frame's render)" if world > 1
-                else "full frame", "rays_per_step": rays_per_frame, "rays": "traced rays (octree traversals), "
+                else "full frame", "frames_in_flight": inflight, "rays_per_step": rays_per_frame, "rays": "traced rays (octree traversals), "
                 "all bounces and ranks",
             },
             "frame_gpu_ms_avg": round(kern_avg_ms, 4),
@@ -228,7 +244,8 @@ def main():
             img = frame.cpu().numpy()
             from octreeraytracer_amd import image
             (image.write_png if args.save.endswith(".png") else image.write_pfm)(args.save, img)
-    r.close()
+    for x in rs:
+        x.close()
     if world > 1:
         dist.destroy_process_group()
     if rank == 0:

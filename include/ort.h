@@ -151,6 +151,11 @@ int ort_scene_export_octree(ort_ctx* ctx, float* node_min, float* node_max, int3
 /* Device time of the last ort_build_scene (HIP events; the reference's Octree::buildTime). */
 int ort_last_build_ms(const ort_ctx* ctx, float* ms);
 
+/* The context's own HIP stream (created non-blocking by ort_create), for callers that keep
+   several frames in flight on several contexts: a frame rendered on each context's stream
+   overlaps the tail of the previous frame (bench.py --inflight).  No reference counterpart. */
+int ort_get_stream(const ort_ctx* ctx, void** stream);
+
 /* Render the tile; rgb_out receives tile->rows * tile->width RGB float triples, row-major,
  * output row 0 first.  out_is_device != 0: rgb_out is a device pointer on ctx's device.
  * stream: a hipStream_t on ctx's device (stream-ordered, returns at once), or NULL for the

@@ -37,7 +37,7 @@ COUNT_NAMES = ("nodes_popped", "child_records", "leaf_objects", "accepted_hits",
 EXPORTED_SYMBOLS = (
     "ort_create", "ort_destroy", "ort_last_error", "ort_set_option", "ort_upload_scene",
     "ort_upload_octree_nodes", "ort_scene_get_info", "ort_render", "ort_last_kernel_ms", "ort_last_trace_ms",
-    "ort_trace_times_ms", "ort_build_scene", "ort_scene_export_octree", "ort_last_build_ms",
+    "ort_trace_times_ms", "ort_build_scene", "ort_scene_export_octree", "ort_last_build_ms", "ort_get_stream",
     "ort_count_traffic", "ort_scene_random", "ort_scene_prebuilt", "ort_scene_debug",
     "ort_octree_build", "ort_octree_sizes", "ort_octree_export", "ort_octree_nodes",
     "ort_octree_indices", "ort_octree_free", "ort_camera_view", "ort_version",
@@ -92,6 +92,7 @@ def _declare(lib):
         "ort_build_scene": (C.c_int, [_vp, _fp, _fp, _fp, C.c_int32, C.c_int32, C.c_int32, C.c_int32]),
         "ort_scene_export_octree": (C.c_int, [_vp, _fp, _fp, _ip, _ip, _ip, _ip]),
         "ort_last_build_ms": (C.c_int, [_vp, _fp]),
+        "ort_get_stream": (C.c_int, [_vp, C.POINTER(C.c_void_p)]),
         "ort_render": (C.c_int, [_vp, C.POINTER(OrtParams), C.POINTER(OrtTile), _vp, C.c_int, _vp]),
         "ort_last_kernel_ms": (C.c_int, [_vp, _fp]),
         "ort_last_trace_ms": (C.c_int, [_vp, _fp]),

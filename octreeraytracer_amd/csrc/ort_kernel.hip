@@ -1515,6 +1515,12 @@ int ort_scene_export_octree(ort_ctx* ctx, float* node_min, float* node_max, int3
     return ORT_OK;
 }
 
+int ort_get_stream(const ort_ctx* ctx, void** stream) {
+    if (!ctx || !stream) return fail(nullptr, ORT_ERR_INVALID_ARG, "ort_get_stream: null argument");
+    *stream = (void*)ctx->stream;
+    return ORT_OK;
+}
+
 int ort_last_build_ms(const ort_ctx* ctx, float* ms) {
     if (!ctx || !ms) return fail(nullptr, ORT_ERR_INVALID_ARG, "ort_last_build_ms: null argument");
     *ms = ctx->build_ms;

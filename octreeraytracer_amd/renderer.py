@@ -177,6 +177,12 @@ class Renderer:
                                                       L.iptr(cnt), L.iptr(idx)))
         return FlatOctree(nmin, nmax, co, oo, cnt, idx[:k])
 
+    def stream_handle(self) -> int:
+        """The context's own (non-blocking) HIP stream, e.g. for torch.cuda.ExternalStream."""
+        h = C.c_void_p()
+        self._check(self._lib.ort_get_stream(self._ctx, C.byref(h)))
+        return h.value or 0
+
     def last_build_ms(self) -> float:
         ms = C.c_float()
         self._check(self._lib.ort_last_build_ms(self._ctx, C.byref(ms)))

@@ -113,6 +113,31 @@ def test_device_output_and_stream(ort, renderer, scene_c1):
         assert np.array_equal(o.cpu().numpy(), host)
 
 
+def test_frames_in_flight(ort, scene_c1):
+    """bench.py --inflight: several contexts, each rendering on its own stream, frames
+    overlapping on the GPU (1 and 3 bounces) -- every frame equals the synchronous render."""
+    torch = pytest.importorskip("torch")
+    s, t = scene_c1
+    rs = [ort.Renderer(0) for _ in range(3)]
+    try:
+        for x in rs:
+            x.upload(s, t)
+        for md in (1, 3):
+            p = ort.FrameParams.default_camera(200, 136, max_depth=md)
+            host = rs[0].render(p)
+            sts = [torch.cuda.ExternalStream(x.stream_handle()) for x in rs]
+            assert all(st.cuda_stream != 0 for st in sts)
+            outs = [torch.full((136, 200, 3), -1.0, dtype=torch.float32, device="cuda:0") for _ in range(9)]
+            for k, o in enumerate(outs):
+                rs[k % 3].render(p, out=o, stream=sts[k % 3].cuda_stream)
+            torch.cuda.synchronize()
+            for o in outs:
+                assert np.array_equal(o.cpu().numpy(), host)
+    finally:
+        for x in rs:
+            x.close()
+
+
 def test_errors(ort, renderer, scene_c1):
     s, t = scene_c1
     renderer.upload(s, t)
@@ -129,18 +154,22 @@ def test_errors(ort, renderer, scene_c1):
     fresh.close()
 
 
-@pytest.mark.parametrize("persistent,exact,refill,packet", [
-    (False, False, 16, True), (False, False, 16, False), (False, True, 16, True), (True, False, 1, False),
-    (True, False, 16, False), (True, True, 64, False), (2, False, 8, False), (2, True, 32, False)])
-def test_kernel_variants_identical(ort, oracle, renderer, scene_c2, persistent, exact, refill, packet):
-    """Every trace-kernel variant (packet walk / one ray per lane / persistent with refill,
-    fast / exact walk) produces the oracle's pixels, also with several samples and bounces."""
+@pytest.mark.parametrize("persistent,exact,refill,packet,queue", [
+    (False, False, 16, True, False), (False, False, 16, False, False), (False, True, 16, True, False),
+    (True, False, 1, False, False), (True, False, 16, False, False), (True, True, 64, False, False),
+    (2, False, 8, False, False), (2, True, 32, False, False), (False, False, 16, False, True),
+    (2, False, 16, False, True), (2, True, 16, False, True)])
+def test_kernel_variants_identical(ort, oracle, renderer, scene_c2, persistent, exact, refill, packet, queue):
+    """Every trace-kernel variant (packet walk / one ray per lane / persistent with refill /
+    wave queue, fast / exact walk) produces the oracle's pixels, also with several samples
+    and bounces."""
     s, t = scene_c2
     renderer.upload(s, t)
     renderer.set_persistent(persistent)
     renderer.set_exact_traversal(exact)
     renderer.set_refill(refill)
     renderer.set_packet(packet)
+    renderer.set_wave_queue(queue)
     try:
         p = ort.FrameParams.default_camera(1920, 1080, num_samples=2, max_depth=3)
         tile = ort.Tile(700, 200, 300, 120)
@@ -154,6 +183,7 @@ def test_kernel_variants_identical(ort, oracle, renderer, scene_c2, persistent, 
         renderer.set_exact_traversal(False)
         renderer.set_refill(16)
         renderer.set_packet(False)
+        renderer.set_wave_queue(False)
 
 
 @pytest.fixture(scope="module")
