@@ -120,21 +120,27 @@ def main():
     # as "no stream" and renders synchronously)
     streams = [torch.cuda.ExternalStream(x.stream_handle()) for x in rs]
     stream = streams[0]
+    gstream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
 
     pending = []
 
     def drain(keep):
+        # finish() (RCCL wait + rank-0 assembly into the one frame buffer) on its own stream,
+        # so assemblies never overlap each other and never queue behind a render
         frame = None
-        while len(pending) > keep:
-            frame = gather.finish(pending.pop(0))
+        with torch.cuda.stream(gstream):
+            while len(pending) > keep:
+                frame = gather.finish(pending.pop(0))
         return frame
 
     def step(k, ev=None):
         slot, j = k % nslot, k % inflight
         st = streams[j]
-        torch.cuda.set_stream(st)  # the gather of frame k waits on this stream; finish() waits here
         drain(nslot - 1)  # the previous use of this slot's tile has been gathered
+        if world > 1:
+            st.wait_stream(gstream)  # ... as far as this frame's stream knows
+        torch.cuda.set_stream(st)  # frame k's gather (submit) waits on this stream
         if ev is not None:
             ev[0].record(st)
         rs[j].render(p, tile, out=outs[slot], stream=st.cuda_stream)
