@@ -58,6 +58,9 @@ def parse():
     ap.add_argument("--inflight", type=int, default=0,
                     help="frames in flight, each on its own context and stream (0 = auto: 1 on one GPU, "
                     "2 with N>1, where a band tile's tail would otherwise idle the GPU)")
+    ap.add_argument("--rehearse-one-gpu", action="store_true",
+                    help="testing only: every rank on GPU 0 with the gloo backend (exercises the N>1 code "
+                    "path on a one-GPU box; not a measurement)")
     ap.add_argument("--save", default="", help="rank 0: save the assembled frame (.pfm/.png)")
     return ap.parse_args()
 
@@ -67,7 +70,7 @@ def main():
     W, H, NSPH, DEPTH, MPN, NS, MAXD = CONFIGS[args.config]
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = 0 if args.rehearse_one_gpu else int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
     inflight = args.inflight or (1 if world == 1 else 2)
@@ -83,7 +86,10 @@ def main():
 
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.rehearse_one_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     spheres = ort.random_spheres(NSPH, args.seed)
     rs = [ort.Renderer(local) for _ in range(inflight)]  # one context (scene copy + stream) per frame in flight

@@ -431,23 +431,35 @@ ORT_FN float fmin3(float a, float b, float c) { return fminf(fminf(a, b), c); }
 // midpoint).  Valid without underflow/overflow in r and q: |n| in [2^-60, 2^100] and
 // a in [2^-3, 2^3] (checked per ray by fast_path_ok); otherwise the IEEE division.
 // 2.56e9 random (n, a) pairs in those ranges were checked bitwise against n / a on the host.
+// any_lane(p): p on any active lane of the wave (a wave-uniform branch: no exec-mask juggling
+// around a path that is almost never taken); p itself on the host.
+ORT_FN bool any_lane(bool p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_ballot_w64(p) != 0;
+#else
+    return p;
+#endif
+}
 ORT_FN float qdiv(float n, float a, float y) {
-    const float an = fabsf(n);
-    if (!(an >= 0x1p-60f && an <= 0x1p100f)) return n / a;
     const float q0 = n * y;
-    return fmaf(fmaf(-q0, a, n), y, q0);
+    float q = fmaf(fmaf(-q0, a, n), y, q0);
+    const float an = fabsf(n);
+    const bool slow = !(an >= 0x1p-60f && an <= 0x1p100f);
+    if (any_lane(slow)) q = slow ? n / a : q;
+    return q;
 }
 // Correctly rounded sqrt for x in [2^-96, 2^100]: the hardware estimate corrected by the
 // two residual tests of the compiler's own IEEE expansion, minus its denormal scaling and
 // special-value handling (not needed in that range); otherwise sqrtf.
 ORT_FN float qsqrt(float x) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    if (!(x >= 0x1p-96f && x <= 0x1p100f)) return sqrtf(x);
     const float s = __builtin_amdgcn_sqrtf(x);
     const float sm = __uint_as_float(__float_as_uint(s) - 1u);
     const float sp = __uint_as_float(__float_as_uint(s) + 1u);
     float r = (fmaf(-sm, s, x) <= 0.0f) ? sm : s;
     r = (fmaf(-sp, s, x) > 0.0f) ? sp : r;
+    const bool slow = !(x >= 0x1p-96f && x <= 0x1p100f);
+    if (any_lane(slow)) r = slow ? sqrtf(x) : r;
     return r;
 #else
     return sqrtf(x);
