@@ -7,7 +7,7 @@ SRC := octreeraytracer_amd/csrc
 OBJ := build/obj
 LIB := octreeraytracer_amd/lib/libort.so
 CXXFLAGS := -O3 -std=c++17 -ffp-contract=off -fno-fast-math -fPIC -Wall -Wextra -Wno-unused-parameter
-HIPFLAGS := -O3 -std=c++17 --offload-arch=$(ARCH) -ffp-contract=off -fno-fast-math -fPIC -Wall -Wno-unused-parameter
+HIPFLAGS := -O3 -std=c++17 --offload-arch=$(ARCH) -ffp-contract=off -fno-fast-math -fno-slp-vectorize -fPIC -Wall -Wno-unused-parameter
 
 HOST_SRCS := octree.cpp scene.cpp host_abi.cpp layout.cpp raytracer.cpp
 HOST_OBJS := $(addprefix $(OBJ)/,$(HOST_SRCS:.cpp=.o))

@@ -79,7 +79,7 @@ constexpr size_t kRankLutBytes = 8 * 256;  // ort::rank_lut_entry table
 // with_tm: the exact walk also keeps a per-level tmin column; the fast walk needs none.
 size_t lds_bytes(int mode, int depth, bool with_tm) {
     if (mode != 0) return 0;
-    const size_t planes = align16(sizeof(float) * 3 * (((size_t)1 << depth) + 1));
+    const size_t planes = align16(sizeof(float) * (size_t)ort::fast_plane_floats(depth));  // + reversed copies
     const size_t levels = (size_t)std::max(depth, 1);
     return planes + kRankLutBytes + (with_tm ? 2 : 1) * levels * kBlock * sizeof(int);
 }
@@ -92,7 +92,7 @@ struct LdsView {
 };
 template <bool WITH_LUT>
 __device__ inline LdsView lds_view(unsigned char* smem, int D) {
-    const int np = 3 * ((1 << D) + 1);
+    const int np = ort::fast_plane_floats(D);
     const size_t poff = align16(sizeof(float) * (size_t)np);
     const size_t foff = poff + kRankLutBytes;
     LdsView v;
@@ -108,9 +108,9 @@ template <bool WITH_LUT>
 __device__ inline LdsView setup_lds(unsigned char* smem, const ort::KScene& S) {
     const int tid = threadIdx.x;
     const int D = S.depth;
-    const int np = 3 * ((1 << D) + 1);
+    const int np = ort::fast_plane_floats(D);
     float* lp = reinterpret_cast<float*>(smem);
-    for (int i = tid; i < np; i += kBlock) lp[i] = S.planes[i];
+    ort::fill_fast_planes(S.planes, lp, D, tid, kBlock);  // forward tables, then reversed
     const size_t poff = align16(sizeof(float) * (size_t)np);
     uint8_t* lut = smem + poff;
     if (WITH_LUT)
@@ -178,7 +178,7 @@ __global__ void __launch_bounds__(kBlock) ort_raygen_kernel(PipeArgs A) {
 // Waves per SIMD of the per-lane trace kernel: 7 (72 VGPRs) -- at 8 (64 VGPRs) the walk with
 // inline leaf children spills ~5 registers per iteration and runs 1.6x slower (tools/ab_libs.py).
 #ifndef ORT_TRACE_WAVES
-#define ORT_TRACE_WAVES 7
+#define ORT_TRACE_WAVES 8
 #endif
 #ifndef ORT_TRACE_WAVES_DEEP  // 96-bit masks, no inline leaf children: 64 VGPRs, spill-free
 #define ORT_TRACE_WAVES_DEEP 8
@@ -242,8 +242,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ORT
             continue;
         }
         if (k >= 0) {
-            if (ort::fast_step<COUNT>(A.S, st, L.fr, cnt)) {
-                A.hit[k] = make_int2(st.hit ? st.hitEntry : -1, __float_as_int(st.closest));
+            if (ort::fast_step<COUNT>(A.S, lut, st, L.fr, cnt)) {
+                A.hit[k] = make_int2(st.hitEntry, __float_as_int(st.closest));
                 k = -1;
             }
         }
@@ -1611,6 +1611,7 @@ int ort_debug_emulate_render(const float* cr, const float* ma, const float* fr, 
         S.n_spheres = n_spheres;
         S.n_nodes = n_nodes;
         ort::CompactLayout cl;
+        std::vector<float> fplanes;  // fast-walk plane tables (forward + reversed)
         std::vector<float> A, B;
         int mode = 2;
         if (p->use_octree == 1) {
@@ -1625,6 +1626,8 @@ int ort_debug_emulate_render(const float* cr, const float* ma, const float* fr, 
                 S.leaf_idx = cl.leaf_idx.data();
                 S.planes = cl.planes.data();
                 S.depth = cl.depth;
+                fplanes.resize(ort::fast_plane_floats(cl.depth));
+                ort::fill_fast_planes(cl.planes.data(), fplanes.data(), cl.depth);
             } else {
                 mode = 1;
                 A.resize(4 * (size_t)n_nodes);
@@ -1661,7 +1664,7 @@ int ort_debug_emulate_render(const float* cr, const float* ma, const float* fr, 
                 ort::Counters cc;
                 for (int k = 0; k < 6; ++k) cc.v[k] = 0;
                 ort::V3 v;
-                if (mode == 0) v = ort::shade_pixel<0, true>(pp, S, S.planes, rank_lut, lf, nullptr, nullptr, t->x0 + c, y, cc);
+                if (mode == 0) v = ort::shade_pixel<0, true>(pp, S, fplanes.data(), rank_lut, lf, nullptr, nullptr, t->x0 + c, y, cc);
                 else if (mode == 1) v = ort::shade_pixel<1, true>(pp, S, nullptr, nullptr, lf, snode.data(), stmin.data(), t->x0 + c, y, cc);
                 else v = ort::shade_pixel<2, true>(pp, S, nullptr, nullptr, lf, nullptr, nullptr, t->x0 + c, y, cc);
                 o[0] = v.x; o[1] = v.y; o[2] = v.z;
@@ -1709,6 +1712,8 @@ int ort_debug_wave_stats(const float* cr, const float* ma, const float* fr, int3
         S.leaf_idx = cl.leaf_idx.data();
         S.planes = cl.planes.data();
         S.depth = cl.depth;
+        std::vector<float> fplanes(ort::fast_plane_floats(cl.depth));
+        ort::fill_fast_planes(cl.planes.data(), fplanes.data(), cl.depth);
         std::vector<uint8_t> lut(kRankLutBytes);
         for (size_t i = 0; i < lut.size(); ++i) lut[i] = ort::rank_lut_entry((uint32_t)i >> 8, (uint32_t)i & 255u);
         const ort::PixelParams pp = pixel_params(p);
@@ -1738,10 +1743,10 @@ int ort_debug_wave_stats(const float* cr, const float* ma, const float* fr, int3
                 if (m0 < 0) m0 = m;
                 else if (m != m0) uniform = false;
                 ort::FastStateT<ort::Masks96> fs;
-                if (!ort::fast_begin(S, S.planes, lut.data(), ray, inv, 0.001f, ORT_MAXFLOAT, fs)) continue;
+                if (!ort::fast_begin(S, fplanes.data(), lut.data(), ray, inv, 0.001f, ORT_MAXFLOAT, fs)) continue;
                 for (;;) {
                     seq[l].push_back(fs.node);
-                    if (ort::fast_step<false>(S, fs, lf, cc)) break;
+                    if (ort::fast_step<false>(S, lut.data(), fs, lf, cc)) break;
                 }
                 maxlen = std::max(maxlen, seq[l].size());
             }

@@ -385,13 +385,16 @@ ORT_FN uint8_t rank_lut_entry(uint32_t m, uint32_t cmask) {
 }
 
 ORT_FN bool a_in_qdiv_range(float a) { return a >= 0.125f && a <= 8.0f; }
+// The fast walk's t_min (the shader's only one, glsl:hit(r, 0.001, ...)) is a literal in the
+// instruction stream rather than a per-ray register.
+constexpr float kFastTMin = 0.001f;
 // The fast walk's preconditions: finite 1/d and origin (no slab value can be NaN), a
 // positive t_min and finite t_max (the push test below relies on both), dot(d,d) in
 // qdiv's range.
 ORT_FN bool fast_path_ok(const Ray& r, V3 inv, float t_min, float t_max) {
     return fabsf(inv.x) <= ORT_MAXFLOAT && fabsf(inv.y) <= ORT_MAXFLOAT && fabsf(inv.z) <= ORT_MAXFLOAT &&
            fabsf(r.o.x) <= ORT_MAXFLOAT && fabsf(r.o.y) <= ORT_MAXFLOAT && fabsf(r.o.z) <= ORT_MAXFLOAT &&
-           t_min > 0.0f && t_max <= ORT_MAXFLOAT && a_in_qdiv_range(dot(r.d, r.d));
+           t_min == kFastTMin && t_max <= ORT_MAXFLOAT && a_in_qdiv_range(dot(r.d, r.d));
 }
 
 // 24-bit signed multiply (plane indices are < 2^11): one full-rate VALU op on the device.
@@ -419,7 +422,10 @@ ORT_FN float fmin3(float a, float b, float c) {
     asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
     return r;
 }
+// max(x, kFastTMin) with the constant as an instruction literal (0x3a83126f = 0.001f)
+ORT_FN float fmax_tmin(float x) { float r; asm("v_max_f32 %0, 0x3a83126f, %1" : "=v"(r) : "v"(x)); return r; }
 #else
+ORT_FN float fmax_tmin(float x) { return fmaxf(x, kFastTMin); }
 ORT_FN float fmax2(float a, float b) { return fmaxf(a, b); }
 ORT_FN float fmin2(float a, float b) { return fminf(a, b); }
 ORT_FN float fmax3(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
@@ -504,9 +510,27 @@ ORT_FN float4 fetch_sphere(const KScene& S, int e) {
 #endif
 }
 
-// Plane idx of a ray-order table: base + s4*idx bytes (s4 = +-4): one v_mad_i32_i24.
-ORT_FN float plane_at(const float* base, int s4, int idx) {
-    return *(const float*)((const char*)base + imul24(s4, idx));
+// Plane idx of a ray-order table (base[idx]; see fast_begin for the reversed copies).
+ORT_FN float plane_at(const float* base, int idx) { return base[idx]; }
+
+// For trees of depth <= 8 the fast walk reads its split planes from a table of
+// 6 * (2^D + 1) floats: the layout's three axis tables (axis a at a * P1) followed by the
+// same three reversed (axis a at 3 * P1 + a * P1, entry i = forward entry 2^D - i), so that
+// a ray walking an axis downwards indexes its planes upwards like every other ray -- no
+// per-ray stride register.  Deeper trees keep the forward tables only (the reversed copies
+// would cost LDS occupancy) and a +-4 byte stride per axis.
+ORT_FN bool fast_rev_planes(int depth) { return depth <= 8; }
+ORT_FN int fast_plane_floats(int depth) { return (fast_rev_planes(depth) ? 6 : 3) * ((1 << depth) + 1); }
+ORT_FN void fill_fast_planes(const float* fwd, float* out, int depth, int i0 = 0, int step = 1) {
+    const int P1 = (1 << depth) + 1;
+    const bool rev = fast_rev_planes(depth);
+    for (int i = i0; i < 3 * P1; i += step) {
+        out[i] = fwd[i];
+        if (rev) {
+            const int a = i / P1, j = i - a * P1;
+            out[3 * P1 + a * P1 + (P1 - 1 - j)] = fwd[i];
+        }
+    }
 }
 
 // Rank-reversed level masks (see above).  pop() returns hb = 8L + 7 - rank.
@@ -514,6 +538,7 @@ struct Masks64 {  // levels 0..7: trees of depth <= 8
     // test the leaf children of a LEAFKIDS node inline (fast_step); pays for its registers on
     // depth <= 8 trees (all leaves at the bottom level with maxSpheresPerNode 0), not deeper
     static constexpr bool kInlineLeaves = true;
+    static constexpr bool kRevPlanes = true;  // depth <= 8: reversed plane tables (fast_rev_planes)
     uint64_t m;
     ORT_FN void clear() { m = 0; }
     ORT_FN bool empty() const { return m == 0; }
@@ -539,6 +564,7 @@ struct Masks64 {  // levels 0..7: trees of depth <= 8
 };
 struct Masks96 {  // levels 0..11
     static constexpr bool kInlineLeaves = false;
+    static constexpr bool kRevPlanes = false;
     uint64_t lo;
     uint32_t hi;
     ORT_FN void clear() { lo = 0; hi = 0; }
@@ -578,26 +604,43 @@ struct Masks96 {  // levels 0..11
 };
 
 // Resumable per-lane state of the fast walk (so a persistent kernel can interleave rays).
+// Registers are what limits the walk (7 waves/SIMD at 72 VGPRs), so nothing derivable is
+// kept: the world-axis origin comes back from the role-axis one (swap = bit 1 of otab's
+// nibble 0, which is m), dot(d, d) is recomputed per leaf, the half width from depth, the
+// LUT row from m, and "hit" is hitEntry >= 0.
 template <class Masks>
 struct FastStateT {
-    Ray r;           // original-axis ray (Sphere_hit uses it as is)
-    float a;         // dot(d, d)
-    float ya;        // RN(1 / a)
+    V3 d;            // original-axis direction (Sphere_hit)
+    float ya;        // RN(1 / dot(d, d))
     float oA, oB, oC, iA, iB, iC;  // role-axis origin / 1/d
-    const float* pA;  // ray-order plane table of each role axis: plane(i) = *(pA + sA*i bytes)
-    const float* pB;
+    const float* pA;  // ray-order plane table of each role axis: plane(i) = pA[i] (kRevPlanes)
+    const float* pB;  // or *(pA + sA * i bytes)
     const float* pC;
-    int sA, sB, sC;   // +-4: byte stride along the ray
-    int h;            // half the current node's width, in plane steps (0 at depth D)
+    int sA, sB, sC;   // +-4 (only without kRevPlanes)
     float tNA, tFA, tNB, tFB, tNC, tFC;  // near/far plane t of the current node's box
-    int cA, cB, cC;  // ray-order index of the current node's near plane
-    uint32_t otab;   // nibble r = octant of rank r
-    const uint8_t* lut_row;  // rank LUT row of this ray's order xor m
+    uint32_t cP;     // ray-order index of the current node's near plane, 10 bits per axis (A, B, C)
+    uint32_t otab;   // nibble r = octant of rank r; nibble 0 = m
     int node, depth;
-    float tmin0, closest;
-    int hitEntry;
-    bool hit;
+    float closest;   // (t_min is kFastTMin)
+    int hitEntry;    // -1: no hit yet
     Masks masks;
+    ORT_FN bool hit() const { return hitEntry >= 0; }
+    ORT_FN float pl(const float* p, int s, int idx) const {
+        return Masks::kRevPlanes ? p[idx] : *(const float*)((const char*)p + imul24(s, idx));
+    }
+    ORT_FN float plA(int idx) const { return pl(pA, sA, idx); }
+    ORT_FN float plB(int idx) const { return pl(pB, sB, idx); }
+    ORT_FN float plC(int idx) const { return pl(pC, sC, idx); }
+    ORT_FN int cA() const { return (int)(cP & 1023u); }
+    ORT_FN int cB() const { return (int)((cP >> 10) & 1023u); }
+    ORT_FN int cC() const { return (int)(cP >> 20); }
+    ORT_FN Ray ray() const {
+        const bool swap = (otab >> 1) & 1u;
+        Ray r;
+        r.o = mk(swap ? oB : oA, swap ? oA : oB, oC);
+        r.d = d;
+        return r;
+    }
 };
 using FastState = FastStateT<Masks96>;
 
@@ -612,39 +655,42 @@ ORT_FN bool fast_begin(const KScene& S, const float* planes, const uint8_t* rank
     const uint32_t m = (nz << 2) | (nx << 1) | ny;
     const bool swap = nx != 0;
     const uint32_t gA = swap ? ny : nx, gB = swap ? nx : ny, gC = nz;
-    st.r = r;
-    st.a = dot(r.d, r.d);
-    st.ya = 1.0f / st.a;
+    st.d = r.d;
+    st.ya = 1.0f / dot(r.d, r.d);
     st.oA = swap ? r.o.y : r.o.x;
     st.oB = swap ? r.o.x : r.o.y;
     st.oC = r.o.z;
     st.iA = swap ? inv.y : inv.x;
     st.iB = swap ? inv.x : inv.y;
     st.iC = inv.z;
-    st.pA = planes + (swap ? P1 : 0) + (gA ? top : 0);
-    st.pB = planes + (swap ? 0 : P1) + (gB ? top : 0);
-    st.pC = planes + 2 * P1 + (gC ? top : 0);
-    st.sA = gA ? -4 : 4;
-    st.sB = gB ? -4 : 4;
-    st.sC = gC ? -4 : 4;
-    st.h = top >> 1;
+    // planes: fast_plane_floats(D) floats (fill_fast_planes)
+    if (Masks::kRevPlanes) {  // forward tables, then reversed
+        st.pA = planes + (gA ? 3 * P1 : 0) + (swap ? P1 : 0);
+        st.pB = planes + (gB ? 3 * P1 : 0) + (swap ? 0 : P1);
+        st.pC = planes + (gC ? 3 * P1 : 0) + 2 * P1;
+        st.sA = st.sB = st.sC = 4;
+    } else {
+        st.pA = planes + (swap ? P1 : 0) + (gA ? top : 0);
+        st.pB = planes + (swap ? 0 : P1) + (gB ? top : 0);
+        st.pC = planes + 2 * P1 + (gC ? top : 0);
+        st.sA = gA ? -4 : 4;
+        st.sB = gB ? -4 : 4;
+        st.sC = gC ? -4 : 4;
+    }
     uint32_t ot = 0;
     for (uint32_t k = 0; k < 8; ++k) ot |= rank_perm(k, m) << (4 * k);
     st.otab = ot;
-    st.lut_row = rank_lut + m * 256u;
-    st.tNA = st.iA * (st.pA[0] - st.oA);
-    st.tFA = st.iA * (plane_at(st.pA, st.sA, top) - st.oA);
-    st.tNB = st.iB * (st.pB[0] - st.oB);
-    st.tFB = st.iB * (plane_at(st.pB, st.sB, top) - st.oB);
-    st.tNC = st.iC * (st.pC[0] - st.oC);
-    st.tFC = st.iC * (plane_at(st.pC, st.sC, top) - st.oC);
-    st.cA = st.cB = st.cC = 0;
+    st.tNA = st.iA * (st.plA(0) - st.oA);
+    st.tFA = st.iA * (st.plA(top) - st.oA);
+    st.tNB = st.iB * (st.plB(0) - st.oB);
+    st.tFB = st.iB * (st.plB(top) - st.oB);
+    st.tNC = st.iC * (st.plC(0) - st.oC);
+    st.tFC = st.iC * (st.plC(top) - st.oC);
+    st.cP = 0;
     st.node = 0;
     st.depth = 0;
-    st.tmin0 = t_min;
     st.closest = t_max;
     st.hitEntry = -1;
-    st.hit = false;
     st.masks.clear();
     return fmin3(st.tFA, st.tFB, st.tFC) >= fmax3(st.tNA, st.tNB, st.tNC);
 }
@@ -653,24 +699,25 @@ ORT_FN bool fast_begin(const KScene& S, const float* planes, const uint8_t* rank
 // true if one was accepted (the walk then ends after this leaf).
 template <bool COUNT, class Masks>
 ORT_FN bool leaf_tests(const KScene& S, FastStateT<Masks>& st, int off, int n, float ntmin, Counters& cnt) {
+    const Ray r = st.ray();
+    const float a = dot(r.d, r.d);  // as fast_begin computed it
     for (int i = 0; i < n; ++i) {
         const float4 sp = fetch_sphere(S, off + i);
         if (COUNT) cnt.v[2] += 1;
         float t;
-        if (sphere_hit_fast(st.r, st.a, st.ya, sp, ntmin, st.closest, t)) {
-            st.hit = true;
+        if (sphere_hit_fast(r, a, st.ya, sp, ntmin, st.closest, t)) {
             st.closest = t;
             st.hitEntry = off + i;
             if (COUNT) cnt.v[3] += 1;
         }
     }
-    return st.hit;
+    return st.hit();
 }
 
 // One node of the walk: visit st.node (push its surviving children, or test its spheres),
 // then pop the next node.  Returns true when the walk is over (hit found, or stack empty).
 template <bool COUNT, class Masks, class Frames>
-ORT_FN bool fast_step(const KScene& S, FastStateT<Masks>& st, Frames& fr, Counters& cnt) {
+ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks>& st, Frames& fr, Counters& cnt) {
     const int D = S.depth;
     const uint2 rec = fetch_node(S, st.node);
     if (COUNT) cnt.v[0] += 1;
@@ -680,15 +727,15 @@ ORT_FN bool fast_step(const KScene& S, FastStateT<Masks>& st, Frames& fr, Counte
             const long long rem = (long long)S.n_nodes - (long long)co;
             cnt.v[1] += (unsigned long long)(rem >= 8 ? 8 : (rem > 0 ? rem : 0));
         }
-        const uint32_t rcm = st.lut_row[rec.y & 0xffu];
-        const int h = st.h;
-        const float tMA = st.iA * (plane_at(st.pA, st.sA, st.cA + h) - st.oA);
-        const float tMB = st.iB * (plane_at(st.pB, st.sB, st.cB + h) - st.oB);
-        const float tMC = st.iC * (plane_at(st.pC, st.sC, st.cC + h) - st.oC);
+        const uint32_t rcm = rank_lut[((st.otab & 7u) << 8) | (rec.y & 0xffu)];  // LUT row m
+        const int h = 1 << (D - 1 - st.depth);  // half the node's width, in plane steps
+        const float tMA = st.iA * (st.plA(st.cA() + h) - st.oA);
+        const float tMB = st.iB * (st.plB(st.cB() + h) - st.oB);
+        const float tMC = st.iC * (st.plC(st.cC() + h) - st.oC);
         const float tNA = st.tNA, tNB = st.tNB, tNC = st.tNC, tFA = st.tFA, tFB = st.tFB, tFC = st.tFC;
         // child R enters at max3 of its axis entries (near half: tN, far half: tM) and exits at
         // min3 of its exits (tM / tF); t_min and t_max are folded into the C axis.
-        const float nN = fmax2(tNC, st.tmin0), nF = fmax2(tMC, st.tmin0);
+        const float nN = fmax_tmin(tNC), nF = fmax_tmin(tMC);
         const float cN = fmin2(tMC, st.closest), cF = fmin2(tFC, st.closest);  // closest == t_max here
         // keep child R <=> exit >= entry, with entry >= t_min > 0 and exit <= t_max finite, so
         // exit - entry is never NaN and is +0 when equal: its sign bit is "drop".  The drop
@@ -718,7 +765,7 @@ ORT_FN bool fast_step(const KScene& S, FastStateT<Masks>& st, Frames& fr, Counte
                 const uint2 lrec = fetch_node(S, co + (int)((st.otab >> (4 * R)) & 15u));
                 if (COUNT) cnt.v[0] += 1;
                 const float eA = (R & 2u) ? tMA : tNA, eB = (R & 1u) ? tMB : tNB, eC = (R & 4u) ? tMC : tNC;
-                if (leaf_tests<COUNT>(S, st, (int)lrec.x, (int)lrec.y, fmax2(fmax3(eA, eB, eC), st.tmin0), cnt))
+                if (leaf_tests<COUNT>(S, st, (int)lrec.x, (int)lrec.y, fmax_tmin(fmax3(eA, eB, eC)), cnt))
                     return true;  // glsl:336
             }
         } else {
@@ -728,28 +775,42 @@ ORT_FN bool fast_step(const KScene& S, FastStateT<Masks>& st, Frames& fr, Counte
             fr.setCo(st.depth, co);
         }
     } else {
-        const float ntmin = st.depth == 0 ? st.tmin0 : fmax2(fmax3(st.tNA, st.tNB, st.tNC), st.tmin0);
+        const float ntmin = st.depth == 0 ? kFastTMin : fmax_tmin(fmax3(st.tNA, st.tNB, st.tNC));
         if (leaf_tests<COUNT>(S, st, (int)rec.x, (int)rec.y, ntmin, cnt)) return true;  // glsl:336
     }
     if (st.masks.empty()) return true;
+#if defined(__HIP_DEVICE_COMPILE__) && defined(ORT_PAD_VALU)
+    {   // issue-sensitivity experiment only (tools): ORT_PAD_VALU extra VALU per step
+        float pv = 0.0f;
+        for (int q = 0; q < ORT_PAD_VALU; ++q) asm volatile("v_mov_b32 %0, %0" : "+v"(pv));
+    }
+#endif
+#if defined(__HIP_DEVICE_COMPILE__) && defined(ORT_PAD_SALU)
+    {   // issue-sensitivity experiment only (tools): ORT_PAD_SALU extra SALU per step
+        int ps = 0;
+        for (int q = 0; q < ORT_PAD_SALU; ++q) asm volatile("s_mov_b32 %0, %0" : "+s"(ps));
+    }
+#endif
     // next node: lowest remaining rank of the deepest level with one left
     const int hb = st.masks.pop();
     const int L = hb >> 3;
     const uint32_t rk = (uint32_t)(~hb) & 7u;
     const int w = 1 << (D - 1 - L);  // child width in plane steps
     const int keep = -2 * w;         // clears the offsets below the level-L ancestor
-    st.cA = (st.cA & keep) | (((rk >> 1) & 1) ? w : 0);
-    st.cB = (st.cB & keep) | ((rk & 1) ? w : 0);
-    st.cC = (st.cC & keep) | (((rk >> 2) & 1) ? w : 0);
+    {   // per 10-bit field: (c & keep) | (axis bit of rk ? w : 0)
+        const uint32_t k3 = ((uint32_t)keep & 1023u) * 0x100401u;
+        const uint32_t bits = ((rk >> 1) & 1u) | ((rk & 1u) << 10) | (((rk >> 2) & 1u) << 20);
+        st.cP = (st.cP & k3) | bits * (uint32_t)w;
+    }
     st.depth = L + 1;
-    st.h = w >> 1;
     st.node = fr.getCo(L) + (int)((st.otab >> (4 * rk)) & 15u);
-    st.tNA = st.iA * (plane_at(st.pA, st.sA, st.cA) - st.oA);
-    st.tFA = st.iA * (plane_at(st.pA, st.sA, st.cA + w) - st.oA);
-    st.tNB = st.iB * (plane_at(st.pB, st.sB, st.cB) - st.oB);
-    st.tFB = st.iB * (plane_at(st.pB, st.sB, st.cB + w) - st.oB);
-    st.tNC = st.iC * (plane_at(st.pC, st.sC, st.cC) - st.oC);
-    st.tFC = st.iC * (plane_at(st.pC, st.sC, st.cC + w) - st.oC);
+    const int cA = st.cA(), cB = st.cB(), cC = st.cC();
+    st.tNA = st.iA * (st.plA(cA) - st.oA);
+    st.tFA = st.iA * (st.plA(cA + w) - st.oA);
+    st.tNB = st.iB * (st.plB(cB) - st.oB);
+    st.tFB = st.iB * (st.plB(cB + w) - st.oB);
+    st.tNC = st.iC * (st.plC(cC) - st.oC);
+    st.tFC = st.iC * (st.plC(cC + w) - st.oC);
     return false;
 }
 
@@ -758,11 +819,11 @@ ORT_FN bool traverse_fast_t(const KScene& S, const float* planes, const uint8_t*
                             float t_min, float t_max, int& hitEntry, float& hitT, Frames& fr, Counters& cnt) {
     FastStateT<Masks> st;
     if (!fast_begin(S, planes, rank_lut, r, inv, t_min, t_max, st)) return false;
-    while (!fast_step<COUNT>(S, st, fr, cnt)) {
+    while (!fast_step<COUNT>(S, rank_lut, st, fr, cnt)) {
     }
     hitEntry = st.hitEntry;
     hitT = st.closest;
-    return st.hit;
+    return st.hit();
 }
 
 template <bool COUNT, class Frames>
