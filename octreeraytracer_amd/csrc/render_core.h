@@ -465,7 +465,12 @@ ORT_FN float qsqrt(float x) {
     float r = (fmaf(-sm, s, x) <= 0.0f) ? sm : s;
     r = (fmaf(-sp, s, x) > 0.0f) ? sp : r;
     const bool slow = !(x >= 0x1p-96f && x <= 0x1p100f);
-    if (any_lane(slow)) r = slow ? sqrtf(x) : r;
+    if (any_lane(slow)) {
+        // the volatile asm keeps this a real (wave-uniform) branch: left alone, the compiler
+        // if-converts it and evaluates sqrtf's IEEE expansion on every call
+        asm volatile("" ::: "memory");
+        r = slow ? sqrtf(x) : r;
+    }
     return r;
 #else
     return sqrtf(x);
@@ -621,6 +626,8 @@ struct FastStateT {
     uint32_t cP;     // ray-order index of the current node's near plane, 10 bits per axis (A, B, C)
     uint32_t otab;   // nibble r = octant of rank r; nibble 0 = m
     int node, depth;
+    uint2 rec;       // node record of `node`, loaded as soon as the pop knows it (its latency
+                     // overlaps the pop's plane reads instead of opening the next step)
     float closest;   // (t_min is kFastTMin)
     int hitEntry;    // -1: no hit yet
     Masks masks;
@@ -688,6 +695,7 @@ ORT_FN bool fast_begin(const KScene& S, const float* planes, const uint8_t* rank
     st.tFC = st.iC * (st.plC(top) - st.oC);
     st.cP = 0;
     st.node = 0;
+    st.rec = fetch_node(S, 0);
     st.depth = 0;
     st.closest = t_max;
     st.hitEntry = -1;
@@ -719,7 +727,7 @@ ORT_FN bool leaf_tests(const KScene& S, FastStateT<Masks>& st, int off, int n, f
 template <bool COUNT, class Masks, class Frames>
 ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks>& st, Frames& fr, Counters& cnt) {
     const int D = S.depth;
-    const uint2 rec = fetch_node(S, st.node);
+    const uint2 rec = st.rec;
     if (COUNT) cnt.v[0] += 1;
     if (rec.y & ORT_INTERNAL_FLAG) {
         const int co = (int)rec.x;
@@ -804,6 +812,7 @@ ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks
     }
     st.depth = L + 1;
     st.node = fr.getCo(L) + (int)((st.otab >> (4 * rk)) & 15u);
+    st.rec = fetch_node(S, st.node);
     const int cA = st.cA(), cB = st.cB(), cC = st.cC();
     st.tNA = st.iA * (st.plA(cA) - st.oA);
     st.tFA = st.iA * (st.plA(cA + w) - st.oA);
