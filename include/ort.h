@@ -90,8 +90,11 @@ typedef struct ort_scene_info {
 #define ORT_OPT_PACKET 5           /* 1: wave-level walk for camera rays; 0 (default): per-lane walk (same pixels) */
 #define ORT_OPT_SORT_PATHS 6       /* 1 (default): sort the alive paths by direction octant + origin cell between
                                       bounces (coherence; same pixels); 0: keep them in slot order */
-#define ORT_OPT_WAVE_QUEUE 7       /* 1 (default): resident workgroups whose waves take 64-slot blocks from
-                                      a queue (balances small tiles); 0: one workgroup per 16x16 tile */
+#define ORT_OPT_WAVE_QUEUE 7       /* 1: resident workgroups whose waves take 64-slot blocks from a queue;
+                                      0 (default): one workgroup per 16x16 tile (same pixels) */
+#define ORT_OPT_XCD_SWIZZLE 8      /* workgroup -> tile order (same pixels): 2 (default) each XCD renders
+                                      runs of 8 consecutive raster tiles; 1: each XCD renders 128x128-pixel
+                                      super-tiles; 0: raster order (tile b on XCD b % 8) */
 
 /* Traffic counters (ort_count_traffic), in the REFERENCE layout's terms. */
 #define ORT_COUNT_NODES_POPPED 0

@@ -43,7 +43,8 @@ struct PipeArgs {
     ort::PixelParams pp;
     ort::KScene S;
     TileMap tm;
-    int tilesX;
+    int tilesX, tilesY;
+    int swizzle;      // ORT_OPT_XCD_SWIZZLE (block_tile)
     int total;        // path slots = workgroups x 256 (tile-block order, some are holes)
     int sample;       // s of main()'s sample loop
     int last;         // this bounce is the last one (b == maxDepth - 1)
@@ -120,11 +121,50 @@ __device__ inline LdsView setup_lds(unsigned char* smem, const ort::KScene& S) {
     return lds_view<WITH_LUT>(smem, D);
 }
 
+// Tile (bx, by) of 16x16 pixels rendered by workgroup blk.  The dispatcher deals workgroup b
+// to XCD b % 8, each XCD with its own L2.  ORT_OPT_XCD_SWIZZLE picks the order:
+//   0  raster: XCD x renders every 8th tile of a tile row -- neighbouring tiles, whose rays
+//      walk the same octree nodes, are spread over all 8 L2s;
+//   2  (default) within every 64 consecutive workgroups the 8 that land on one XCD get 8
+//      consecutive raster tiles (a 128x16-pixel run): c3 +2%, c5 +2% in interleaved A/B
+//      (tools/ab_stream.py);
+//   1  within every 512 the 64 of one XCD get an 8x8-tile super-tile (128x128 pixels): more
+//      compact but slower at c3 (-1.5% vs raster) -- the run order keeps consecutive
+//      workgroups of one XCD on neighbouring tiles while they are resident together.
+// Each is a bijection on any tile grid (a last partial group keeps raster order; super-tiles at
+// the frame's right/bottom edge are narrower), so the pixels are the same whichever order runs.
+__host__ __device__ inline void block_tile(const PipeArgs& A, int blk, int& bx, int& by) {
+    if (!A.swizzle) {
+        bx = blk % A.tilesX;
+        by = blk / A.tilesX;
+        return;
+    }
+    int l = blk;
+    if (A.swizzle == 2) {  // raster order in chunks of 8 tiles per XCD
+        if ((blk | 63) < A.tilesX * A.tilesY) l = (blk & ~63) | ((blk & 7) << 3) | ((blk >> 3) & 7);
+        bx = l % A.tilesX;
+        by = l / A.tilesX;
+        return;
+    }
+    if ((blk | 511) < A.tilesX * A.tilesY) l = (blk & ~511) | ((blk & 7) << 6) | ((blk >> 3) & 63);
+    // logical order: super-rows of 8 tile rows; in one, super-tiles of 8 tile columns left to
+    // right; in one, tiles in raster order
+    const int srow = l / (A.tilesX * 8);
+    const int rem = l - srow * A.tilesX * 8;
+    const int rows = A.tilesY - srow * 8 < 8 ? A.tilesY - srow * 8 : 8;
+    const int sc = rem / (8 * rows);
+    const int r2 = rem - sc * 8 * rows;
+    const int cols = A.tilesX - sc * 8 < 8 ? A.tilesX - sc * 8 : 8;
+    bx = sc * 8 + r2 % cols;
+    by = srow * 8 + r2 / cols;
+}
+
 // Path slot k (tile-block order: 256 slots = one 16x16 tile, 64 = one 8x8 wave block)
 // -> tile column/row.  Returns false for slots outside the tile.
 __host__ __device__ inline bool slot_coords(const PipeArgs& A, int k, int& col, int& row) {
     const int blk = k >> 8, tid = k & 255, wave = tid >> 6, lane = tid & 63;
-    const int bx = blk % A.tilesX, by = blk / A.tilesX;
+    int bx, by;
+    block_tile(A, blk, bx, by);
     col = bx * 16 + (wave & 1) * 8 + (lane & 7);
     row = by * 16 + (wave >> 1) * 8 + (lane >> 3);
     return col < A.tm.tw && row < A.tm.th;
@@ -301,9 +341,11 @@ __device__ inline void shade_direct(const PipeArgs& A, int k, ort::Ray ray, ort_
     (void)ort::shade_bounce(hit, rec, ray, c, importance, st);
     const ort::V3 v = ort::finish_pixel(ort::add(ort::mk(0.0f, 0.0f, 0.0f), c), 1);
     float* o = A.out + 3 * ((size_t)row * A.tm.tw + col);
-    o[0] = v.x;
-    o[1] = v.y;
-    o[2] = v.z;
+    // the frame is written once and never read here: non-temporal stores keep its 12 B/pixel
+    // from evicting scene lines out of L2 and the Infinity Cache
+    __builtin_nontemporal_store(v.x, o + 0);
+    __builtin_nontemporal_store(v.y, o + 1);
+    __builtin_nontemporal_store(v.z, o + 2);
 }
 // Tile rows past the frame (band padding) are written as zeros, as the shade kernel does.
 __device__ inline void shade_direct_padding(const PipeArgs& A, int k) {
@@ -807,6 +849,7 @@ struct ort_ctx {
     int persistent = 2;  // ORT_OPT_PERSISTENT: 0 off, 1 every trace, 2 bounce >= 1 traces (default)
     void* wclock = nullptr;  // ort_debug_wave_clock
     long long wclock_n = 0;
+    int xcd_swizzle = 2;  // ORT_OPT_XCD_SWIZZLE: workgroup -> tile order (block_tile)
     int wave_queue = 0;  // ORT_OPT_WAVE_QUEUE: per-lane walk from a wave-level block queue (opt-in)
     int packet = 0;     // ORT_OPT_PACKET: wave-level walk for camera rays (SALU-bound so far: off)
     int sort_paths = 1; // ORT_OPT_SORT_PATHS: coherence-sort the alive paths between bounces
@@ -1224,6 +1267,8 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     a.S = device_scene(ctx);
     a.tm = {t->x0, t->width, t->y0, t->rows, t->band_height, t->band_stride};
     a.tilesX = tilesX;
+    a.tilesY = tilesY;
+    a.swizzle = ctx->xcd_swizzle;
     a.total = (int)slots;
     a.exact_only = ctx->exact_only || !ctx->ordered;
     a.refill = ctx->refill;
@@ -1406,6 +1451,11 @@ int ort_set_option(ort_ctx* ctx, int option, int value) {
     }
     if (option == ORT_OPT_PACKET) {
         ctx->packet = value ? 1 : 0;
+        return ORT_OK;
+    }
+    if (option == ORT_OPT_XCD_SWIZZLE) {
+        if (value < 0 || value > 2) return fail(ctx, ORT_ERR_INVALID_ARG, "xcd swizzle must be 0, 1 or 2");
+        ctx->xcd_swizzle = value;
         return ORT_OK;
     }
     if (option == ORT_OPT_WAVE_QUEUE) {

@@ -119,8 +119,13 @@ class Renderer:
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_PACKET, int(bool(on))))
 
     def set_wave_queue(self, on: bool):
-        """Wave-level block queue for the per-lane trace kernels (default on); same pixels."""
+        """Wave-level block queue for the per-lane trace kernels (default off); same pixels."""
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_WAVE_QUEUE, int(bool(on))))
+
+    def set_xcd_swizzle(self, mode: int):
+        """Workgroup -> tile order (ORT_OPT_XCD_SWIZZLE): 2 (default) runs of 8 raster tiles per
+        XCD, 1 128x128-pixel super-tiles per XCD, 0 raster; same pixels."""
+        self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_XCD_SWIZZLE, int(mode)))
 
     def set_sort_paths(self, on: bool):
         """Coherence-sort the alive paths between bounces (default on); same pixels."""

@@ -254,3 +254,20 @@ def test_deep_tree_kernel_bit_exact(ort, oracle, renderer, depth, mspn):
         ref = oracle.render(s, t, pb, tile.x0, tile.y0, tile.width, tile.rows, band_height=tile.band_height,
                             band_stride=tile.band_stride)
         assert_same(got, ref, f"deep d{depth} bounces {tile}")
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_xcd_swizzle_orders_identical(ort, oracle, renderer, scene_c2, mode):
+    """Every workgroup -> tile order (ORT_OPT_XCD_SWIZZLE) renders the oracle's pixels: a
+    ragged tile (partial 512/64-workgroup groups, edge super-tiles), bounces included."""
+    s, t = scene_c2
+    renderer.upload(s, t)
+    renderer.set_xcd_swizzle(mode)
+    try:
+        p = ort.FrameParams.default_camera(1920, 1080, num_samples=1, max_depth=3)
+        tile = ort.Tile(13, 1900, 7, 1010)  # 119 x 64 tiles: ragged in both directions
+        assert_same(renderer.render(p, tile), oracle.render(s, t, p, 13, 7, 1900, 1010), f"swizzle {mode}")
+        with pytest.raises(ort.OrtError):
+            renderer.set_xcd_swizzle(3)
+    finally:
+        renderer.set_xcd_swizzle(2)

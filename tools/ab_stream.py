@@ -2,9 +2,16 @@
 GPU, device output, each build's frames back to back on its own stream (no host sync per
 frame), builds alternating in blocks of --block frames in ABBA order so clock and thermal
 drift hit every build alike.  Also checks that every build writes bit-identical frames.
-usage: python tools/ab_stream.py LIB_A LIB_B [...] [--config c3] [--rounds 12] [--block 10]"""
+usage: python tools/ab_stream.py LIB_A LIB_B [...] [--config c3] [--rounds 12] [--block 10]
+A build may carry options: path@option=value,... with option one of the Renderer setters
+(e.g. build/ab/libA.so@xcd_swizzle=0).
+
+Each build runs in a worker process of its own (all resident on the GPU, one rendering at a
+time): two builds loaded into ONE process share kernel names, and the HIP runtime then
+launched one build's kernels with the other's argument layout -- wrong frames, bogus times."""
 import argparse
-import ctypes as C
+import hashlib
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -12,61 +19,97 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 import numpy as np  # noqa: E402
-import torch  # noqa: E402
 
-import bench  # noqa: E402
-import octreeraytracer_amd as ort  # noqa: E402
-from octreeraytracer_amd import _lib as L  # noqa: E402
 
-ap = argparse.ArgumentParser()
-ap.add_argument("libs", nargs="+")
-ap.add_argument("--config", default="c3")
-ap.add_argument("--rounds", type=int, default=12)
-ap.add_argument("--block", type=int, default=10)
-args = ap.parse_args()
-W, H, N, D, M, NS, MD = bench.CONFIGS[args.config]
-s = ort.random_spheres(N, 42)
-p = ort.FrameParams.default_camera(W, H, num_samples=NS, max_depth=MD)
-libs, rs, outs, sts = [], [], [], []
-for path in args.libs:
+def worker(spec, config, block):
+    import ctypes as C
+
+    import torch
+
+    import bench
+    import octreeraytracer_amd as ort
+    from octreeraytracer_amd import _lib as L
+
+    W, H, N, D, M, NS, MD = bench.CONFIGS[config]
+    path, _, opts = spec.partition("@")
     lib = C.CDLL(str(Path(path).resolve()), mode=C.RTLD_LOCAL)
     L._declare(lib)
     L._lib = lib
     r = ort.Renderer(0)
-    r.build_scene(s, D, M)
-    libs.append(lib)
-    rs.append(r)
-    outs.append(torch.empty((H, W, 3), dtype=torch.float32, device="cuda"))
-    sts.append(torch.cuda.ExternalStream(r.stream_handle()))
-n = len(libs)
-per_frame = [[] for _ in range(n)]
-trace = [[] for _ in range(n)]
+    for o in filter(None, opts.split(",")):
+        name, val = o.split("=")
+        getattr(r, "set_" + name)(int(val))
+    r.build_scene(ort.random_spheres(N, 42), D, M)
+    p = ort.FrameParams.default_camera(W, H, num_samples=NS, max_depth=MD)
+    out = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+    st = torch.cuda.ExternalStream(r.stream_handle())
+    print("ready", flush=True)
+    for line in sys.stdin:
+        if line.strip() == "hash":
+            print(hashlib.md5(out.cpu().numpy().tobytes()).hexdigest(), flush=True)
+            continue
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(block):
+            r.render(p, out=out, stream=st.cuda_stream)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / block * 1e3
+        print(dt, float(np.median(r.trace_times_ms(block))), flush=True)
 
 
-def block(i, record):
-    L._lib = libs[i]
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.block):
-        rs[i].render(p, out=outs[i], stream=sts[i].cuda_stream)
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / args.block * 1e3
-    if record:
-        per_frame[i].append(dt)
-        trace[i].extend(rs[i].trace_times_ms(args.block))
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs="+")
+    ap.add_argument("--config", default="c3")
+    ap.add_argument("--rounds", type=int, default=12)
+    ap.add_argument("--block", type=int, default=10)
+    ap.add_argument("--worker", action="store_true")
+    args = ap.parse_args()
+    if args.worker:
+        return worker(args.libs[0], args.config, args.block)
+    import bench
+    W, H, N, D, M, NS, MD = bench.CONFIGS[args.config]
+    procs = []
+    for spec in args.libs:
+        procs.append(subprocess.Popen([sys.executable, "-u", __file__, spec, "--worker", "--config", args.config,
+                                       "--block", str(args.block)], stdin=subprocess.PIPE, stdout=subprocess.PIPE,
+                                      text=True, cwd=str(ROOT)))
+        while procs[-1].stdout.readline().strip() != "ready":
+            if procs[-1].poll() is not None:
+                raise SystemExit(f"worker for {spec} died")
+    n = len(procs)
+    per_frame = [[] for _ in range(n)]
+    trace = [[] for _ in range(n)]
+
+    def ask(i, cmd):
+        procs[i].stdin.write(cmd + "\n")
+        procs[i].stdin.flush()
+        ans = procs[i].stdout.readline()
+        if not ans:
+            raise SystemExit(f"worker {args.libs[i]} died")
+        return ans.split()
+
+    for i in range(n):
+        ask(i, "block")  # warm-up
+    for k in range(args.rounds):
+        for i in (range(n) if k % 2 == 0 else reversed(range(n))):
+            f, tr = ask(i, "block")
+            per_frame[i].append(float(f))
+            trace[i].append(float(tr))
+    hashes = [ask(i, "hash")[0] for i in range(n)]
+    for p in procs:
+        p.stdin.close()
+        p.wait()
+    for i in range(1, n):
+        if hashes[i] != hashes[0]:
+            print(f"WARNING: build {args.libs[i]} writes a different frame than {args.libs[0]}")
+    base = np.median(per_frame[0])
+    for i, spec in enumerate(args.libs):
+        f, tr = np.median(per_frame[i]), np.median(trace[i])
+        print(f"{args.config} {spec.split('/')[-1]:24s} frame {f:.4f} ms (min {np.min(per_frame[i]):.4f})  "
+              f"trace {tr:.4f} ms  -> {W * H * NS / f / 1e3:.1f} Mrays/s  "
+              f"({base / f:.3f}x of {args.libs[0].split('/')[-1]})")
 
 
-for i in range(n):
-    block(i, False)  # warm-up
-for k in range(args.rounds):
-    order = list(range(n)) if k % 2 == 0 else list(reversed(range(n)))
-    for i in order:
-        block(i, True)
-ref = outs[0].cpu().numpy().view(np.uint32)
-for i in range(1, n):
-    assert np.array_equal(ref, outs[i].cpu().numpy().view(np.uint32)), f"build {args.libs[i]} differs"
-base = np.median(per_frame[0])
-for i, path in enumerate(args.libs):
-    f, tr = np.median(per_frame[i]), np.median(trace[i])
-    print(f"{args.config} {Path(path).name:14s} frame {f:.4f} ms (min {np.min(per_frame[i]):.4f})  "
-          f"trace {tr:.4f} ms  -> {W * H * NS / f / 1e3:.1f} Mrays/s  ({base / f:.3f}x of {Path(args.libs[0]).name})")
+if __name__ == "__main__":
+    main()
