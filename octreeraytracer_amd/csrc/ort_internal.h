@@ -27,4 +27,16 @@ int ort_debug_wave_stats(const float* sphere_center_radius, const float* sphere_
                          const int32_t* object_count, int32_t n_nodes, const int32_t* object_indices,
                          int64_t n_indices, const ort_params* params, int32_t block_step, double* stats,
                          int32_t n_stats);
+// ANALYSIS-ONLY: the per-step work of the fast walk (the kernel's own fast_step, inline leaf
+// children) for the 64 lanes of sampled 8x8 primary-ray blocks (tools/walk_sim.py).
+// lens[64 * w + l] = steps of lane l of sampled wave w (0: not a fast-walk lane); steps[] =
+// the lanes' steps back to back, one uint16 each: objects tested (bits 0-7, saturated),
+// leaf children tested (bits 8-11), bit 15 = the step's node has leaf children (LEAFKIDS).
+// Returns the number of steps (or, if cap is too small, minus the number needed).
+int64_t ort_debug_walk_steps(const float* sphere_center_radius, const float* sphere_mat_albedo,
+                             const float* sphere_fuzz_ri, int32_t n_spheres, const float* node_min,
+                             const float* node_max, const int32_t* children_offset, const int32_t* objects_offset,
+                             const int32_t* object_count, int32_t n_nodes, const int32_t* object_indices,
+                             int64_t n_indices, const ort_params* params, int32_t block_step, int32_t* lens,
+                             int64_t n_lens, uint16_t* steps, int64_t cap);
 }

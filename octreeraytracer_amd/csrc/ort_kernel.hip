@@ -1846,4 +1846,69 @@ int ort_debug_wave_stats(const float* cr, const float* ma, const float* fr, int3
     }
 }
 
+
+int64_t ort_debug_walk_steps(const float* cr, const float* ma, const float* fr, int32_t n_spheres,
+                             const float* node_min, const float* node_max, const int32_t* co, const int32_t* oo,
+                             const int32_t* cnt, int32_t n_nodes, const int32_t* idx, int64_t n_indices,
+                             const ort_params* p, int32_t block_step, int32_t* lens, int64_t n_lens, uint16_t* steps,
+                             int64_t cap) {
+    try {
+        if (block_step < 1) return fail(nullptr, ORT_ERR_INVALID_ARG, "bad block_step");
+        ort::SceneInput in{cr, ma, fr, n_spheres, node_min, node_max, co, oo, cnt, n_nodes, idx, n_indices};
+        ort::CompactLayout cl;
+        std::string why;
+        if (!ort::buildCompactLayout(in, ORT_COMPACT_MAX_DEPTH, cl, why)) return fail(nullptr, ORT_ERR_UNSUPPORTED, why);
+        if (cl.depth > 8) return fail(nullptr, ORT_ERR_UNSUPPORTED, "walk_steps: depth <= 8 walk only");
+        ort::KScene S;
+        std::memset(&S, 0, sizeof(S));
+        S.n_spheres = n_spheres;
+        S.n_nodes = n_nodes;
+        S.node = (const uint2*)cl.node.data();
+        S.leaf_sph = (const float4*)cl.leaf_sph.data();
+        S.leaf_idx = cl.leaf_idx.data();
+        S.planes = cl.planes.data();
+        S.depth = cl.depth;
+        std::vector<float> fplanes(ort::fast_plane_floats(cl.depth));
+        ort::fill_fast_planes(cl.planes.data(), fplanes.data(), cl.depth);
+        std::vector<uint8_t> lut(kRankLutBytes);
+        for (size_t i = 0; i < lut.size(); ++i) lut[i] = ort::rank_lut_entry((uint32_t)i >> 8, (uint32_t)i & 255u);
+        const ort::PixelParams pp = pixel_params(p);
+        ort::LocalFrames lf;
+        const int bw = (p->width + 7) / 8, bh = (p->height + 7) / 8;
+        int64_t w = 0, n = 0;
+        for (int b = 0; b < bw * bh; b += block_step, ++w) {
+            const int bx = b % bw, by = b / bw;
+            for (int l = 0; l < 64; ++l) {
+                int32_t len = 0;
+                const int px = bx * 8 + (l & 7), py = by * 8 + (l >> 3);
+                if (px < p->width && py < p->height) {
+                    ort_rng st;
+                    ort::pixel_rng_init(pp, px, py, st);
+                    const ort::Ray ray = ort::primary_ray(pp, px, py, 0, st);
+                    const ort::V3 inv = ort::mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
+                    ort::FastStateT<ort::Masks64> fs;
+                    if (ort::fast_path_ok(ray, inv, 0.001f, ORT_MAXFLOAT) &&
+                        ort::fast_begin(S, fplanes.data(), lut.data(), ray, inv, 0.001f, ORT_MAXFLOAT, fs)) {
+                        for (bool done = false; !done;) {
+                            ort::Counters cc;
+                            for (int k = 0; k < 6; ++k) cc.v[k] = 0;
+                            const uint32_t y = fs.rec.y;
+                            done = ort::fast_step<true>(S, lut.data(), fs, lf, cc);
+                            const uint64_t objs = cc.v[2] < 255 ? cc.v[2] : 255, kids = cc.v[0] - 1;
+                            const bool lk = (y & ORT_INTERNAL_FLAG) && (y & ORT_LEAFKIDS_FLAG);
+                            if (n < cap) steps[n] = (uint16_t)(objs | (kids < 15 ? kids : 15) << 8 | (lk ? 0x8000u : 0u));
+                            ++n;
+                            ++len;
+                        }
+                    }
+                }
+                if (64 * w + l < n_lens) lens[64 * w + l] = len;
+            }
+        }
+        return n <= cap ? n : -n;
+    } catch (const std::exception& ex) {
+        return fail(nullptr, ORT_ERR_INTERNAL, ex.what());
+    }
+}
+
 }  // extern "C"
