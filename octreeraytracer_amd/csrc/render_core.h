@@ -825,11 +825,16 @@ ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks
 
 template <bool COUNT, class Masks, class Frames>
 ORT_FN bool traverse_fast_t(const KScene& S, const float* planes, const uint8_t* rank_lut, const Ray& r, V3 inv,
-                            float t_min, float t_max, int& hitEntry, float& hitT, Frames& fr, Counters& cnt) {
+                            float t_min, float t_max, int& hitEntry, float& hitT, Frames& fr, Counters& cnt,
+                            Ray* walked = nullptr) {
     FastStateT<Masks> st;
-    if (!fast_begin(S, planes, rank_lut, r, inv, t_min, t_max, st)) return false;
-    while (!fast_step<COUNT>(S, rank_lut, st, fr, cnt)) {
-    }
+    const bool in = fast_begin(S, planes, rank_lut, r, inv, t_min, t_max, st);
+    if (in)
+        while (!fast_step<COUNT>(S, rank_lut, st, fr, cnt)) {
+        }
+    // the ray back from the walk state (bit-identical to r; no extra registers across the walk)
+    if (walked) *walked = st.ray();
+    if (!in) return false;
     hitEntry = st.hitEntry;
     hitT = st.closest;
     return st.hit();
