@@ -341,11 +341,11 @@ __device__ inline void shade_direct(const PipeArgs& A, int k, ort::Ray ray, ort_
     (void)ort::shade_bounce(hit, rec, ray, c, importance, st);
     const ort::V3 v = ort::finish_pixel(ort::add(ort::mk(0.0f, 0.0f, 0.0f), c), 1);
     float* o = A.out + 3 * ((size_t)row * A.tm.tw + col);
-    // the frame is written once and never read here: non-temporal stores keep its 12 B/pixel
-    // from evicting scene lines out of L2 and the Infinity Cache
-    __builtin_nontemporal_store(v.x, o + 0);
-    __builtin_nontemporal_store(v.y, o + 1);
-    __builtin_nontemporal_store(v.z, o + 2);
+    // plain stores (one global_store_dwordx3): non-temporal ones ran no faster and, their
+    // partial 64-byte lines written out unmerged, moved 1.38x the frame's bytes (PMC WRITE_SIZE)
+    o[0] = v.x;
+    o[1] = v.y;
+    o[2] = v.z;
 }
 // Tile rows past the frame (band padding) are written as zeros, as the shade kernel does.
 __device__ inline void shade_direct_padding(const PipeArgs& A, int k) {
