@@ -338,7 +338,7 @@ __device__ inline void shade_direct(const PipeArgs& A, int k, ort::Ray ray, ort_
     float importance = 1.0f;
     ort::HitRec rec;
     if (hit) rec = ort::hit_record<0>(A.S, ray, t, entry);
-    (void)ort::shade_bounce(hit, rec, ray, c, importance, st);
+    (void)ort::shade_bounce<true>(hit, rec, ray, c, importance, st);  // 1 sample, 1 bounce: final
     const ort::V3 v = ort::finish_pixel(ort::add(ort::mk(0.0f, 0.0f, 0.0f), c), 1);
     float* o = A.out + 3 * ((size_t)row * A.tm.tw + col);
     // plain stores (one global_store_dwordx3): non-temporal ones ran no faster and, their
@@ -779,7 +779,10 @@ __global__ void __launch_bounds__(kBlock) ort_shade_kernel(PipeArgs A) {
         const int2 h = A.hit[k];
         ort::HitRec rec;
         if (h.x >= 0) rec = ort::hit_record<MODE>(A.S, ray, __int_as_float(h.y), h.x);
-        done = ort::shade_bounce(h.x >= 0, rec, ray, c, importance, st);
+        if (A.last && A.sample == A.pp.ns - 1)  // nothing reads the ray or RNG state after this bounce
+            done = ort::shade_bounce<true>(h.x >= 0, rec, ray, c, importance, st);
+        else
+            done = ort::shade_bounce(h.x >= 0, rec, ray, c, importance, st);
         if (!done && (A.last || importance < 0.01f)) done = true;  // loop bound / glsl:605
     }
     if constexpr (DIRECT) {

@@ -1006,8 +1006,18 @@ ORT_FN float schlick(float cosine, float ri) {
 }
 
 // Material_bsdf (glsl:525-589)
+// FINAL: nothing after this bounce reads the scattered ray or the RNG state (last bounce of
+// the last sample), so only what reaches the pixel is computed: Lambert and dielectric
+// attenuations do not depend on the sampled direction (their sampling is skipped); metal
+// still samples, its absorption test needs the direction.
+template <bool FINAL = false>
 ORT_FN bool bsdf(const HitRec& h, const Ray& wo, Ray& wi, V3& att, ort_rng& st) {
     wi.o = h.point;
+    if (FINAL && (h.mat == 0 || h.mat == 2)) {
+        att = h.mat == 0 ? h.albedo : mk(1.0f, 1.0f, 1.0f);
+        wi.d = wo.d;
+        return true;
+    }
     switch (h.mat) {
         case 0: {
             const V3 ld = random_cosine_direction(st);
@@ -1173,12 +1183,13 @@ ORT_FN HitRec hit_record(const KScene& S, const Ray& r, float t, int entry) {
 
 // One iteration of radiance()'s bounce loop after intersectScene (glsl:607-627).
 // Returns true when the path ends here (absorbed, or escaped to the sky).
+template <bool FINAL = false>
 ORT_FN bool shade_bounce(bool hit, const HitRec& h, Ray& ray, V3& c, float& importance, ort_rng& st) {
     if (hit) {
         Ray wi;
         wi.d = ray.d;
         V3 att = mk(0.0f, 0.0f, 0.0f);
-        const bool scattered = bsdf(h, ray, wi, att, st);
+        const bool scattered = bsdf<FINAL>(h, ray, wi, att, st);
         ray.o = wi.o;
         ray.d = wi.d;
         if (!scattered) {
@@ -1220,7 +1231,10 @@ ORT_FN V3 shade_pixel(const PixelParams& P, const KScene& S, const float* planes
             const int tr = trace_ray<MODE, COUNT>(S, planes, rank_lut, ray, false, t, entry, fr, snode, stmin, cnt);
             HitRec h;
             if (tr == ORT_TRACE_HIT) h = hit_record<MODE>(S, ray, t, entry);
-            if (shade_bounce(tr == ORT_TRACE_HIT, h, ray, c, importance, st)) break;
+            const bool hit = tr == ORT_TRACE_HIT;
+            const bool fin = b == P.maxDepth - 1 && s == P.ns - 1;  // the RNG state is dead after it
+            if (fin ? shade_bounce<true>(hit, h, ray, c, importance, st) : shade_bounce(hit, h, ray, c, importance, st))
+                break;
         }
         col = add(col, c);
     }
