@@ -105,20 +105,23 @@ __device__ inline LdsView lds_view(unsigned char* smem, int D) {
     v.fr.lane = threadIdx.x;
     return v;
 }
+// The plane tables and rank LUT are the same for every workgroup of a scene: k_lds_image
+// builds them once per scene (ort_ctx::lds_img) and each workgroup copies the image in
+// 16-byte pieces -- building them per workgroup (an integer division per plane entry, ~80
+// VALU per LUT byte) cost as much VALU as several walk steps of every wave.
+__global__ void __launch_bounds__(kBlock) k_lds_image(const float* planes, int D, unsigned char* img) {
+    const int tid = threadIdx.x;
+    ort::fill_fast_planes(planes, reinterpret_cast<float*>(img), D, tid, kBlock);  // forward, then reversed
+    uint8_t* lut = img + align16(sizeof(float) * (size_t)ort::fast_plane_floats(D));
+    for (int i = tid; i < (int)kRankLutBytes; i += kBlock) lut[i] = ort::rank_lut_entry((uint32_t)i >> 8, (uint32_t)i & 255u);
+}
 template <bool WITH_LUT>
 __device__ inline LdsView setup_lds(unsigned char* smem, const ort::KScene& S) {
-    const int tid = threadIdx.x;
-    const int D = S.depth;
-    const int np = ort::fast_plane_floats(D);
-    float* lp = reinterpret_cast<float*>(smem);
-    ort::fill_fast_planes(S.planes, lp, D, tid, kBlock);  // forward tables, then reversed
-    const size_t poff = align16(sizeof(float) * (size_t)np);
-    uint8_t* lut = smem + poff;
-    if (WITH_LUT)
-        for (int i = tid; i < (int)kRankLutBytes; i += kBlock)
-            lut[i] = ort::rank_lut_entry((uint32_t)i >> 8, (uint32_t)i & 255u);
+    const int n16 = WITH_LUT ? S.lds_img_n16 : S.lds_img_p16;
+    uint4* dst = reinterpret_cast<uint4*>(smem);
+    for (int i = threadIdx.x; i < n16; i += kBlock) dst[i] = S.lds_img[i];
     __syncthreads();
-    return lds_view<WITH_LUT>(smem, D);
+    return lds_view<WITH_LUT>(smem, S.depth);
 }
 
 // Tile (bx, by) of 16x16 pixels rendered by workgroup blk.  The dispatcher deals workgroup b
@@ -866,6 +869,7 @@ struct ort_ctx {
     int64_t n_indices = 0;
     DevBuf sph_cr, sph_ma, sph_fr;
     DevBuf node, leaf_sph, leaf_idx, planes;    // compact
+    DevBuf lds_img;                              // compact: the workgroup LDS image (k_lds_image)
     DevBuf nodeA, nodeB, cnt, indices;           // explicit
     DevBuf scratch_out, counters;
     // wavefront pipeline state, sized for the largest tile rendered so far
@@ -901,7 +905,7 @@ void free_buf(DevBuf& b) {
 
 void free_scene(ort_ctx* c) {
     DevBuf* all[] = {&c->sph_cr, &c->sph_ma, &c->sph_fr, &c->node, &c->leaf_sph, &c->leaf_idx,
-                     &c->planes, &c->nodeA, &c->nodeB, &c->cnt, &c->indices};
+                     &c->planes, &c->lds_img, &c->nodeA, &c->nodeB, &c->cnt, &c->indices};
     for (DevBuf* b : all) free_buf(*b);
     ort::freeGpuTree(c->tree);
     c->has_scene = false;
@@ -913,6 +917,17 @@ int upload(ort_ctx* ctx, DevBuf& b, const void* src, size_t bytes) {
     HIPCHK(ctx, hipMalloc(&b.p, bytes));
     b.bytes = bytes;
     if (src) HIPCHK(ctx, hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+    return ORT_OK;
+}
+
+// The compact layout's workgroup LDS image (plane tables | rank LUT) from ctx->planes.
+int build_lds_image(ort_ctx* ctx) {
+    const size_t bytes = align16(sizeof(float) * (size_t)ort::fast_plane_floats(ctx->depth)) + kRankLutBytes;
+    int rc;
+    if ((rc = upload(ctx, ctx->lds_img, nullptr, bytes))) return rc;
+    hipLaunchKernelGGL(k_lds_image, dim3(1), dim3(kBlock), 0, ctx->stream, (const float*)ctx->planes.p, ctx->depth,
+                       (unsigned char*)ctx->lds_img.p);
+    HIPCHK(ctx, hipGetLastError());
     return ORT_OK;
 }
 
@@ -990,6 +1005,10 @@ int build_impl(ort_ctx* ctx, const float* cr, const float* ma, const float* fr, 
         ctx->leaf_sph = {cd.leaf_sph, cd.leaf_bytes};
         ctx->leaf_idx = {cd.leaf_idx, cd.idx_bytes};
         ctx->planes = {cd.planes, cd.plane_bytes};
+        if ((rc = build_lds_image(ctx))) {
+            ort::freeGpuTree(t);
+            return rc;
+        }
     } else {
         if (ctx->force_layout == ORT_LAYOUT_COMPACT) {
             ort::freeGpuTree(t);
@@ -1042,6 +1061,7 @@ int upload_impl(ort_ctx* ctx, const ort::SceneInput& in) {
             if ((rc = upload(ctx, ctx->leaf_sph, cl.leaf_sph.data(), 4 * cl.leaf_sph.size()))) return rc;
             if ((rc = upload(ctx, ctx->leaf_idx, cl.leaf_idx.data(), 4 * cl.leaf_idx.size()))) return rc;
             if ((rc = upload(ctx, ctx->planes, cl.planes.data(), 4 * cl.planes.size()))) return rc;
+            if ((rc = build_lds_image(ctx))) return rc;
             HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
         } else {
             const int d = ort::treeDepth(in);
@@ -1082,6 +1102,9 @@ ort::KScene device_scene(const ort_ctx* c) {
     S.leaf_bytes = (uint32_t)c->leaf_sph.bytes;
     S.leaf_idx = (const int*)c->leaf_idx.p;
     S.planes = (const float*)c->planes.p;
+    S.lds_img = (const uint4*)c->lds_img.p;
+    S.lds_img_p16 = (int)(align16(sizeof(float) * (size_t)ort::fast_plane_floats(c->depth)) / 16);
+    S.lds_img_n16 = S.lds_img_p16 + (int)(kRankLutBytes / 16);
     S.depth = c->depth;
     S.nodeA = (const float4*)c->nodeA.p;
     S.nodeB = (const float4*)c->nodeB.p;
@@ -1528,7 +1551,7 @@ int ort_scene_get_info(const ort_ctx* ctx, ort_scene_info* info) {
     info->layout = ctx->layout;
     info->tree_depth = ctx->depth;
     const DevBuf* all[] = {&ctx->sph_cr, &ctx->sph_ma, &ctx->sph_fr, &ctx->node, &ctx->leaf_sph, &ctx->leaf_idx,
-                           &ctx->planes, &ctx->nodeA, &ctx->nodeB, &ctx->cnt, &ctx->indices};
+                           &ctx->planes, &ctx->lds_img, &ctx->nodeA, &ctx->nodeB, &ctx->cnt, &ctx->indices};
     int64_t b = 0;
     for (const DevBuf* d : all) b += (int64_t)d->bytes;
     info->device_bytes = b;

@@ -92,6 +92,9 @@ struct KScene {
     const float4* leaf_sph;  // per objectIndices entry: the sphere's center.xyz, radius
     const int* leaf_idx;     // per entry: sphere index (= objectIndices)
     const float* planes;     // 3 x (2^depth + 1) split-plane coordinates (global copy)
+    const uint4* lds_img;    // the workgroup LDS image (fast plane tables | rank LUT), built once
+    int lds_img_n16;         // per scene; its size in 16-byte chunks (planes part: lds_img_p16)
+    int lds_img_p16;
     int depth;               // tree depth D (root = 0)
     uint32_t node_bytes;     // buffer sizes for the range-checked buffer loads (< 2^32)
     uint32_t leaf_bytes;
