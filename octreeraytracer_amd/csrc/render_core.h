@@ -687,9 +687,8 @@ ORT_FN bool fast_begin(const KScene& S, const float* planes, const uint8_t* rank
         st.sB = gB ? -4 : 4;
         st.sC = gC ? -4 : 4;
     }
-    uint32_t ot = 0;
-    for (uint32_t k = 0; k < 8; ++k) ot |= rank_perm(k, m) << (4 * k);
-    st.otab = ot;
+    // nibble k = rank_perm(k, m): the identity (or, swap, bits 0/1 exchanged) XOR m per nibble
+    st.otab = (swap ? 0x75643120u : 0x76543210u) ^ (m * 0x11111111u);
     st.tNA = st.iA * (st.plA(0) - st.oA);
     st.tFA = st.iA * (st.plA(top) - st.oA);
     st.tNB = st.iB * (st.plB(0) - st.oB);
@@ -776,9 +775,11 @@ ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks
                 const uint2 lrec = fetch_node(S, co + (int)((st.otab >> (4 * R)) & 15u));
                 if (COUNT) cnt.v[0] += 1;
                 const float eA = (R & 2u) ? tMA : tNA, eB = (R & 1u) ? tMB : tNB, eC = (R & 4u) ? tMC : tNC;
-                if (leaf_tests<COUNT>(S, st, (int)lrec.x, (int)lrec.y, fmax_tmin(fmax3(eA, eB, eC)), cnt))
-                    return true;  // glsl:336
+                // a hit ends the walk after this leaf (glsl:336): no later sibling is tested
+                const bool h = leaf_tests<COUNT>(S, st, (int)lrec.x, (int)lrec.y, fmax_tmin(fmax3(eA, eB, eC)), cnt);
+                todo = h ? 0u : todo;
             }
+            if (st.hit()) return true;
         } else {
             // level depth holds nothing yet (every deeper level is empty), so both writes are
             // harmless when no child survives
