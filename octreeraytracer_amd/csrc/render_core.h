@@ -487,11 +487,14 @@ ORT_FN bool sphere_hit_fast(const Ray& r, float a, float ya, float4 sp, float t_
     const float c = dot(oc, oc) - sp.w * sp.w;
     const float disc = half_b * half_b - a * c;
     if (disc > 0.0f) {
+        // both roots, no branch between them: the near one if in range, else the far one
         const float sq = qsqrt(disc);
-        float temp = qdiv(-half_b - sq, a, ya);
-        if (temp < t_max && temp > t_min) { t = temp; return true; }
-        temp = qdiv(-half_b + sq, a, ya);
-        if (temp < t_max && temp > t_min) { t = temp; return true; }
+        const float t1 = qdiv(-half_b - sq, a, ya);
+        const float t2 = qdiv(-half_b + sq, a, ya);
+        const bool ok1 = t1 < t_max && t1 > t_min;
+        const bool ok2 = t2 < t_max && t2 > t_min;
+        t = ok1 ? t1 : t2;
+        return ok1 || ok2;
     }
     return false;
 }
