@@ -240,7 +240,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ORT
     const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     ort::Counters cnt;
     for (int q = 0; q < 6; ++q) cnt.v[q] = 0;
-    ort::FastState st;
+    ort::FastStateT<ort::Masks96Lean> st;  // lean state: no cached near-plane pointers
     int k = -1;
     int next = 0, end = 0;   // wave-uniform: remaining work items [next, end) of the wave's chunk
     bool drained = false;    // wave-uniform: the global cursor passed the item count

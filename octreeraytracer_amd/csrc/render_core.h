@@ -550,6 +550,7 @@ struct Masks64 {  // levels 0..7: trees of depth <= 8
     // depth <= 8 trees (all leaves at the bottom level with maxSpheresPerNode 0), not deeper
     static constexpr bool kInlineLeaves = true;
     static constexpr bool kRevPlanes = true;  // depth <= 8: reversed plane tables (fast_rev_planes)
+    static constexpr bool kKeepNear = true;   // keep the node's near-plane pointers (FastStateT::nA..)
     uint64_t m;
     ORT_FN void clear() { m = 0; }
     ORT_FN bool empty() const { return m == 0; }
@@ -576,6 +577,7 @@ struct Masks64 {  // levels 0..7: trees of depth <= 8
 struct Masks96 {  // levels 0..11
     static constexpr bool kInlineLeaves = false;
     static constexpr bool kRevPlanes = false;
+    static constexpr bool kKeepNear = true;
     uint64_t lo;
     uint32_t hi;
     ORT_FN void clear() { lo = 0; hi = 0; }
@@ -641,6 +643,13 @@ struct FastStateT {
     ORT_FN float pl(const float* p, int s, int idx) const {
         return Masks::kRevPlanes ? p[idx] : *(const float*)((const char*)p + imul24(s, idx));
     }
+    // near planes of the current node (set by the pop): its mid plane is h steps further
+    const float* nA;
+    const float* nB;
+    const float* nC;
+    ORT_FN const float* at(const float* p, int s, int idx) const {
+        return Masks::kRevPlanes ? p + idx : (const float*)((const char*)p + imul24(s, idx));
+    }
     ORT_FN float plA(int idx) const { return pl(pA, sA, idx); }
     ORT_FN float plB(int idx) const { return pl(pB, sB, idx); }
     ORT_FN float plC(int idx) const { return pl(pC, sC, idx); }
@@ -656,6 +665,11 @@ struct FastStateT {
     }
 };
 using FastState = FastStateT<Masks96>;
+// The persistent kernel keeps a lane's state across refills; there three more registers for
+// the near-plane pointers cost occupancy, so it re-derives them from cP.
+struct Masks96Lean : Masks96 {
+    static constexpr bool kKeepNear = false;
+};
 
 // Root test and state setup (glsl:296-311).  Returns false when the root box is missed.
 template <class Masks>
@@ -699,6 +713,11 @@ ORT_FN bool fast_begin(const KScene& S, const float* planes, const uint8_t* rank
     st.tNC = st.iC * (st.plC(0) - st.oC);
     st.tFC = st.iC * (st.plC(top) - st.oC);
     st.cP = 0;
+    if (Masks::kKeepNear) {
+        st.nA = st.pA;
+        st.nB = st.pB;
+        st.nC = st.pC;
+    }
     st.node = 0;
     st.rec = fetch_node(S, 0);
     st.depth = 0;
@@ -742,9 +761,12 @@ ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks
         }
         const uint32_t rcm = rank_lut[((st.otab & 7u) << 8) | (rec.y & 0xffu)];  // LUT row m
         const int h = 1 << (D - 1 - st.depth);  // half the node's width, in plane steps
-        const float tMA = st.iA * (st.plA(st.cA() + h) - st.oA);
-        const float tMB = st.iB * (st.plB(st.cB() + h) - st.oB);
-        const float tMC = st.iC * (st.plC(st.cC() + h) - st.oC);
+        const float* nA = Masks::kKeepNear ? st.nA : st.at(st.pA, st.sA, st.cA());
+        const float* nB = Masks::kKeepNear ? st.nB : st.at(st.pB, st.sB, st.cB());
+        const float* nC = Masks::kKeepNear ? st.nC : st.at(st.pC, st.sC, st.cC());
+        const float tMA = st.iA * (*st.at(nA, st.sA, h) - st.oA);
+        const float tMB = st.iB * (*st.at(nB, st.sB, h) - st.oB);
+        const float tMC = st.iC * (*st.at(nC, st.sC, h) - st.oC);
         const float tNA = st.tNA, tNB = st.tNB, tNC = st.tNC, tFA = st.tFA, tFB = st.tFB, tFC = st.tFC;
         // child R enters at max3 of its axis entries (near half: tN, far half: tM) and exits at
         // min3 of its exits (tM / tF); t_min and t_max are folded into the C axis.
@@ -820,13 +842,20 @@ ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks
     st.depth = L + 1;
     st.node = fr.getCo(L) + (int)((st.otab >> (4 * rk)) & 15u);
     st.rec = fetch_node(S, st.node);
-    const int cA = st.cA(), cB = st.cB(), cC = st.cC();
-    st.tNA = st.iA * (st.plA(cA) - st.oA);
-    st.tFA = st.iA * (st.plA(cA + w) - st.oA);
-    st.tNB = st.iB * (st.plB(cB) - st.oB);
-    st.tFB = st.iB * (st.plB(cB + w) - st.oB);
-    st.tNC = st.iC * (st.plC(cC) - st.oC);
-    st.tFC = st.iC * (st.plC(cC + w) - st.oC);
+    const float* nA = st.at(st.pA, st.sA, st.cA());
+    const float* nB = st.at(st.pB, st.sB, st.cB());
+    const float* nC = st.at(st.pC, st.sC, st.cC());
+    if (Masks::kKeepNear) {
+        st.nA = nA;
+        st.nB = nB;
+        st.nC = nC;
+    }
+    st.tNA = st.iA * (nA[0] - st.oA);
+    st.tFA = st.iA * (*st.at(nA, st.sA, w) - st.oA);
+    st.tNB = st.iB * (nB[0] - st.oB);
+    st.tFB = st.iB * (*st.at(nB, st.sB, w) - st.oB);
+    st.tNC = st.iC * (nC[0] - st.oC);
+    st.tFC = st.iC * (*st.at(nC, st.sC, w) - st.oC);
     return false;
 }
 
