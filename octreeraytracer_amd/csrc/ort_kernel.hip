@@ -539,13 +539,13 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ORT
             // ---- packet walk: every lane of the wave executes this block ----
             const int D = S.depth;
             const int top = 1 << D;
-            const int P1 = top + 1;
             const bool swap = (m >> 1) & 1u;
             const uint32_t gA = swap ? (m & 1u) : ((m >> 1) & 1u), gB = swap ? ((m >> 1) & 1u) : (m & 1u),
                            gC = (m >> 2) & 1u;
-            const float* pA = LV.planes + (swap ? P1 : 0) + (gA ? top : 0);
-            const float* pB = LV.planes + (swap ? 0 : P1) + (gB ? top : 0);
-            const float* pC = LV.planes + 2 * P1 + (gC ? top : 0);
+            const int S1 = ort::fast_axis_floats(D);  // forward tables at a * S1 (fill_fast_planes)
+            const float* pA = LV.planes + (swap ? S1 : 0) + (gA ? top : 0);
+            const float* pB = LV.planes + (swap ? 0 : S1) + (gB ? top : 0);
+            const float* pC = LV.planes + 2 * S1 + (gC ? top : 0);
             const int sA = gA ? -1 : 1, sB = gB ? -1 : 1, sC = gC ? -1 : 1;
             uint32_t otab = 0;
             for (uint32_t r = 0; r < 8; ++r) otab |= ort::rank_perm(r, m) << (4 * r);

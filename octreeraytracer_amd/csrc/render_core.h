@@ -233,6 +233,32 @@ struct LevelMasks {
     }
 };
 
+// The fast walk's split-plane tables.  Trees of depth <= 8: per axis a a 3 KiB block at
+// byte 3072 a -- the layout's forward table (entry i = plane i) at its start and the same
+// table reversed (entry i = plane 2^D - i) 1 KiB further -- so that a ray walking an axis
+// downwards indexes its planes upwards like every other ray (no per-ray stride), and every
+// table starts at a multiple of 1024 bytes: a node's near plane (index < 256) is then a byte
+// offset whose low 10 bits are the index, and the pop moves it to a child's with one
+// and/or (fast_step).  At depth 8 the forward table's last entry is the reversed one's first
+// (the same plane), and the reversed table's last sits at byte 2048 of the block.  Deeper
+// trees keep the forward tables only, back to back (the reversed copies would cost LDS
+// occupancy), and a +-4 byte stride per axis.
+ORT_FN bool fast_rev_planes(int depth) { return depth <= 8; }
+ORT_FN int fast_axis_floats(int depth) { return fast_rev_planes(depth) ? 768 : (1 << depth) + 1; }
+ORT_FN int fast_plane_floats(int depth) { return 3 * fast_axis_floats(depth); }
+ORT_FN void fill_fast_planes(const float* fwd, float* out, int depth, int i0 = 0, int step = 1) {
+    const int P1 = (1 << depth) + 1;
+    const int S = fast_axis_floats(depth);
+    const bool rev = fast_rev_planes(depth);
+    for (int o = i0; o < 3 * S; o += step) {  // gather form: one writer per entry
+        const int a = o / S, r = o - a * S;
+        float v = 0.0f;  // the gaps: never read
+        if (r < P1) v = fwd[a * P1 + r];
+        else if (rev && r >= 256 && r - 256 < P1) v = fwd[a * P1 + (P1 - 1 - (r - 256))];
+        out[o] = v;
+    }
+}
+
 // Child-box entry t of octant `oct` for a node at depth `dep` with cell (cx,cy,cz):
 // recomputes the reference's rayBoxIntersection for that child (tmin only + hit flag).
 ORT_FN float plane_t(float inv, float p, float o) { return inv * (p - o); }
@@ -241,10 +267,10 @@ template <bool COUNT, class Frames>
 ORT_FN bool traverse_compact(const KScene& S, const float* planes, const Ray& r, float t_min, float t_max,
                              int& hitEntry, float& hitT, Frames& fr, Counters& cnt) {
     const int D = S.depth;
-    const int P1 = (1 << D) + 1;
+    const int S1 = fast_axis_floats(D);  // fast_plane_floats layout: forward tables at a * S1
     const float* PX = planes;
-    const float* PY = planes + P1;
-    const float* PZ = planes + 2 * P1;
+    const float* PY = planes + S1;
+    const float* PZ = planes + 2 * S1;
     const V3 inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
     const float a = dot(r.d, r.d);
     {
@@ -524,26 +550,6 @@ ORT_FN float4 fetch_sphere(const KScene& S, int e) {
 // Plane idx of a ray-order table (base[idx]; see fast_begin for the reversed copies).
 ORT_FN float plane_at(const float* base, int idx) { return base[idx]; }
 
-// For trees of depth <= 8 the fast walk reads its split planes from a table of
-// 6 * (2^D + 1) floats: the layout's three axis tables (axis a at a * P1) followed by the
-// same three reversed (axis a at 3 * P1 + a * P1, entry i = forward entry 2^D - i), so that
-// a ray walking an axis downwards indexes its planes upwards like every other ray -- no
-// per-ray stride register.  Deeper trees keep the forward tables only (the reversed copies
-// would cost LDS occupancy) and a +-4 byte stride per axis.
-ORT_FN bool fast_rev_planes(int depth) { return depth <= 8; }
-ORT_FN int fast_plane_floats(int depth) { return (fast_rev_planes(depth) ? 6 : 3) * ((1 << depth) + 1); }
-ORT_FN void fill_fast_planes(const float* fwd, float* out, int depth, int i0 = 0, int step = 1) {
-    const int P1 = (1 << depth) + 1;
-    const bool rev = fast_rev_planes(depth);
-    for (int i = i0; i < 3 * P1; i += step) {
-        out[i] = fwd[i];
-        if (rev) {
-            const int a = i / P1, j = i - a * P1;
-            out[3 * P1 + a * P1 + (P1 - 1 - j)] = fwd[i];
-        }
-    }
-}
-
 // Rank-reversed level masks (see above).  pop() returns hb = 8L + 7 - rank.
 struct Masks64 {  // levels 0..7: trees of depth <= 8
     // test the leaf children of a LEAFKIDS node inline (fast_step); pays for its registers on
@@ -626,12 +632,18 @@ struct FastStateT {
     V3 d;            // original-axis direction (Sphere_hit)
     float ya;        // RN(1 / dot(d, d))
     float oA, oB, oC, iA, iB, iC;  // role-axis origin / 1/d
-    const float* pA;  // ray-order plane table of each role axis: plane(i) = pA[i] (kRevPlanes)
-    const float* pB;  // or *(pA + sA * i bytes)
+    // kRevPlanes (depth <= 8): byte offsets from pl0 of the current node's near plane per role
+    // axis (table start, a multiple of 1024, + 4 * index; see fast_axis_floats)
+    const float* pl0;
+    uint32_t aA, aB, aC;
+    ORT_FN float plane(uint32_t off) const { return *(const float*)((const char*)pl0 + off); }
+    // otherwise: the ray-order plane table of each role axis, plane(i) = *(pA + sA * i bytes)
+    const float* pA;
+    const float* pB;
     const float* pC;
-    int sA, sB, sC;   // +-4 (only without kRevPlanes)
+    int sA, sB, sC;   // +-4
     float tNA, tFA, tNB, tFB, tNC, tFC;  // near/far plane t of the current node's box
-    uint32_t cP;     // ray-order index of the current node's near plane, 10 bits per axis (A, B, C)
+    uint32_t cP;     // (not kRevPlanes) ray-order index of the current node's near plane, 10 bits per axis
     uint32_t otab;   // nibble r = octant of rank r; nibble 0 = m
     int node, depth;
     uint2 rec;       // node record of `node`, loaded as soon as the pop knows it (its latency
@@ -677,7 +689,6 @@ ORT_FN bool fast_begin(const KScene& S, const float* planes, const uint8_t* rank
                        float t_max, FastStateT<Masks>& st) {
     const int D = S.depth;
     const int top = 1 << D;
-    const int P1 = top + 1;
     const uint32_t nx = r.d.x < 0.0f, ny = r.d.y < 0.0f, nz = r.d.z < 0.0f;
     const uint32_t m = (nz << 2) | (nx << 1) | ny;
     const bool swap = nx != 0;
@@ -690,33 +701,41 @@ ORT_FN bool fast_begin(const KScene& S, const float* planes, const uint8_t* rank
     st.iA = swap ? inv.y : inv.x;
     st.iB = swap ? inv.x : inv.y;
     st.iC = inv.z;
+    // nibble k = rank_perm(k, m): the identity (or, swap, bits 0/1 exchanged) XOR m per nibble
+    st.otab = (swap ? 0x75643120u : 0x76543210u) ^ (m * 0x11111111u);
     // planes: fast_plane_floats(D) floats (fill_fast_planes)
-    if (Masks::kRevPlanes) {  // forward tables, then reversed
-        st.pA = planes + (gA ? 3 * P1 : 0) + (swap ? P1 : 0);
-        st.pB = planes + (gB ? 3 * P1 : 0) + (swap ? 0 : P1);
-        st.pC = planes + (gC ? 3 * P1 : 0) + 2 * P1;
-        st.sA = st.sB = st.sC = 4;
+    if (Masks::kRevPlanes) {  // per axis: forward table, reversed one 1 KiB further
+        st.pl0 = planes;
+        st.aA = 4u * ((swap ? 768u : 0u) + (gA ? 256u : 0u));
+        st.aB = 4u * ((swap ? 0u : 768u) + (gB ? 256u : 0u));
+        st.aC = 4u * (1536u + (gC ? 256u : 0u));
+        const uint32_t t4 = 4u * (uint32_t)top;
+        st.tNA = st.iA * (st.plane(st.aA) - st.oA);
+        st.tFA = st.iA * (st.plane(st.aA + t4) - st.oA);
+        st.tNB = st.iB * (st.plane(st.aB) - st.oB);
+        st.tFB = st.iB * (st.plane(st.aB + t4) - st.oB);
+        st.tNC = st.iC * (st.plane(st.aC) - st.oC);
+        st.tFC = st.iC * (st.plane(st.aC + t4) - st.oC);
     } else {
-        st.pA = planes + (swap ? P1 : 0) + (gA ? top : 0);
-        st.pB = planes + (swap ? 0 : P1) + (gB ? top : 0);
-        st.pC = planes + 2 * P1 + (gC ? top : 0);
+        const int S1 = fast_axis_floats(D);
+        st.pA = planes + (swap ? S1 : 0) + (gA ? top : 0);
+        st.pB = planes + (swap ? 0 : S1) + (gB ? top : 0);
+        st.pC = planes + 2 * S1 + (gC ? top : 0);
         st.sA = gA ? -4 : 4;
         st.sB = gB ? -4 : 4;
         st.sC = gC ? -4 : 4;
-    }
-    // nibble k = rank_perm(k, m): the identity (or, swap, bits 0/1 exchanged) XOR m per nibble
-    st.otab = (swap ? 0x75643120u : 0x76543210u) ^ (m * 0x11111111u);
-    st.tNA = st.iA * (st.plA(0) - st.oA);
-    st.tFA = st.iA * (st.plA(top) - st.oA);
-    st.tNB = st.iB * (st.plB(0) - st.oB);
-    st.tFB = st.iB * (st.plB(top) - st.oB);
-    st.tNC = st.iC * (st.plC(0) - st.oC);
-    st.tFC = st.iC * (st.plC(top) - st.oC);
-    st.cP = 0;
-    if (Masks::kKeepNear) {
-        st.nA = st.pA;
-        st.nB = st.pB;
-        st.nC = st.pC;
+        st.tNA = st.iA * (st.plA(0) - st.oA);
+        st.tFA = st.iA * (st.plA(top) - st.oA);
+        st.tNB = st.iB * (st.plB(0) - st.oB);
+        st.tFB = st.iB * (st.plB(top) - st.oB);
+        st.tNC = st.iC * (st.plC(0) - st.oC);
+        st.tFC = st.iC * (st.plC(top) - st.oC);
+        st.cP = 0;
+        if (Masks::kKeepNear) {
+            st.nA = st.pA;
+            st.nB = st.pB;
+            st.nC = st.pC;
+        }
     }
     st.node = 0;
     st.rec = fetch_node(S, 0);
@@ -761,12 +780,20 @@ ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks
         }
         const uint32_t rcm = rank_lut[((st.otab & 7u) << 8) | (rec.y & 0xffu)];  // LUT row m
         const int h = 1 << (D - 1 - st.depth);  // half the node's width, in plane steps
-        const float* nA = Masks::kKeepNear ? st.nA : st.at(st.pA, st.sA, st.cA());
-        const float* nB = Masks::kKeepNear ? st.nB : st.at(st.pB, st.sB, st.cB());
-        const float* nC = Masks::kKeepNear ? st.nC : st.at(st.pC, st.sC, st.cC());
-        const float tMA = st.iA * (*st.at(nA, st.sA, h) - st.oA);
-        const float tMB = st.iB * (*st.at(nB, st.sB, h) - st.oB);
-        const float tMC = st.iC * (*st.at(nC, st.sC, h) - st.oC);
+        float tMA, tMB, tMC;
+        if (Masks::kRevPlanes) {
+            const uint32_t h4 = 4u * (uint32_t)h;
+            tMA = st.iA * (st.plane(st.aA + h4) - st.oA);
+            tMB = st.iB * (st.plane(st.aB + h4) - st.oB);
+            tMC = st.iC * (st.plane(st.aC + h4) - st.oC);
+        } else {
+            const float* nA = Masks::kKeepNear ? st.nA : st.at(st.pA, st.sA, st.cA());
+            const float* nB = Masks::kKeepNear ? st.nB : st.at(st.pB, st.sB, st.cB());
+            const float* nC = Masks::kKeepNear ? st.nC : st.at(st.pC, st.sC, st.cC());
+            tMA = st.iA * (*st.at(nA, st.sA, h) - st.oA);
+            tMB = st.iB * (*st.at(nB, st.sB, h) - st.oB);
+            tMC = st.iC * (*st.at(nC, st.sC, h) - st.oC);
+        }
         const float tNA = st.tNA, tNB = st.tNB, tNC = st.tNC, tFA = st.tFA, tFB = st.tFB, tFC = st.tFC;
         // child R enters at max3 of its axis entries (near half: tN, far half: tM) and exits at
         // min3 of its exits (tM / tF); t_min and t_max are folded into the C axis.
@@ -833,29 +860,47 @@ ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks
     const int L = hb >> 3;
     const uint32_t rk = (uint32_t)(~hb) & 7u;
     const int w = 1 << (D - 1 - L);  // child width in plane steps
-    const int keep = -2 * w;         // clears the offsets below the level-L ancestor
-    {   // per 10-bit field: (c & keep) | (axis bit of rk ? w : 0)
-        const uint32_t k3 = ((uint32_t)keep & 1023u) * 0x100401u;
-        const uint32_t bits = ((rk >> 1) & 1u) | ((rk & 1u) << 10) | (((rk >> 2) & 1u) << 20);
-        st.cP = (st.cP & k3) | bits * (uint32_t)w;
-    }
     st.depth = L + 1;
     st.node = fr.getCo(L) + (int)((st.otab >> (4 * rk)) & 15u);
     st.rec = fetch_node(S, st.node);
-    const float* nA = st.at(st.pA, st.sA, st.cA());
-    const float* nB = st.at(st.pB, st.sB, st.cB());
-    const float* nC = st.at(st.pC, st.sC, st.cC());
-    if (Masks::kKeepNear) {
-        st.nA = nA;
-        st.nB = nB;
-        st.nC = nC;
+    if (Masks::kRevPlanes) {
+        // near plane of the level-(L+1) child: the level-L ancestor's (offset bits below 8w
+        // cleared; the table start is a multiple of 1024 > 8w) plus w planes on the axes
+        // where the child is the far half
+        const uint32_t w4 = 4u << (D - 1 - L);
+        const uint32_t m8 = ~(2u * w4 - 1u);
+        const uint32_t s = (uint32_t)(D + 1 - L);  // log2(w4)
+        st.aA = (st.aA & m8) | (((rk >> 1) & 1u) << s);
+        st.aB = (st.aB & m8) | ((rk & 1u) << s);
+        st.aC = (st.aC & m8) | (((rk >> 2) & 1u) << s);
+        st.tNA = st.iA * (st.plane(st.aA) - st.oA);
+        st.tFA = st.iA * (st.plane(st.aA + w4) - st.oA);
+        st.tNB = st.iB * (st.plane(st.aB) - st.oB);
+        st.tFB = st.iB * (st.plane(st.aB + w4) - st.oB);
+        st.tNC = st.iC * (st.plane(st.aC) - st.oC);
+        st.tFC = st.iC * (st.plane(st.aC + w4) - st.oC);
+    } else {
+        const int keep = -2 * w;  // clears the offsets below the level-L ancestor
+        {   // per 10-bit field: (c & keep) | (axis bit of rk ? w : 0)
+            const uint32_t k3 = ((uint32_t)keep & 1023u) * 0x100401u;
+            const uint32_t bits = ((rk >> 1) & 1u) | ((rk & 1u) << 10) | (((rk >> 2) & 1u) << 20);
+            st.cP = (st.cP & k3) | bits * (uint32_t)w;
+        }
+        const float* nA = st.at(st.pA, st.sA, st.cA());
+        const float* nB = st.at(st.pB, st.sB, st.cB());
+        const float* nC = st.at(st.pC, st.sC, st.cC());
+        if (Masks::kKeepNear) {
+            st.nA = nA;
+            st.nB = nB;
+            st.nC = nC;
+        }
+        st.tNA = st.iA * (nA[0] - st.oA);
+        st.tFA = st.iA * (*st.at(nA, st.sA, w) - st.oA);
+        st.tNB = st.iB * (nB[0] - st.oB);
+        st.tFB = st.iB * (*st.at(nB, st.sB, w) - st.oB);
+        st.tNC = st.iC * (nC[0] - st.oC);
+        st.tFC = st.iC * (*st.at(nC, st.sC, w) - st.oC);
     }
-    st.tNA = st.iA * (nA[0] - st.oA);
-    st.tFA = st.iA * (*st.at(nA, st.sA, w) - st.oA);
-    st.tNB = st.iB * (nB[0] - st.oB);
-    st.tFB = st.iB * (*st.at(nB, st.sB, w) - st.oB);
-    st.tNC = st.iC * (nC[0] - st.oC);
-    st.tFC = st.iC * (*st.at(nC, st.sC, w) - st.oC);
     return false;
 }
 
