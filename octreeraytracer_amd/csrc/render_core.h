@@ -475,11 +475,15 @@ ORT_FN bool any_lane(bool p) {
     return p;
 #endif
 }
+// n / a for the fast walk's sphere roots (callers: t_min >= kFastTMin).  Below |n| = 2^-60 the
+// Markstein step may miss the correct rounding, but then |n / a| < 2^-57 (a >= 1/8) is far
+// below t_min and the root is rejected whatever its last bit, so only |n| > 2^100 (and NaN)
+// takes the IEEE division.
 ORT_FN float qdiv(float n, float a, float y) {
     const float q0 = n * y;
     float q = fmaf(fmaf(-q0, a, n), y, q0);
     const float an = fabsf(n);
-    const bool slow = !(an >= 0x1p-60f && an <= 0x1p100f);
+    const bool slow = !(an <= 0x1p100f);
     if (any_lane(slow)) q = slow ? n / a : q;
     return q;
 }
@@ -493,7 +497,8 @@ ORT_FN float qsqrt(float x) {
     const float sp = __uint_as_float(__float_as_uint(s) + 1u);
     float r = (fmaf(-sm, s, x) <= 0.0f) ? sm : s;
     r = (fmaf(-sp, s, x) > 0.0f) ? sp : r;
-    const bool slow = !(x >= 0x1p-96f && x <= 0x1p100f);
+    // x in [2^-96, 2^100] as one unsigned compare of the bits (x > 0 here: disc > 0)
+    const bool slow = f2u(x) - f2u(0x1p-96f) > f2u(0x1p100f) - f2u(0x1p-96f);
     if (any_lane(slow)) {
         // the volatile asm keeps this a real (wave-uniform) branch: left alone, the compiler
         // if-converts it and evaluates sqrtf's IEEE expansion on every call
