@@ -809,6 +809,29 @@ ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks
         // bits are shifted in rank order (rank 0 ends at bit 7: the reversed layout) -- one
         // v_max3 + v_min3 + v_sub + v_alignbit per child, no compare/select.
         uint32_t drop = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+        // the eight tests as ONE asm block: separate min3/max3 asm statements each made the
+        // compiler's hazard recognizer put an s_nop before their consumer
+        {
+            float e, x;
+#define ORT_C(EA, EB, EC, XA, XB, XC)                                                         \
+    "v_max3_f32 %[e], " EA ", " EB ", " EC "\n\tv_min3_f32 %[x], " XA ", " XB ", " XC "\n\t" \
+    "v_sub_f32 %[x], %[x], %[e]\n\tv_alignbit_b32 %[d], %[d], %[x], 31\n\t"
+            asm("v_mov_b32 %[d], 0\n\t"
+                ORT_C("%[NA]", "%[NB]", "%[nN]", "%[MA]", "%[MB]", "%[cN]")  // rank 0: A near, B near, C near
+                ORT_C("%[NA]", "%[MB]", "%[nN]", "%[MA]", "%[FB]", "%[cN]")  // rank 1: B far
+                ORT_C("%[MA]", "%[NB]", "%[nN]", "%[FA]", "%[MB]", "%[cN]")  // rank 2: A far
+                ORT_C("%[MA]", "%[MB]", "%[nN]", "%[FA]", "%[FB]", "%[cN]")  // rank 3
+                ORT_C("%[NA]", "%[NB]", "%[nF]", "%[MA]", "%[MB]", "%[cF]")  // ranks 4-7: C far
+                ORT_C("%[NA]", "%[MB]", "%[nF]", "%[MA]", "%[FB]", "%[cF]")
+                ORT_C("%[MA]", "%[NB]", "%[nF]", "%[FA]", "%[MB]", "%[cF]")
+                ORT_C("%[MA]", "%[MB]", "%[nF]", "%[FA]", "%[FB]", "%[cF]")
+                : [d] "=&v"(drop), [e] "=&v"(e), [x] "=&v"(x)
+                : [NA] "v"(tNA), [NB] "v"(tNB), [MA] "v"(tMA), [MB] "v"(tMB), [FA] "v"(tFA), [FB] "v"(tFB),
+                  [nN] "v"(nN), [nF] "v"(nF), [cN] "v"(cN), [cF] "v"(cF));
+#undef ORT_C
+        }
+#else
 #define ORT_CHILD(EA, EB, EC, XA, XB, XC) drop = (drop << 1) | (f2u(fmin3(XA, XB, XC) - fmax3(EA, EB, EC)) >> 31);
         ORT_CHILD(tNA, tNB, nN, tMA, tMB, cN)  // rank 0: A near, B near, C near
         ORT_CHILD(tNA, tMB, nN, tMA, tFB, cN)  // rank 1: B far
@@ -819,6 +842,7 @@ ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks
         ORT_CHILD(tMA, tNB, nF, tFA, tMB, cF)
         ORT_CHILD(tMA, tMB, nF, tFA, tFB, cF)
 #undef ORT_CHILD
+#endif
         const uint32_t keep = rcm & ~drop & 0xffu;
         if (Masks::kInlineLeaves && (rec.y & ORT_LEAFKIDS_FLAG)) {
             // Every existing child is a leaf, so the reference pops the surviving ones next,
