@@ -641,6 +641,7 @@ struct FastStateT {
     // axis (table start, a multiple of 1024, + 4 * index; see fast_axis_floats)
     const float* pl0;
     uint32_t aA, aB, aC;
+    uint32_t h4;      // half the current node's width, in bytes of plane table (4 * 2^(D-1-depth))
     ORT_FN float plane(uint32_t off) const { return *(const float*)((const char*)pl0 + off); }
     // otherwise: the ray-order plane table of each role axis, plane(i) = *(pA + sA * i bytes)
     const float* pA;
@@ -714,6 +715,7 @@ ORT_FN bool fast_begin(const KScene& S, const float* planes, const uint8_t* rank
         st.aA = 4u * ((swap ? 768u : 0u) + (gA ? 256u : 0u));
         st.aB = 4u * ((swap ? 0u : 768u) + (gB ? 256u : 0u));
         st.aC = 4u * (1536u + (gC ? 256u : 0u));
+        st.h4 = 2u * (uint32_t)top;
         const uint32_t t4 = 4u * (uint32_t)top;
         st.tNA = st.iA * (st.plane(st.aA) - st.oA);
         st.tFA = st.iA * (st.plane(st.aA + t4) - st.oA);
@@ -787,7 +789,7 @@ ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks
         const int h = 1 << (D - 1 - st.depth);  // half the node's width, in plane steps
         float tMA, tMB, tMC;
         if (Masks::kRevPlanes) {
-            const uint32_t h4 = 4u * (uint32_t)h;
+            const uint32_t h4 = st.h4;
             tMA = st.iA * (st.plane(st.aA + h4) - st.oA);
             tMB = st.iB * (st.plane(st.aB + h4) - st.oB);
             tMC = st.iC * (st.plane(st.aC + h4) - st.oC);
@@ -897,6 +899,7 @@ ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks
         // cleared; the table start is a multiple of 1024 > 8w) plus w planes on the axes
         // where the child is the far half
         const uint32_t w4 = 4u << (D - 1 - L);
+        st.h4 = w4 >> 1;
         const uint32_t m8 = ~(2u * w4 - 1u);
         const uint32_t s = (uint32_t)(D + 1 - L);  // log2(w4)
         st.aA = (st.aA & m8) | (((rk >> 1) & 1u) << s);
