@@ -104,3 +104,26 @@ def test_inverted_or_nan_boxes_take_the_exact_walk(ort, oracle):
             u.node_min[0, 2] = np.float32("nan")
         img, _ = emulate_render_host(s, u, p, layout=L.ORT_LAYOUT_COMPACT)
         assert same_bits(img, oracle.render(s, u, p)), bad
+
+
+def extreme_root_scene(ort):
+    """Sphere-root edge cases for the fast walk's quotient/sqrt shortcuts (render_core.h
+    qdiv/qsqrt): the camera inside a sphere (near root negative, far root taken), a sphere
+    whose surface passes by the lens (roots near 0), one far enough that half_b^2 overflows
+    (disc = inf: the IEEE division path), one whose disc exceeds 2^100 (the IEEE sqrt path),
+    and ordinary spheres in front."""
+    return ort.SphereSet.from_arrays(
+        [[0, 2.5, -10], [0, 2.5, -12], [0.5, 2.5, -1e20], [0, 2.5, -2e18], [0, 2.5, -20], [1.5, 2, -16],
+         [-1, 3, -25]],
+        [3.0, 2.0, 1e19, 1e18, 1.0, 0.5, 0.75], [2, 1, 0, 0, 0, 1, 2],
+        [[0.9, 0.9, 0.9], [0.8, 0.6, 0.2], [0.2, 0.4, 0.8], [0.5, 0.9, 0.3], [0.7, 0.1, 0.1], [0.3, 0.3, 0.9],
+         [0.9, 0.9, 0.6]],
+        [0, 0.2, 0, 0, 0, 0.1, 0], [1.5, 1, 1, 1, 1, 1, 1.3])
+
+
+@pytest.mark.parametrize("use_octree", [1, 0])
+def test_extreme_sphere_roots(ort, oracle, use_octree):
+    s = extreme_root_scene(ort)
+    t = ort.build_octree(s, 5, 0) if use_octree else None
+    p = ort.FrameParams.default_camera(64, 40, max_depth=4, use_octree=use_octree)
+    assert same_bits(emulate_render_host(s, t, p)[0], oracle.render(s, t, p))

@@ -271,3 +271,17 @@ def test_xcd_swizzle_orders_identical(ort, oracle, renderer, scene_c2, mode):
             renderer.set_xcd_swizzle(3)
     finally:
         renderer.set_xcd_swizzle(2)
+
+
+@pytest.mark.parametrize("use_octree", [1, 0])
+def test_extreme_sphere_roots(ort, oracle, renderer, use_octree):
+    """The kernel's quotient/sqrt shortcuts at their edges (tests/test_emulation.py
+    extreme_root_scene): camera inside a sphere, roots near 0, half_b^2 overflow, disc > 2^100."""
+    from test_emulation import extreme_root_scene
+    s = extreme_root_scene(ort)
+    t = ort.build_octree(s, 5, 0) if use_octree else None
+    renderer.upload(s, t)
+    p = ort.FrameParams.default_camera(64, 40, max_depth=4, use_octree=use_octree)
+    assert_same(renderer.render(p), oracle.render(s, t, p), "extreme roots")
+    p1 = ort.FrameParams.default_camera(64, 40, use_octree=use_octree)
+    assert_same(renderer.render(p1), oracle.render(s, t, p1), "extreme roots, primary")
