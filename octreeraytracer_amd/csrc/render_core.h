@@ -1061,25 +1061,15 @@ ORT_FN V3 random_in_unit_disk(ort_rng& st) {
     const float PI_F = (float)3.14159265359;
     const float spx = 2.0f * ort_rand2D(&st) - 1.0f;
     const float spy = 2.0f * ort_rand2D(&st) - 1.0f;
-    float r, phi;
-    if (spx > -spy) {
-        if (spx > spy) {
-            r = spx;
-            phi = spy / spx;
-        } else {
-            r = spy;
-            phi = 2.0f - spx / spy;
-        }
-    } else {
-        if (spx < spy) {
-            r = -spx;
-            phi = 4.0f + spy / spx;
-        } else {
-            r = -spy;
-            if (spy != 0.0f) phi = 6.0f - spx / spy;
-            else phi = 0.0f;
-        }
-    }
+    // the four branches of glsl:109-131 with their one division hoisted out (divergent
+    // branches each ran a full IEEE division): q = num / den, then the branch's phi from q
+    const bool right = spx > -spy;
+    const bool xbig = right ? (spx > spy) : (spx < spy);  // |spx| dominates: phi from spy / spx
+    const float r = right ? (xbig ? spx : spy) : (xbig ? -spx : -spy);
+    const float q = (xbig ? spy : spx) / (xbig ? spx : spy);
+    float phi;
+    if (xbig) phi = right ? q : 4.0f + q;
+    else phi = right ? 2.0f - q : (spy != 0.0f ? 6.0f - q : 0.0f);
     phi *= PI_F / 4.0f;
     return mk(r * ort_cosf(phi), r * ort_sinf(phi), 0.0f);
 }
