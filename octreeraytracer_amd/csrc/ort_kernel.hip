@@ -218,16 +218,17 @@ __global__ void __launch_bounds__(kBlock) ort_raygen_kernel(PipeArgs A) {
 // chunk, MI355X_MICROARCH.md 'dequeue') and hands the next slots of its chunk to lanes
 // that finished, so the wave stays full until the queue drains.  Rays the fast walk
 // cannot take are appended to the defer list for ort_trace_exact.
-// Waves per SIMD of the per-lane trace kernel: 7 (72 VGPRs) -- at 8 (64 VGPRs) the walk with
-// inline leaf children spills ~5 registers per iteration and runs 1.6x slower (tools/ab_libs.py).
+// Waves per SIMD (minimum, amdgpu_waves_per_eu): the per-lane trace kernels run at 8 (57 / 60
+// VGPRs, spill-free); the persistent kernel at 6 (79 VGPRs) -- forced to 8 it spills and C5
+// runs 11 % slower, at 7 no faster (tools/ab_stream.py).
+#ifndef ORT_PERSISTENT_WAVES
+#define ORT_PERSISTENT_WAVES 5
+#endif
 #ifndef ORT_TRACE_WAVES
 #define ORT_TRACE_WAVES 8
 #endif
 #ifndef ORT_TRACE_WAVES_DEEP  // 96-bit masks, no inline leaf children: 64 VGPRs, spill-free
 #define ORT_TRACE_WAVES_DEEP 8
-#endif
-#ifndef ORT_PERSISTENT_WAVES
-#define ORT_PERSISTENT_WAVES 5
 #endif
 constexpr int kChunk = 256;
 
