@@ -234,7 +234,7 @@ constexpr int kChunk = 256;
 
 template <bool COUNT>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ORT_PERSISTENT_WAVES))) ort_trace_persistent(PipeArgs A) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];  // plane tables: 1 KiB-aligned
     LdsView L = setup_lds<true>(smem, A.S);
     const uint8_t* lut = L.lut;
     const int lane = threadIdx.x & 63;
@@ -463,24 +463,24 @@ __device__ __forceinline__ void trace_queue_body(PipeArgs& A, unsigned char* sme
 // FUSE: 1 sample, 1 bounce -- the kernel also shades (shade_direct), no hit records.
 template <bool COUNT, bool PRIMARY, bool FUSE>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ORT_TRACE_WAVES))) ort_trace_compact(PipeArgs A) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];  // plane tables: 1 KiB-aligned
     trace_compact_body<COUNT, PRIMARY, false, FUSE>(A, smem);
 }
 template <bool COUNT, bool PRIMARY, bool FUSE>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ORT_TRACE_WAVES_DEEP)))
 ort_trace_compact_deep(PipeArgs A) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];  // plane tables: 1 KiB-aligned
     trace_compact_body<COUNT, PRIMARY, true, FUSE>(A, smem);
 }
 template <bool COUNT, bool PRIMARY, bool FUSE>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ORT_TRACE_WAVES))) ort_trace_compact_q(PipeArgs A) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];  // plane tables: 1 KiB-aligned
     trace_queue_body<COUNT, PRIMARY, false, FUSE>(A, smem);
 }
 template <bool COUNT, bool PRIMARY, bool FUSE>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ORT_TRACE_WAVES_DEEP)))
 ort_trace_compact_deep_q(PipeArgs A) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];  // plane tables: 1 KiB-aligned
     trace_queue_body<COUNT, PRIMARY, true, FUSE>(A, smem);
 }
 
@@ -514,7 +514,7 @@ __device__ inline uint32_t wave_or(uint32_t v) {
 // while the per-lane loop ran a ~46-VALU pop for every lane every iteration.
 template <bool COUNT, bool DEEP>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ORT_TRACE_WAVES))) ort_trace_packet(PipeArgs A) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];  // plane tables: 1 KiB-aligned
     using Masks = typename std::conditional<DEEP, ort::Masks96, ort::Masks64>::type;
     const ort::KScene& S = A.S;
     // planes and rank LUT in LDS: wave-uniform reads are LDS broadcasts addressed by one VALU
@@ -715,7 +715,7 @@ __global__ void __launch_bounds__(kBlock) ort_trace_kernel(PipeArgs A) {
 // Exact compact walk (traverse_compact) for the deferred rays; grid-stride loop.
 template <bool COUNT, bool PRIMARY, bool FUSE>
 __global__ void __launch_bounds__(kBlock) ort_trace_exact(PipeArgs A) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];  // plane tables: 1 KiB-aligned
     LdsView L = setup_lds<false>(smem, A.S);
     const int n = *A.sync;
     ort::Counters cnt;

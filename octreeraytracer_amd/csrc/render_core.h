@@ -642,7 +642,18 @@ struct FastStateT {
     const float* pl0;
     uint32_t aA, aB, aC;
     uint32_t h4;      // half the current node's width, in bytes of plane table (4 * 2^(D-1-depth))
+#if defined(__HIP_DEVICE_COMPILE__)
+    // device: the offsets are absolute LDS byte addresses (the table image sits in LDS, at a
+    // 1 KiB-aligned start), so a read is one ds_read with no base add -- the dynamic LDS
+    // symbol's address is a link-time constant the compiler would otherwise add every time
+    ORT_FN float plane(uint32_t a) const { return *(const __attribute__((address_space(3))) float*)(size_t)a; }
+    static ORT_FN uint32_t table_base(const float* planes) {
+        return (uint32_t)(size_t)(const __attribute__((address_space(3))) float*)planes;
+    }
+#else
     ORT_FN float plane(uint32_t off) const { return *(const float*)((const char*)pl0 + off); }
+    static ORT_FN uint32_t table_base(const float*) { return 0u; }
+#endif
     // otherwise: the ray-order plane table of each role axis, plane(i) = *(pA + sA * i bytes)
     const float* pA;
     const float* pB;
@@ -712,9 +723,10 @@ ORT_FN bool fast_begin(const KScene& S, const float* planes, const uint8_t* rank
     // planes: fast_plane_floats(D) floats (fill_fast_planes)
     if (Masks::kRevPlanes) {  // per axis: forward table, reversed one 1 KiB further
         st.pl0 = planes;
-        st.aA = 4u * ((swap ? 768u : 0u) + (gA ? 256u : 0u));
-        st.aB = 4u * ((swap ? 0u : 768u) + (gB ? 256u : 0u));
-        st.aC = 4u * (1536u + (gC ? 256u : 0u));
+        const uint32_t b0 = FastStateT<Masks>::table_base(planes);  // 1 KiB-aligned (ort_kernel.hip)
+        st.aA = b0 + 4u * ((swap ? 768u : 0u) + (gA ? 256u : 0u));
+        st.aB = b0 + 4u * ((swap ? 0u : 768u) + (gB ? 256u : 0u));
+        st.aC = b0 + 4u * (1536u + (gC ? 256u : 0u));
         st.h4 = 2u * (uint32_t)top;
         const uint32_t t4 = 4u * (uint32_t)top;
         st.tNA = st.iA * (st.plane(st.aA) - st.oA);
