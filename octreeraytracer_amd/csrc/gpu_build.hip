@@ -253,7 +253,8 @@ __global__ void k_compact_nodes(const int32_t* co, const int32_t* oo, const int3
 __global__ void k_leaf_gather(const int32_t* idx, int64_t n, const float4* sp, float4* leaf_sph, int32_t* leaf_idx) {
     for (int64_t e = blockIdx.x * (int64_t)kB + threadIdx.x; e < n; e += (int64_t)gridDim.x * kB) {
         const int32_t s = idx[e];
-        leaf_sph[e] = sp[s];
+        const float4 v = sp[s];
+        leaf_sph[e] = make_float4(v.x, v.y, v.z, v.w * v.w);  // radius^2 (layout.h)
         leaf_idx[e] = s;
     }
 }

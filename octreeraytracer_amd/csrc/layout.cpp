@@ -148,7 +148,9 @@ bool buildCompactLayout(const SceneInput& in, int maxDepth, CompactLayout& out, 
     out.leaf_idx.resize((size_t)in.n_indices);
     for (int64_t e = 0; e < in.n_indices; ++e) {
         const int32_t s = in.indices[e];
-        std::memcpy(&out.leaf_sph[4 * (size_t)e], in.sph_cr + 4 * (size_t)s, 16);
+        std::memcpy(&out.leaf_sph[4 * (size_t)e], in.sph_cr + 4 * (size_t)s, 12);
+        const float rad = in.sph_cr[4 * (size_t)s + 3];
+        out.leaf_sph[4 * (size_t)e + 3] = rad * rad;  // the kernel's r * r, rounded once (fp32)
         out.leaf_idx[(size_t)e] = s;
     }
     return true;

@@ -11,7 +11,8 @@
 //                   leaf     -> {objectsOffset, objectCount}
 //     childMask bit k = child (childrenOffset + k) is in range and is not an empty leaf
 //     (the glsl:456 and glsl:467 skip tests, precomputed).
-//   leaf_sph[e] = spheres[objectIndices[e]] (16 B): one gather instead of index + sphere.
+//   leaf_sph[e] = spheres[objectIndices[e]] with .w = radius * radius (16 B): one gather
+//   instead of index + sphere, and the sphere test's r * r precomputed (rounded as it would be).
 //   leaf_idx[e] = objectIndices[e], read only for the final hit (material lookup).
 //   planes[a][k], k = 0..2^D: coordinate of the axis-a split plane at dyadic position
 //     k / 2^D.  The reference builder derives every child box from its parent by

@@ -89,7 +89,7 @@ struct KScene {
     int n_nodes;
     // compact layout
     const uint2* node;       // internal: {childrenOffset, FLAG|childMask}; leaf: {objectsOffset, objectCount}
-    const float4* leaf_sph;  // per objectIndices entry: the sphere's center.xyz, radius
+    const float4* leaf_sph;  // per objectIndices entry: the sphere's center.xyz, radius^2 (as float r*r)
     const int* leaf_idx;     // per entry: sphere index (= objectIndices)
     const float* planes;     // 3 x (2^depth + 1) split-plane coordinates (global copy)
     const uint4* lds_img;    // the workgroup LDS image (fast plane tables | rank LUT), built once
@@ -169,10 +169,12 @@ ORT_FN bool ray_box(const Ray& r, V3 inv, V3 bmin, V3 bmax, float& tmin, float& 
 }
 
 // Sphere_hit (glsl:224-273) returning only the accepted t; a = dot(d,d) precomputed.
+// R2: sp.w already holds radius * radius (the compact layout's leaf_sph), else the radius.
+template <bool R2 = false>
 ORT_FN bool sphere_hit_t(const Ray& r, float a, float4 sp, float t_min, float t_max, float& t) {
     const V3 oc = mk(r.o.x - sp.x, r.o.y - sp.y, r.o.z - sp.z);
     const float half_b = dot(oc, r.d);
-    const float c = dot(oc, oc) - sp.w * sp.w;
+    const float c = dot(oc, oc) - (R2 ? sp.w : sp.w * sp.w);
     const float disc = half_b * half_b - a * c;
     if (disc > 0.0f) {
         const float sq = sqrtf(disc);
@@ -338,7 +340,7 @@ ORT_FN bool traverse_compact(const KScene& S, const float* planes, const Ray& r,
                 const float4 sp = S.leaf_sph[off + i];
                 if (COUNT) cnt.v[2] += 1;
                 float t;
-                if (sphere_hit_t(r, a, sp, ntmin, closest, t)) {
+                if (sphere_hit_t<true>(r, a, sp, ntmin, closest, t)) {  // leaf_sph: .w = r^2
                     hit = true;
                     closest = t;
                     hitEntry = off + i;
@@ -515,7 +517,7 @@ ORT_FN float qsqrt(float x) {
 ORT_FN bool sphere_hit_fast(const Ray& r, float a, float ya, float4 sp, float t_min, float t_max, float& t) {
     const V3 oc = mk(r.o.x - sp.x, r.o.y - sp.y, r.o.z - sp.z);
     const float half_b = dot(oc, r.d);
-    const float c = dot(oc, oc) - sp.w * sp.w;
+    const float c = dot(oc, oc) - sp.w;  // leaf_sph: .w = radius * radius
     const float disc = half_b * half_b - a * c;
     if (disc > 0.0f) {
         // both roots, no branch between them: the near one if in range, else the far one
@@ -1275,7 +1277,7 @@ ORT_FN HitRec hit_record(const KScene& S, const Ray& r, float t, int entry) {
     float4 sp;
     if (MODE == 0) {
         sidx = S.leaf_idx[entry];
-        sp = S.leaf_sph[entry];
+        sp = S.sph_cr[sidx];  // (leaf_sph holds radius^2)
     } else if (MODE == 1) {
         sidx = S.indices[entry];
         sp = S.sph_cr[sidx];
