@@ -871,9 +871,11 @@ ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks
                 const uint32_t R = 7u - (uint32_t)hb;
                 const uint2 lrec = fetch_node(S, co + (int)((st.otab >> (4 * R)) & 15u));
                 if (COUNT) cnt.v[0] += 1;
-                const float eA = (R & 2u) ? tMA : tNA, eB = (R & 1u) ? tMB : tNB, eC = (R & 4u) ? tMC : tNC;
+                // max(max3(entries), t_min) with t_min folded into the C entry (nN / nF, as in
+                // the child tests; max is exact, so the order does not matter)
+                const float eA = (R & 2u) ? tMA : tNA, eB = (R & 1u) ? tMB : tNB, eC = (R & 4u) ? nF : nN;
                 // a hit ends the walk after this leaf (glsl:336): no later sibling is tested
-                const bool h = leaf_tests<COUNT>(S, st, (int)lrec.x, (int)lrec.y, fmax_tmin(fmax3(eA, eB, eC)), cnt);
+                const bool h = leaf_tests<COUNT>(S, st, (int)lrec.x, (int)lrec.y, fmax3(eA, eB, eC), cnt);
                 todo = h ? 0u : todo;
             }
             if (st.hit()) return true;
