@@ -53,6 +53,7 @@ struct V3 {
 };
 ORT_FN int f2i(float f) { int i; __builtin_memcpy(&i, &f, 4); return i; }
 ORT_FN uint32_t f2u(float f) { uint32_t i; __builtin_memcpy(&i, &f, 4); return i; }
+ORT_FN float u2f(uint32_t i) { float f; __builtin_memcpy(&f, &i, 4); return f; }
 ORT_FN V3 mk(float x, float y, float z) { V3 r; r.x = x; r.y = y; r.z = z; return r; }
 ORT_FN V3 add(V3 a, V3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
 ORT_FN V3 sub(V3 a, V3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
@@ -873,7 +874,22 @@ ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks
                 if (COUNT) cnt.v[0] += 1;
                 // max(max3(entries), t_min) with t_min folded into the C entry (nN / nF, as in
                 // the child tests; max is exact, so the order does not matter)
+#if defined(__HIP_DEVICE_COMPILE__)
+                // bitwise selects (v_bfe_i32 + v_bfi_b32) in one asm block: the compiler turns
+                // a plain select into v_cmp + s_nop + v_cndmask
+                float eA, eB, eC;
+                {
+                    uint32_t m;
+                    asm("v_bfe_i32 %[m], %[R], 1, 1\n\tv_bfi_b32 %[a], %[m], %[MA], %[NA]\n\t"
+                        "v_bfe_i32 %[m], %[R], 0, 1\n\tv_bfi_b32 %[b], %[m], %[MB], %[NB]\n\t"
+                        "v_bfe_i32 %[m], %[R], 2, 1\n\tv_bfi_b32 %[c], %[m], %[CF], %[CN]"
+                        : [a] "=&v"(eA), [b] "=&v"(eB), [c] "=&v"(eC), [m] "=&v"(m)
+                        : [R] "v"(R), [MA] "v"(tMA), [NA] "v"(tNA), [MB] "v"(tMB), [NB] "v"(tNB), [CF] "v"(nF),
+                          [CN] "v"(nN));
+                }
+#else
                 const float eA = (R & 2u) ? tMA : tNA, eB = (R & 1u) ? tMB : tNB, eC = (R & 4u) ? nF : nN;
+#endif
                 // a hit ends the walk after this leaf (glsl:336): no later sibling is tested
                 const bool h = leaf_tests<COUNT>(S, st, (int)lrec.x, (int)lrec.y, fmax3(eA, eB, eC), cnt);
                 todo = h ? 0u : todo;
