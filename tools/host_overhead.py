@@ -3,9 +3,13 @@ world size, rank 0's band tile of an N-GPU run (is the host fast enough to feed 
 renders 1/N of the frame?).  With inflight > 1, that many renderers (each with its own copy of
 the scene) take frames in turn on their own streams, so one frame's tail overlaps the next.
 usage: python tools/host_overhead.py [config] [frames] [world] [inflight] [torch|hip|prio]"""
+import os
 import sys
 import time
 from pathlib import Path
+
+if len(sys.argv) > 4 and int(sys.argv[4]) > 1:  # as bench.py: overlap needs its own HW queues
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
