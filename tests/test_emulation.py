@@ -127,3 +127,27 @@ def test_extreme_sphere_roots(ort, oracle, use_octree):
     t = ort.build_octree(s, 5, 0) if use_octree else None
     p = ort.FrameParams.default_camera(64, 40, max_depth=4, use_octree=use_octree)
     assert same_bits(emulate_render_host(s, t, p)[0], oracle.render(s, t, p))
+
+
+def test_walk_steps_analysis_matches_counters(ort, oracle, scene_c1):
+    """ort_debug_walk_steps (tools/walk_sim.py's input, analysis only) replays the kernel's own
+    fast walk: over every 8x8 block its per-step object counts add up to the oracle's."""
+    import ctypes as C
+    from octreeraytracer_amd import _lib as L
+    s, t = scene_c1
+    p = ort.FrameParams.default_camera(256, 256)
+    _, rc = oracle.render(s, t, p, counts=True)
+    f = L.lib().ort_debug_walk_steps
+    f.restype = C.c_int64
+    fp = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+    arr = [np.ascontiguousarray(x) for x in (s.center_radius, s.mat_albedo, s.fuzz_ri)]
+    tt = [np.ascontiguousarray(x) for x in (t.node_min, t.node_max, t.children_offset, t.objects_offset,
+                                             t.object_count, t.object_indices)]
+    lens = np.zeros(32 * 32 * 64, np.int32)
+    steps = np.zeros(256 * 256 * 200, np.uint16)
+    n = f(fp(arr[0]), fp(arr[1]), fp(arr[2]), C.c_int32(s.n), fp(tt[0]), fp(tt[1]), fp(tt[2]), fp(tt[3]),
+          fp(tt[4]), C.c_int32(t.n_nodes), fp(tt[5]), C.c_int64(t.n_indices), C.byref(p.to_c()), C.c_int32(1),
+          fp(lens), C.c_int64(len(lens)), fp(steps), C.c_int64(len(steps)))
+    assert n == int(lens.sum()) > 0
+    assert int((steps[:n] & 0xff).astype(np.int64).sum()) == rc["leaf_objects"]
+    assert 0 < int(np.count_nonzero(lens)) <= rc["traversals"]  # root-box misses take no step
