@@ -93,6 +93,45 @@ for w in range(nw):
         leafB += 1
         for i in parked:
             pend[i] = None
+# (C) fold the leaf-children (LK) nodes into their parent's step: a run of LK steps after a
+# step belongs to that step (the parent's surviving children, popped consecutively)
+FOLD = 55  # per folded child: its box by selects from the parent's slabs, mid planes, 8 tests
+totC = itC = 0
+lkall = (steps[:n] & 0x8000) != 0
+for w in range(nw):
+    macro = []
+    for l in range(64):
+        a, b = offs[64 * w + l], offs[64 * w + l + 1]
+        if b <= a:
+            continue
+        ms = []
+        for i in range(a, b):
+            if lkall[i] and ms:
+                ms[-1][1].append((objs_all[i], kids_all[i]))
+            else:
+                ms.append(((objs_all[i], kids_all[i]), []))
+        macro.append(ms)
+    if not macro:
+        continue
+    mx = max(len(m) for m in macro)
+    for k in range(mx):
+        here = [m[k] for m in macro if k < len(m)]
+        totC += POP + INTERNAL
+        itC += 1
+        mo = max(h[0][0] for h in here)
+        mk = max(h[0][1] for h in here)
+        if mk:
+            totC += KID * mk + OBJ * mo
+        nch = max(len(h[1]) for h in here)
+        for j in range(nch):
+            ch = [h[1][j] for h in here if j < len(h[1])]
+            totC += FOLD
+            mo = max(c[0] for c in ch)
+            mk = max(c[1] for c in ch)
+            if mk:
+                totC += KID * mk + OBJ * mo
+print(f"(C) fold leaf-children nodes into the parent step: {totC / nw:.0f} VALU/wave ({itC / nw:.1f} iterations), "
+      f"C/A {totC / totA:.3f}")
 print(f"{cfg}: {nw} sampled waves; model VALU/wave: A {totA / nw:.0f} ({itA / nw:.1f} iterations, "
       f"{leafA / nw:.1f} leaf loops)  B {totB / nw:.0f} ({itB / nw:.1f} iterations, {leafB / nw:.1f} leaf loops)  "
       f"B/A {totB / totA:.3f}")
