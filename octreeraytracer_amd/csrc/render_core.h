@@ -29,6 +29,7 @@
 
 #include "../../include/ort_math.h"
 
+
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
 #define ORT_FN __host__ __device__ __forceinline__
@@ -787,6 +788,85 @@ ORT_FN bool leaf_tests(const KScene& S, FastStateT<Masks>& st, int off, int n, f
     return st.hit();
 }
 
+// Drop bits of a node's eight children, rank order (rank 0 ends at bit 7: the reversed
+// layout), from its per-axis slab values N (near), M (mid), F (far); t_min is folded into the
+// C entries (nN, nF) and t_max into the C exits (cN, cF).  Keep child R <=> exit >= entry, with
+// entry >= t_min > 0 and exit <= t_max finite, so exit - entry is never NaN and is +0 when
+// equal: its sign bit is "drop" -- one v_max3 + v_min3 + v_sub + v_alignbit per child.
+ORT_FN uint32_t child_drops(float tNA, float tNB, float tMA, float tMB, float tFA, float tFB, float nN, float nF,
+                            float cN, float cF) {
+    uint32_t drop = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+    // the eight tests as ONE asm block: separate min3/max3 asm statements each made the
+    // compiler's hazard recognizer put an s_nop before their consumer
+    float e, x;
+#define ORT_C(EA, EB, EC, XA, XB, XC)                                                         \
+    "v_max3_f32 %[e], " EA ", " EB ", " EC "\n\tv_min3_f32 %[x], " XA ", " XB ", " XC "\n\t" \
+    "v_sub_f32 %[x], %[x], %[e]\n\tv_alignbit_b32 %[d], %[d], %[x], 31\n\t"
+    asm("v_mov_b32 %[d], 0\n\t"
+        ORT_C("%[NA]", "%[NB]", "%[nN]", "%[MA]", "%[MB]", "%[cN]")  // rank 0: A near, B near, C near
+        ORT_C("%[NA]", "%[MB]", "%[nN]", "%[MA]", "%[FB]", "%[cN]")  // rank 1: B far
+        ORT_C("%[MA]", "%[NB]", "%[nN]", "%[FA]", "%[MB]", "%[cN]")  // rank 2: A far
+        ORT_C("%[MA]", "%[MB]", "%[nN]", "%[FA]", "%[FB]", "%[cN]")  // rank 3
+        ORT_C("%[NA]", "%[NB]", "%[nF]", "%[MA]", "%[MB]", "%[cF]")  // ranks 4-7: C far
+        ORT_C("%[NA]", "%[MB]", "%[nF]", "%[MA]", "%[FB]", "%[cF]")
+        ORT_C("%[MA]", "%[NB]", "%[nF]", "%[FA]", "%[MB]", "%[cF]")
+        ORT_C("%[MA]", "%[MB]", "%[nF]", "%[FA]", "%[FB]", "%[cF]")
+        : [d] "=&v"(drop), [e] "=&v"(e), [x] "=&v"(x)
+        : [NA] "v"(tNA), [NB] "v"(tNB), [MA] "v"(tMA), [MB] "v"(tMB), [FA] "v"(tFA), [FB] "v"(tFB), [nN] "v"(nN),
+          [nF] "v"(nF), [cN] "v"(cN), [cF] "v"(cF));
+#undef ORT_C
+#else
+#define ORT_CHILD(EA, EB, EC, XA, XB, XC) drop = (drop << 1) | (f2u(fmin3(XA, XB, XC) - fmax3(EA, EB, EC)) >> 31);
+    ORT_CHILD(tNA, tNB, nN, tMA, tMB, cN)  // rank 0: A near, B near, C near
+    ORT_CHILD(tNA, tMB, nN, tMA, tFB, cN)  // rank 1: B far
+    ORT_CHILD(tMA, tNB, nN, tFA, tMB, cN)  // rank 2: A far
+    ORT_CHILD(tMA, tMB, nN, tFA, tFB, cN)  // rank 3
+    ORT_CHILD(tNA, tNB, nF, tMA, tMB, cF)  // ranks 4-7: C far
+    ORT_CHILD(tNA, tMB, nF, tMA, tFB, cF)
+    ORT_CHILD(tMA, tNB, nF, tFA, tMB, cF)
+    ORT_CHILD(tMA, tMB, nF, tFA, tFB, cF)
+#undef ORT_CHILD
+#endif
+    return drop;
+}
+
+// The surviving leaf children (keep, rank-reversed bits) of a leaf-children node whose
+// children start at co, tested in rank order -- the order the reference pops them -- each
+// with the tmin the reference pushed for it (max(max3(child entries), t_min), t_min folded
+// into the C entries nN / nF; max is exact, so the order does not matter).  A hit ends the
+// walk after its leaf (glsl:336): no later sibling is tested.  Returns whether one hit.
+template <bool COUNT, class Masks>
+ORT_FN bool leaf_kids(const KScene& S, FastStateT<Masks>& st, int co, uint32_t keep, float tNA, float tMA, float tNB,
+                      float tMB, float nN, float nF, Counters& cnt) {
+    uint32_t todo = keep;
+    while (todo) {
+        const int hb = 31 - __builtin_clz(todo);
+        todo ^= 1u << hb;
+        const uint32_t R = 7u - (uint32_t)hb;
+        const uint2 lrec = fetch_node(S, co + (int)((st.otab >> (4 * R)) & 15u));
+        if (COUNT) cnt.v[0] += 1;
+#if defined(__HIP_DEVICE_COMPILE__)
+        // bitwise selects (v_bfe_i32 + v_bfi_b32) in one asm block: the compiler turns a
+        // plain select into v_cmp + s_nop + v_cndmask
+        float eA, eB, eC;
+        {
+            uint32_t m;
+            asm("v_bfe_i32 %[m], %[R], 1, 1\n\tv_bfi_b32 %[a], %[m], %[MA], %[NA]\n\t"
+                "v_bfe_i32 %[m], %[R], 0, 1\n\tv_bfi_b32 %[b], %[m], %[MB], %[NB]\n\t"
+                "v_bfe_i32 %[m], %[R], 2, 1\n\tv_bfi_b32 %[c], %[m], %[CF], %[CN]"
+                : [a] "=&v"(eA), [b] "=&v"(eB), [c] "=&v"(eC), [m] "=&v"(m)
+                : [R] "v"(R), [MA] "v"(tMA), [NA] "v"(tNA), [MB] "v"(tMB), [NB] "v"(tNB), [CF] "v"(nF), [CN] "v"(nN));
+        }
+#else
+        const float eA = (R & 2u) ? tMA : tNA, eB = (R & 1u) ? tMB : tNB, eC = (R & 4u) ? nF : nN;
+#endif
+        const bool h = leaf_tests<COUNT>(S, st, (int)lrec.x, (int)lrec.y, fmax3(eA, eB, eC), cnt);
+        todo = h ? 0u : todo;
+    }
+    return st.hit();
+}
+
 // One node of the walk: visit st.node (push its surviving children, or test its spheres),
 // then pop the next node.  Returns true when the walk is over (hit found, or stack empty).
 template <bool COUNT, class Masks, class Frames>
@@ -825,76 +905,11 @@ ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks
         // exit - entry is never NaN and is +0 when equal: its sign bit is "drop".  The drop
         // bits are shifted in rank order (rank 0 ends at bit 7: the reversed layout) -- one
         // v_max3 + v_min3 + v_sub + v_alignbit per child, no compare/select.
-        uint32_t drop = 0;
-#if defined(__HIP_DEVICE_COMPILE__)
-        // the eight tests as ONE asm block: separate min3/max3 asm statements each made the
-        // compiler's hazard recognizer put an s_nop before their consumer
-        {
-            float e, x;
-#define ORT_C(EA, EB, EC, XA, XB, XC)                                                         \
-    "v_max3_f32 %[e], " EA ", " EB ", " EC "\n\tv_min3_f32 %[x], " XA ", " XB ", " XC "\n\t" \
-    "v_sub_f32 %[x], %[x], %[e]\n\tv_alignbit_b32 %[d], %[d], %[x], 31\n\t"
-            asm("v_mov_b32 %[d], 0\n\t"
-                ORT_C("%[NA]", "%[NB]", "%[nN]", "%[MA]", "%[MB]", "%[cN]")  // rank 0: A near, B near, C near
-                ORT_C("%[NA]", "%[MB]", "%[nN]", "%[MA]", "%[FB]", "%[cN]")  // rank 1: B far
-                ORT_C("%[MA]", "%[NB]", "%[nN]", "%[FA]", "%[MB]", "%[cN]")  // rank 2: A far
-                ORT_C("%[MA]", "%[MB]", "%[nN]", "%[FA]", "%[FB]", "%[cN]")  // rank 3
-                ORT_C("%[NA]", "%[NB]", "%[nF]", "%[MA]", "%[MB]", "%[cF]")  // ranks 4-7: C far
-                ORT_C("%[NA]", "%[MB]", "%[nF]", "%[MA]", "%[FB]", "%[cF]")
-                ORT_C("%[MA]", "%[NB]", "%[nF]", "%[FA]", "%[MB]", "%[cF]")
-                ORT_C("%[MA]", "%[MB]", "%[nF]", "%[FA]", "%[FB]", "%[cF]")
-                : [d] "=&v"(drop), [e] "=&v"(e), [x] "=&v"(x)
-                : [NA] "v"(tNA), [NB] "v"(tNB), [MA] "v"(tMA), [MB] "v"(tMB), [FA] "v"(tFA), [FB] "v"(tFB),
-                  [nN] "v"(nN), [nF] "v"(nF), [cN] "v"(cN), [cF] "v"(cF));
-#undef ORT_C
-        }
-#else
-#define ORT_CHILD(EA, EB, EC, XA, XB, XC) drop = (drop << 1) | (f2u(fmin3(XA, XB, XC) - fmax3(EA, EB, EC)) >> 31);
-        ORT_CHILD(tNA, tNB, nN, tMA, tMB, cN)  // rank 0: A near, B near, C near
-        ORT_CHILD(tNA, tMB, nN, tMA, tFB, cN)  // rank 1: B far
-        ORT_CHILD(tMA, tNB, nN, tFA, tMB, cN)  // rank 2: A far
-        ORT_CHILD(tMA, tMB, nN, tFA, tFB, cN)  // rank 3
-        ORT_CHILD(tNA, tNB, nF, tMA, tMB, cF)  // ranks 4-7: C far
-        ORT_CHILD(tNA, tMB, nF, tMA, tFB, cF)
-        ORT_CHILD(tMA, tNB, nF, tFA, tMB, cF)
-        ORT_CHILD(tMA, tMB, nF, tFA, tFB, cF)
-#undef ORT_CHILD
-#endif
-        const uint32_t keep = rcm & ~drop & 0xffu;
+        const uint32_t keep = rcm & ~child_drops(tNA, tNB, tMA, tMB, tFA, tFB, nN, nF, cN, cF) & 0xffu;
         if (Masks::kInlineLeaves && (rec.y & ORT_LEAFKIDS_FLAG)) {
             // Every existing child is a leaf, so the reference pops the surviving ones next,
-            // consecutively in rank order (a leaf pushes nothing): test them right here, with
-            // the tmin the reference pushed for each (max(max3(child entries), t_min)).
-            uint32_t todo = keep;
-            while (todo) {
-                const int hb = 31 - __builtin_clz(todo);
-                todo ^= 1u << hb;
-                const uint32_t R = 7u - (uint32_t)hb;
-                const uint2 lrec = fetch_node(S, co + (int)((st.otab >> (4 * R)) & 15u));
-                if (COUNT) cnt.v[0] += 1;
-                // max(max3(entries), t_min) with t_min folded into the C entry (nN / nF, as in
-                // the child tests; max is exact, so the order does not matter)
-#if defined(__HIP_DEVICE_COMPILE__)
-                // bitwise selects (v_bfe_i32 + v_bfi_b32) in one asm block: the compiler turns
-                // a plain select into v_cmp + s_nop + v_cndmask
-                float eA, eB, eC;
-                {
-                    uint32_t m;
-                    asm("v_bfe_i32 %[m], %[R], 1, 1\n\tv_bfi_b32 %[a], %[m], %[MA], %[NA]\n\t"
-                        "v_bfe_i32 %[m], %[R], 0, 1\n\tv_bfi_b32 %[b], %[m], %[MB], %[NB]\n\t"
-                        "v_bfe_i32 %[m], %[R], 2, 1\n\tv_bfi_b32 %[c], %[m], %[CF], %[CN]"
-                        : [a] "=&v"(eA), [b] "=&v"(eB), [c] "=&v"(eC), [m] "=&v"(m)
-                        : [R] "v"(R), [MA] "v"(tMA), [NA] "v"(tNA), [MB] "v"(tMB), [NB] "v"(tNB), [CF] "v"(nF),
-                          [CN] "v"(nN));
-                }
-#else
-                const float eA = (R & 2u) ? tMA : tNA, eB = (R & 1u) ? tMB : tNB, eC = (R & 4u) ? nF : nN;
-#endif
-                // a hit ends the walk after this leaf (glsl:336): no later sibling is tested
-                const bool h = leaf_tests<COUNT>(S, st, (int)lrec.x, (int)lrec.y, fmax3(eA, eB, eC), cnt);
-                todo = h ? 0u : todo;
-            }
-            if (st.hit()) return true;
+            // consecutively in rank order (a leaf pushes nothing): test them right here.
+            if (leaf_kids<COUNT>(S, st, co, keep, tNA, tMA, tNB, tMB, nN, nF, cnt)) return true;
         } else {
             // level depth holds nothing yet (every deeper level is empty), so both writes are
             // harmless when no child survives
