@@ -93,7 +93,8 @@ typedef struct ort_scene_info {
 #define ORT_OPT_WAVE_QUEUE 7       /* 1: resident workgroups whose waves take 64-slot blocks from a queue;
                                       0 (default): one workgroup per 16x16 tile (same pixels) */
 #define ORT_OPT_XCD_SWIZZLE 8      /* workgroup -> tile order (same pixels): 2 (default) each XCD renders
-                                      runs of 8 consecutive raster tiles; 1: each XCD renders 128x128-pixel
+                                      runs of consecutive raster tiles (about 1/15 of a tile row, a power
+                                      of two: 16 at 3840 px); 1: each XCD renders 128x128-pixel
                                       super-tiles; 0: raster order (tile b on XCD b % 8) */
 
 /* Traffic counters (ort_count_traffic), in the REFERENCE layout's terms. */

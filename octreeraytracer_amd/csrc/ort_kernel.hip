@@ -45,6 +45,7 @@ struct PipeArgs {
     TileMap tm;
     int tilesX, tilesY;
     int swizzle;      // ORT_OPT_XCD_SWIZZLE (block_tile)
+    int xrun_log2;    // swizzle 2: log2 of the tiles per XCD run (xcd_run_log2)
     int total;        // path slots = workgroups x 256 (tile-block order, some are holes)
     int sample;       // s of main()'s sample loop
     int last;         // this bounce is the last one (b == maxDepth - 1)
@@ -128,14 +129,24 @@ __device__ inline LdsView setup_lds(unsigned char* smem, const ort::KScene& S) {
 // to XCD b % 8, each XCD with its own L2.  ORT_OPT_XCD_SWIZZLE picks the order:
 //   0  raster: XCD x renders every 8th tile of a tile row -- neighbouring tiles, whose rays
 //      walk the same octree nodes, are spread over all 8 L2s;
-//   2  (default) within every 64 consecutive workgroups the 8 that land on one XCD get 8
-//      consecutive raster tiles (a 128x16-pixel run): c3 +2%, c5 +2% in interleaved A/B
+//   2  (default) within every 8*run consecutive workgroups the `run` that land on one XCD
+//      get `run` consecutive raster tiles (run = xcd_run_log2: 16 tiles, a 256x16-pixel run,
+//      at 3840 px): c3 +2% (8-tile runs) and another +1.7% (16), c5 +2% in interleaved A/B
 //      (tools/ab_stream.py);
 //   1  within every 512 the 64 of one XCD get an 8x8-tile super-tile (128x128 pixels): more
 //      compact but slower at c3 (-1.5% vs raster) -- the run order keeps consecutive
 //      workgroups of one XCD on neighbouring tiles while they are resident together.
 // Each is a bijection on any tile grid (a last partial group keeps raster order; super-tiles at
 // the frame's right/bottom edge are narrower), so the pixels are the same whichever order runs.
+// Swizzle 2's run length: the largest power of two <= tilesX / 15 (1..64), i.e. each XCD's
+// run covers about a fifteenth of a tile row.  Measured (interleaved A/B): 8-tile runs are
+// best at 1920 px (120 tiles per row; 16 is 1.9 % slower), 16-tile runs at 3840 px (+1.2 %
+// over 8).
+inline int xcd_run_log2(int tilesX) {
+    int lr = 0;
+    while (lr < 6 && (2 << lr) * 15 <= tilesX) ++lr;
+    return lr;
+}
 __host__ __device__ inline void block_tile(const PipeArgs& A, int blk, int& bx, int& by) {
     if (!A.swizzle) {
         bx = blk % A.tilesX;
@@ -144,7 +155,9 @@ __host__ __device__ inline void block_tile(const PipeArgs& A, int blk, int& bx, 
     }
     int l = blk;
     if (A.swizzle == 2) {  // raster order in chunks of 8 tiles per XCD
-        if ((blk | 63) < A.tilesX * A.tilesY) l = (blk & ~63) | ((blk & 7) << 3) | ((blk >> 3) & 7);
+        const int lr = A.xrun_log2, run = 1 << lr, group = 8 << lr;
+        if ((blk | (group - 1)) < A.tilesX * A.tilesY)
+            l = (blk & ~(group - 1)) | ((blk & 7) << lr) | ((blk >> 3) & (run - 1));
         bx = l % A.tilesX;
         by = l / A.tilesX;
         return;
@@ -1294,6 +1307,7 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     a.tilesX = tilesX;
     a.tilesY = tilesY;
     a.swizzle = ctx->xcd_swizzle;
+    a.xrun_log2 = xcd_run_log2(tilesX);
     a.total = (int)slots;
     a.exact_only = ctx->exact_only || !ctx->ordered;
     a.refill = ctx->refill;
