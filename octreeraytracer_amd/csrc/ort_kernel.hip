@@ -245,7 +245,9 @@ __global__ void __launch_bounds__(kBlock) ort_raygen_kernel(PipeArgs A) {
 #endif
 constexpr int kChunk = 256;
 
-template <bool COUNT>
+// DEEP: trees deeper than 8 levels (96-bit masks, lean state); depth <= 8 takes the
+// primary-ray walk's 64-bit masks and reversed plane tables (71 VGPRs, 7 waves/SIMD).
+template <bool COUNT, bool DEEP>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ORT_PERSISTENT_WAVES))) ort_trace_persistent(PipeArgs A) {
     extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];  // plane tables: 1 KiB-aligned
     LdsView L = setup_lds<true>(smem, A.S);
@@ -254,7 +256,10 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ORT
     const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     ort::Counters cnt;
     for (int q = 0; q < 6; ++q) cnt.v[q] = 0;
-    ort::FastStateT<ort::Masks96Lean> st;  // lean state: no cached near-plane pointers
+    // depth <= 8 without the inline leaf children: on incoherent bounce rays they cost 9 %
+    // (C3 scene, 8 bounces); the plain 64-bit walk is 5 % faster than the 96-bit one there
+    using Masks = typename std::conditional<DEEP, ort::Masks96Lean, ort::Masks64Plain>::type;
+    ort::FastStateT<Masks> st;
     int k = -1;
     int next = 0, end = 0;   // wave-uniform: remaining work items [next, end) of the wave's chunk
     bool drained = false;    // wave-uniform: the global cursor passed the item count
@@ -1173,7 +1178,10 @@ int ensure(ort_ctx* ctx, DevBuf& b, size_t bytes) {
 template <bool COUNT, bool PRIMARY>
 hipError_t launch_trace_p(int mode, const PipeArgs& a, int blocks, int pblocks, size_t lds, hipStream_t s, bool packet,
                           bool fuse, int qblocks) {
-    if (mode == 0 && pblocks > 0) hipLaunchKernelGGL((ort_trace_persistent<COUNT>), dim3(pblocks), dim3(kBlock), lds, s, a);
+    if (mode == 0 && pblocks > 0) {
+        if (a.S.depth > 8) hipLaunchKernelGGL((ort_trace_persistent<COUNT, true>), dim3(pblocks), dim3(kBlock), lds, s, a);
+        else hipLaunchKernelGGL((ort_trace_persistent<COUNT, false>), dim3(pblocks), dim3(kBlock), lds, s, a);
+    }
     else if (mode == 0 && qblocks > 0 && !(PRIMARY && packet)) {
         const dim3 g(qblocks), t(kBlock);
         if (a.S.depth > 8) {
@@ -1239,13 +1247,15 @@ int queue_blocks(ort_ctx* ctx, bool count, size_t lds, long long needed) {
 
 // Resident workgroups of the persistent trace kernel (a plain launch: extra groups just
 // start when others finish; no grid-wide synchronisation depends on residency).
-int persistent_blocks(int device, bool count, size_t lds, long long needed) {
+int persistent_blocks(int device, bool count, bool deep, size_t lds, long long needed) {
     int per_cu = 0, cus = 0;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
     if (count)
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ort_trace_persistent<true>, kBlock, lds);
+        (void)(deep ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ort_trace_persistent<true, true>, kBlock, lds)
+                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ort_trace_persistent<true, false>, kBlock, lds));
     else
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ort_trace_persistent<false>, kBlock, lds);
+        (void)(deep ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ort_trace_persistent<false, true>, kBlock, lds)
+                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ort_trace_persistent<false, false>, kBlock, lds));
     long long b = (long long)std::max(per_cu, 1) * std::max(cus, 1);
     return (int)std::max(1LL, std::min(b, needed));
 }
@@ -1326,7 +1336,7 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     a.wclock_n = (int)ctx->wclock_n;
     const size_t lds = lds_bytes(mode, ctx->depth, false);
     const size_t lds_exact = lds_bytes(mode, ctx->depth, true);
-    const int pblocks = (mode == 0 && ctx->persistent) ? persistent_blocks(ctx->device, dcounters != nullptr, lds, blocks) : 0;
+    const int pblocks = (mode == 0 && ctx->persistent) ? persistent_blocks(ctx->device, dcounters != nullptr, ctx->depth > 8, lds, blocks) : 0;
     const int exact_blocks = 1024;
     // wave queue: as many workgroups as are resident (never more than the frame has)
     const int qblocks = (mode == 0 && ctx->wave_queue) ? queue_blocks(ctx, dcounters != nullptr, lds, blocks) : 0;

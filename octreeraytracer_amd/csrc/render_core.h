@@ -703,6 +703,11 @@ using FastState = FastStateT<Masks96>;
 struct Masks96Lean : Masks96 {
     static constexpr bool kKeepNear = false;
 };
+// Depth <= 8 walk without the inline leaf children: the persistent bounce kernel's walk
+// (inline leaves pay off on coherent camera rays, not on scattered bounce rays).
+struct Masks64Plain : Masks64 {
+    static constexpr bool kInlineLeaves = false;
+};
 
 // Root test and state setup (glsl:296-311).  Returns false when the root box is missed.
 template <class Masks>

@@ -21,7 +21,7 @@ sys.path.insert(0, str(ROOT))
 import numpy as np  # noqa: E402
 
 
-def worker(spec, config, block):
+def worker(spec, config, block, max_depth=0):
     import ctypes as C
 
     import torch
@@ -31,6 +31,7 @@ def worker(spec, config, block):
     from octreeraytracer_amd import _lib as L
 
     W, H, N, D, M, NS, MD = bench.CONFIGS[config]
+    MD = max_depth or MD
     path, _, opts = spec.partition("@")
     lib = C.CDLL(str(Path(path).resolve()), mode=C.RTLD_LOCAL)
     L._declare(lib)
@@ -63,16 +64,18 @@ def main():
     ap.add_argument("--config", default="c3")
     ap.add_argument("--rounds", type=int, default=12)
     ap.add_argument("--block", type=int, default=10)
+    ap.add_argument("--max-depth", type=int, default=0, help="override the config's ray bounce depth")
     ap.add_argument("--worker", action="store_true")
     args = ap.parse_args()
     if args.worker:
-        return worker(args.libs[0], args.config, args.block)
+        return worker(args.libs[0], args.config, args.block, args.max_depth)
     import bench
     W, H, N, D, M, NS, MD = bench.CONFIGS[args.config]
+    MD = args.max_depth or MD
     procs = []
     for spec in args.libs:
         procs.append(subprocess.Popen([sys.executable, "-u", __file__, spec, "--worker", "--config", args.config,
-                                       "--block", str(args.block)], stdin=subprocess.PIPE, stdout=subprocess.PIPE,
+                                       "--block", str(args.block), "--max-depth", str(args.max_depth)], stdin=subprocess.PIPE, stdout=subprocess.PIPE,
                                       text=True, cwd=str(ROOT)))
         while procs[-1].stdout.readline().strip() != "ready":
             if procs[-1].poll() is not None:
