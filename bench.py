@@ -5,24 +5,35 @@ One step = one frame of primary rays (numSamples=1, maxDepth=1 -> one traversal 
 over the seeded synthetic sphere cloud, rendered by the gfx950 kernel with the scene
 already resident in HBM (octree built on the GPU by ort_build_scene, byte-identical to the
 reference builder; --host-build uses the host builder + upload instead).  `value` counts
-traced rays (octree traversals) per second, which for primary-only configs is W*H/s.  With N GPUs (one process per GPU, torchrun) the frame is
-partitioned into 16-row bands dealt round-robin to the ranks; each rank renders its bands
-into device memory and the bands are gathered to rank 0 over RCCL and de-interleaved into
-the final frame -- the gather is inside the timed region.  Total work per step is one
-frame whatever N is ("scaling": "strong").
+traced rays (octree traversals, every bounce) per second, which for primary-only configs is
+W*H/s.  With N GPUs (one process per GPU) the frame is partitioned into 16-row bands dealt
+round-robin to the ranks; each rank renders its bands into device memory and the bands are
+gathered to rank 0 over RCCL and de-interleaved into the final frame -- the gather is inside
+the timed region.  Total work per step is one frame whatever N is ("scaling": "strong").
+
+`python bench.py --gpus N` (N > 1) without a launcher starts its own N ranks: it runs
+`torch.distributed.run` as a child process before anything touches a GPU and passes rank 0's
+line through.
 
 Prints ONE JSON line on rank 0 (contract in the task description).  Extra keys:
-  roofline      -- dominant kernel (ort_trace_kernel) against the HBM roof, algorithmic
-                   bytes = reference-layout record bytes per SURVEY.md 8(d), counted on the
-                   GPU by the kernel's counting variant, / HIP-event kernel time.
+  roofline      -- the frame's trace kernels (all bounces) against the VALU issue roof: the
+                   kernel is instruction-issue bound.  achieved = VALU
+                   wave-instructions per frame (rocprofv3 PMC SQ_INSTS_VALU, committed under
+                   profiles/pmc_<config>.json) / the trace kernels' summed HIP-event time
+                   measured live in this run; peak = 1024 SIMDs x 2.4 GHz / 2 cycles per
+                   wave64 VALU instruction (MI355X_MICROARCH.md).  hbm_frac and the
+                   reference-layout byte rate are reported beside it.
   cpu_baseline  -- the CPU oracle (line-by-line restatement of the reference shader; the
                    reference itself has no CPU path) on a bounded row sample, rank 0, N=1.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -39,10 +50,15 @@ CONFIGS = {
     "c3": (3840, 2160, 100_000, 8, 0, 1, 1),
     "c5": (7680, 4320, 1_000_000, 10, 1, 1, 4),
 }
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+BASELINE_METRIC = "Mrays/sec at 3840x2160, 100k spheres, depth 8; 1/2/4/8-GPU scaling"
+HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+SIMDS = 1024                # 256 CUs x 4 SIMDs
+CLOCK_GHZ = 2.4             # max engine clock (MI355X_MICROARCH.md)
+VALU_CYCLES_PER_INST = 2    # a wave64 VALU instruction issues over 2 cycles (MI355X_MICROARCH.md)
+VALU_PEAK_GINST = SIMDS * CLOCK_GHZ / VALU_CYCLES_PER_INST  # 1228.8 G wave-instructions/s
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -50,29 +66,147 @@ def parse():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU-baseline threads (0 = the CPUs this job may use: its cgroup CPU quota when it has "
+                    "one, else every CPU of os.sched_getaffinity)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--host-build", action="store_true", help="build the octree on the host and upload it "
                     "(default: ort_build_scene, the GPU builder)")
-    ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"),
-                    help="PMC-measured HBM bytes per launch (written by tools/pmc_traffic.py)")
+    ap.add_argument("--pmc-json", default="",
+                    help="PMC record of the trace kernels (default profiles/pmc_<config>.json, written by "
+                    "tools/summarize_profile.py)")
     ap.add_argument("--inflight", type=int, default=0,
                     help="frames in flight, each on its own context and stream (0 = auto: 1 on one GPU, "
                     "2 with N>1, where a band tile's tail would otherwise idle the GPU)")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="testing only: every rank on GPU 0 with the gloo backend (exercises the N>1 code "
                     "path on a one-GPU box; not a measurement)")
+    ap.add_argument("--emulate", action="store_true",
+                    help="testing only, no GPU: every rank renders its tile with the host build of the kernel's "
+                    "per-pixel code and the bands are gathered with gloo (exercises the launcher, partition and "
+                    "gather on CPU; never a measurement)")
     ap.add_argument("--save", default="", help="rank 0: save the assembled frame (.pfm/.png)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def self_launch(args) -> int:
+    """`bench.py --gpus N` without a launcher: start N ranks with torch.distributed.run as a
+    CHILD process (nothing here has touched a GPU) and pass its output and exit code on."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", str(Path(__file__).resolve())] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def metric_name(cfg: str) -> str:
+    W, H, NSPH, DEPTH, MPN, NS, MAXD = CONFIGS[cfg]
+    if cfg == "c3":
+        return BASELINE_METRIC
+    sph = f"{NSPH // 1_000_000}M" if NSPH % 1_000_000 == 0 else (f"{NSPH // 1000}k" if NSPH >= 1000 else str(NSPH))
+    extra = f", bounce depth {MAXD}" if MAXD > 1 else ""
+    return f"Mrays/sec at {W}x{H}, {sph} spheres, depth {DEPTH}{extra}; 1/2/4/8-GPU scaling"
+
+
+def cpu_info() -> dict:
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    quota = None
+    try:  # cgroup v2 CPU quota, if any
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return {"model": model, "nproc": os.cpu_count() or 1, "affinity": aff, "cgroup_cpu_quota": quota}
+
+
+def lib_sha() -> str:
+    p = ROOT / "octreeraytracer_amd" / "lib" / "libort.so"
+    return hashlib.sha256(p.read_bytes()).hexdigest()[:16] if p.exists() else ""
+
+
+def load_pmc(args, tile_rows) -> dict | None:
+    path = Path(args.pmc_json) if args.pmc_json else ROOT / "profiles" / f"pmc_{args.config}.json"
+    if not path.exists():
+        return None
+    try:
+        rec = json.loads(path.read_text())
+    except (OSError, ValueError):
+        return None
+    if rec.get("config") != args.config:
+        return None
+    rec["_path"] = str(path.relative_to(ROOT)) if path.is_relative_to(ROOT) else str(path)
+    return rec
+
+
+def roofline(pmc, counts, full_traversals, alg_bytes, trace_ms_avg, kernels_ran):
+    """The trace kernels of one frame against the VALU issue roof (see the module docstring)."""
+    t = trace_ms_avg * 1e-3
+    r = {"bound": "valu", "achieved": None, "peak": round(VALU_PEAK_GINST, 1), "unit": "Gwave-inst/s (VALU issue)",
+         "frac": None, "traffic": None, "kernels": kernels_ran, "trace_ms_per_frame": round(trace_ms_avg, 4)}
+    r["ref_layout_equiv_GBs"] = round(alg_bytes / t / 1e9, 1)
+    r["algorithmic_bytes_per_frame"] = int(alg_bytes)
+    r["ref_layout_bytes_per_ray"] = round(alg_bytes / max(1, counts["traversals"]), 1)
+    r["counts"] = counts
+    if pmc is None:
+        r["note"] = "no PMC record for this config (profiles/pmc_<config>.json): issue rate unmeasured"
+        return r
+    tr = pmc["trace"]
+    # per-rank share of the full-frame counters (N > 1: the rank's traversals / the frame's)
+    share = counts["traversals"] / max(1, full_traversals) if full_traversals else 1.0
+    insts = tr["valu_insts_per_frame"] * share
+    achieved = insts / t / 1e9
+    r["achieved"] = round(achieved, 1)
+    r["frac"] = round(achieved / VALU_PEAK_GINST, 4)
+    r["valu_lane_utilization"] = round(tr["valu_lane_utilization"], 4)
+    r["useful_lane_frac"] = round(r["frac"] * tr["valu_lane_utilization"], 4)
+    r["valu_insts_per_wave"] = round(tr["valu_insts_per_wave"], 1)
+    r["salu_insts_per_wave"] = round(tr["salu_insts_per_wave"], 1)
+    if tr.get("hbm_bytes_per_frame") is not None:
+        traffic = tr["hbm_bytes_per_frame"] * share
+        r["traffic"] = int(traffic)
+        r["hbm_GBs"] = round(traffic / t / 1e9, 1)
+        r["hbm_frac"] = round(traffic / t / 1e9 / HBM_PEAK_GBS, 5)
+    r["pmc_source"] = pmc["_path"]
+    r["pmc_trace_ms_per_frame"] = round(tr["trace_ms_per_frame"], 4)
+    r["pmc_build_sha"] = pmc.get("lib_sha", "")
+    r["pmc_matches_build"] = pmc.get("lib_sha", "") == lib_sha()
+    if share != 1.0:
+        r["pmc_scaled_by_traversal_share"] = round(share, 5)
+    return r
 
 
 def main():
     args = parse()
     W, H, NSPH, DEPTH, MPN, NS, MAXD = CONFIGS[args.config]
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = 0 if args.rehearse_one_gpu else int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.emulate:
+        return emulate(args, world, rank)
+    local = 0 if args.rehearse_one_gpu else int(os.environ.get("LOCAL_RANK", "0"))
     inflight = args.inflight or (1 if world == 1 else 2)
     if inflight > 1:
         # frames in flight only overlap when their streams sit on different hardware queues;
@@ -120,14 +254,12 @@ def main():
     # renders, and frame k+1 (next context, next stream) fills the tail of frame k
     nslot = inflight + 1
     outs = [torch.empty((tile.rows, W, 3), dtype=torch.float32, device="cuda") for _ in range(nslot)]
-    out = outs[0]
     gather = FrameGather(dist, W, H, world, rank, "cuda", depth=nslot)
     # each context's own stream (never the HIP null stream, handle 0, which the C ABI reads
     # as "no stream" and renders synchronously)
     streams = [torch.cuda.ExternalStream(x.stream_handle()) for x in rs]
-    stream = streams[0]
     gstream = torch.cuda.Stream()
-    torch.cuda.set_stream(stream)
+    torch.cuda.set_stream(streams[0])
 
     pending = []
 
@@ -171,8 +303,12 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    kern_ms = [a.elapsed_time(b) for a, b in evs]          # whole per-frame pipeline (trace+shade)
-    trace_ms = r.trace_times_ms(min(-(-args.steps // inflight), 64))  # dominant kernel, context 0's timed frames
+    kern_ms = [a.elapsed_time(b) for a, b in evs]          # whole per-frame pipeline (trace+shade+sort)
+    nframes0 = min(-(-args.steps // inflight), 64)          # context 0's timed frames
+    first_trace_ms = r.trace_times_ms(nframes0)             # bounce-0 trace kernel of each frame
+    ftrace = r.frame_trace_times_ms(nframes0)               # every trace kernel of each frame, summed
+    trace_ms = [m for m, _ in ftrace]
+    launches = sorted({n for _, n in ftrace})
     t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -182,8 +318,6 @@ def main():
     # of a step = traversals summed over the ranks (W*H*spp for primary-only configs)
     counts = r.count_traffic(p, tile)
     alg_bytes = ort.algorithmic_bytes(counts)
-    kern_avg_ms = float(np.mean(kern_ms))
-    trace_avg_ms = float(np.mean(trace_ms))
     trav = torch.tensor([counts["traversals"]], dtype=torch.float64, device="cuda")
     if world > 1:
         dist.all_reduce(trav)
@@ -193,18 +327,10 @@ def main():
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
         value = rays_per_frame * args.steps / elapsed / 1e6
-        achieved = alg_bytes / (trace_avg_ms * 1e-3) / 1e9
-        traffic = None
-        tj = Path(args.traffic_json)
-        if tj.exists():
-            try:
-                tr = json.loads(tj.read_text())
-                if tr.get("config") == args.config and tr.get("tile_rows") == tile.rows:
-                    traffic = int(tr.get("hbm_bytes_per_launch"))
-            except Exception:
-                traffic = None
+        pmc = load_pmc(args, tile.rows)
+        kernels = trace_kernel_names(args.config, info, MAXD, NS)
         result = {
-            "metric": "Mrays/sec at 3840x2160, 100k spheres, depth 8; 1/2/4/8-GPU scaling",
+            "metric": metric_name(args.config),
             "value": round(value, 2),
             "unit": "Mrays/s",
             "n_gpus": world,
@@ -226,32 +352,22 @@ def main():
                 else "full frame", "frames_in_flight": inflight, "rays_per_step": rays_per_frame, "rays": "traced rays (octree traversals), "
                 "all bounces and ranks",
             },
-            "frame_gpu_ms_avg": round(kern_avg_ms, 4),
-            "trace_kernel_ms_avg": round(trace_avg_ms, 4),
-            "trace_kernel_ms_min": round(float(np.min(trace_ms)), 4),
-            "roofline": {
-                "bound": "hbm",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "algorithmic_bytes_per_launch": int(alg_bytes),
-                "bytes_per_ray": round(alg_bytes / max(1, counts["pixels"]), 1),
-                "counts": counts,
-                "kernel": "ort_trace_compact<false,true,true> (camera rays + octree walk + shading)",
-                "note": "achieved = reference-layout record bytes (SURVEY.md 8(d)) the reference walk reads per "
-                        "frame / trace-kernel time; this kernel reads far fewer bytes (compact layout, L2/MALL "
-                        "residency) and is instruction-issue bound -- see traffic and DESIGN.md",
-            },
+            "frame_gpu_ms_avg": round(float(np.mean(kern_ms)), 4),
+            "trace_kernels_ms_avg": round(float(np.mean(trace_ms)), 4),
+            "trace_launches_per_frame": launches,
+            "first_trace_kernel_ms_avg": round(float(np.mean(first_trace_ms)), 4),
+            "first_trace_kernel_ms_min": round(float(np.min(first_trace_ms)), 4),
+            "roofline": roofline(pmc, counts, (pmc or {}).get("traversals_per_frame"), alg_bytes,
+                                 float(np.mean(trace_ms)), kernels),
             "setup": setup,
+            "build_sha": lib_sha(),
         }
         if world == 1 and not args.no_cpu_baseline:
             if tree is None:
                 t0 = time.time()
                 tree = ort.build_octree(spheres, DEPTH, MPN)  # the oracle walks the host tree
                 setup["host_octree_build_s"] = round(time.time() - t0, 3)
-            result["cpu_baseline"] = cpu_baseline(spheres, tree, p, args.cpu_seconds)
+            result["cpu_baseline"] = cpu_baseline(spheres, tree, p, args.cpu_seconds, args.cpu_threads)
         if args.save:
             img = frame.cpu().numpy()
             from octreeraytracer_amd import image
@@ -264,10 +380,65 @@ def main():
         print(json.dumps(result), flush=True)
 
 
-def cpu_baseline(spheres, tree, p, budget_s):
+def trace_kernel_names(cfg, info, maxd, ns):
+    """The trace kernels a frame of this config launches (ort_kernel.hip render_impl)."""
+    deep = info["tree_depth"] > 8
+    if maxd == 1 and ns == 1:
+        return ["ort_trace_compact%s<false, true, true> (camera rays + walk + shading)" % ("_deep" if deep else "")]
+    return ["ort_trace_compact%s<false, true, false> (camera rays + walk)" % ("_deep" if deep else ""),
+            "ort_trace_persistent<false, %s> (bounces >= 1, sorted alive paths, lane refill)" % str(deep).lower()]
+
+
+def emulate(args, world, rank):
+    """--emulate: the N>1 control path on CPU (gloo), tiles rendered by the host build of the
+    kernel's per-pixel code.  Prints a JSON line marked as emulation; never a measurement."""
+    import torch
+    import torch.distributed as dist
+
+    import octreeraytracer_amd as ort
+    from octreeraytracer_amd.distributed import FrameGather, rank_tile
+    from octreeraytracer_amd.renderer import emulate_render_host
+    W, H, NSPH, DEPTH, MPN, NS, MAXD = CONFIGS[args.config]
+    if world > 1:
+        dist.init_process_group("gloo")
+    spheres = ort.random_spheres(NSPH, args.seed)
+    tree = ort.build_octree(spheres, DEPTH, MPN)
+    p = ort.FrameParams.default_camera(W, H, num_samples=NS, max_depth=MAXD)
+    tile = rank_tile(W, H, rank, world)
+    gather = FrameGather(dist, W, H, world, rank, "cpu")
+    t0 = time.perf_counter()
+    frame = None
+    trav = 0
+    for _ in range(args.steps):
+        local, counts = emulate_render_host(spheres, tree, p, tile)
+        trav = counts["traversals"]
+        frame = gather(torch.from_numpy(local))
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed, float(trav)], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+        dist.all_reduce(t[:1], op=dist.ReduceOp.MAX)
+    if rank == 0:
+        digest = hashlib.sha256(np.ascontiguousarray(frame.numpy()).tobytes()).hexdigest()
+        print(json.dumps({"metric": metric_name(args.config), "value": round(float(t[1]) * args.steps / float(t[0]) / 1e6, 4),
+                          "unit": "Mrays/s", "n_gpus": world, "steps": args.steps, "warmup": 0,
+                          "ms_per_step": round(float(t[0]) / args.steps * 1e3, 3), "higher_is_better": True,
+                          "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+                          "data": "EMULATION (host build of the kernel code, gloo): a control-path test, not a "
+                                  "measurement", "config": {"workload": args.config, "width": W, "height": H},
+                          "frame_sha256": digest}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(spheres, tree, p, budget_s, threads=0):
     """Oracle on the host cores over evenly spaced full rows, sized to ~budget_s of wall time."""
     from oracle import oracle
-    threads = min(16, os.cpu_count() or 1)
+    ci = cpu_info()
+    # the job's CPU share: a cgroup quota (the GPU box grants 16 CPUs of a 256-thread host) caps
+    # throughput, and more threads than the quota only get throttled (measured: 256 threads
+    # on a 16-CPU quota ran the oracle 2.3x slower than 16)
+    threads = threads or (max(1, int(ci["cgroup_cpu_quota"])) if ci["cgroup_cpu_quota"] else ci["affinity"])
 
     def run(n):
         stride = max(1, p.height // n)
@@ -276,8 +447,8 @@ def cpu_baseline(spheres, tree, p, budget_s):
         return time.perf_counter() - t0, stride
 
     n = 2 * threads
-    dt, _ = run(n)  # calibration sample
-    n = int(max(n, min(p.height, n * budget_s / max(dt, 1e-3))))
+    dt, _ = run(min(n, p.height))  # calibration sample
+    n = int(max(min(n, p.height), min(p.height, n * budget_s / max(dt, 1e-3))))
     dt, stride = run(n)
     rays = n * p.width * p.num_samples
     # one core (report all cores and 1 core), a smaller row sample
@@ -289,7 +460,9 @@ def cpu_baseline(spheres, tree, p, budget_s):
     rays1 = n1 * p.width * p.num_samples
     return {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
             "sample": f"{n} of {p.height} rows (every {stride}th), {rays} camera rays, {dt:.1f} s wall; "
-                      f"oracle/ort_oracle.c -O3, OpenMP dynamic over rows",
+                      f"oracle/ort_oracle.c -O3, OpenMP dynamic over rows, {threads} threads",
+            "cpu_model": ci["model"], "nproc": ci["nproc"], "affinity_cpus": ci["affinity"],
+            "cgroup_cpu_quota": ci["cgroup_cpu_quota"],
             "value_1core": round(rays1 / dt1 / 1e6, 3),
             "sample_1core": f"{n1} rows (every {stride1}th), {rays1} camera rays, {dt1:.1f} s wall, 1 thread"}
 

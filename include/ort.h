@@ -180,6 +180,13 @@ int ort_last_trace_ms(ort_ctx* ctx, float* ms);
  * written, or a negative ORT_ERR_* code. */
 int ort_trace_times_ms(ort_ctx* ctx, int n, float* ms);
 
+/* Per frame, the summed duration of ALL its trace kernels (every sample and bounce: camera
+ * rays and the bounce >= 1 walks; at most the first 16 trace launches of a frame are timed),
+ * last n frames (at most 64), oldest first; launches[i] (may be NULL) receives how many
+ * launches frame i summed.  Returns how many frames were written, or a negative ORT_ERR_*.
+ * Shading, path sorting and the deferred-ray exact walk are not included. */
+int ort_frame_trace_times_ms(ort_ctx* ctx, int n, float* ms, int32_t* launches);
+
 /* Run the counting variant of the kernel over the tile and return, summed over all
  * pixels, the reference-layout work counters ORT_COUNT_* (counts[ORT_COUNT_N]). */
 int ort_count_traffic(ort_ctx* ctx, const ort_params* params, const ort_tile* tile, uint64_t* counts);

@@ -38,7 +38,7 @@ COUNT_NAMES = ("nodes_popped", "child_records", "leaf_objects", "accepted_hits",
 EXPORTED_SYMBOLS = (
     "ort_create", "ort_destroy", "ort_last_error", "ort_set_option", "ort_upload_scene",
     "ort_upload_octree_nodes", "ort_scene_get_info", "ort_render", "ort_last_kernel_ms", "ort_last_trace_ms",
-    "ort_trace_times_ms", "ort_build_scene", "ort_scene_export_octree", "ort_last_build_ms", "ort_get_stream",
+    "ort_trace_times_ms", "ort_frame_trace_times_ms", "ort_build_scene", "ort_scene_export_octree", "ort_last_build_ms", "ort_get_stream",
     "ort_count_traffic", "ort_scene_random", "ort_scene_prebuilt", "ort_scene_debug",
     "ort_octree_build", "ort_octree_sizes", "ort_octree_export", "ort_octree_nodes",
     "ort_octree_indices", "ort_octree_free", "ort_camera_view", "ort_version",
@@ -98,6 +98,7 @@ def _declare(lib):
         "ort_last_kernel_ms": (C.c_int, [_vp, _fp]),
         "ort_last_trace_ms": (C.c_int, [_vp, _fp]),
         "ort_trace_times_ms": (C.c_int, [_vp, C.c_int, _fp]),
+        "ort_frame_trace_times_ms": (C.c_int, [_vp, C.c_int, _fp, _ip]),
         "ort_count_traffic": (C.c_int, [_vp, C.POINTER(OrtParams), C.POINTER(OrtTile), _u64p]),
         "ort_scene_random": (C.c_int, [C.c_int32, C.c_uint32, _fp, _fp, _fp]),
         "ort_scene_prebuilt": (C.c_int, [_fp, _fp, _fp, _ip]),

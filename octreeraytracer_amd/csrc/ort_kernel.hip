@@ -231,9 +231,11 @@ __global__ void __launch_bounds__(kBlock) ort_raygen_kernel(PipeArgs A) {
 // chunk, MI355X_MICROARCH.md 'dequeue') and hands the next slots of its chunk to lanes
 // that finished, so the wave stays full until the queue drains.  Rays the fast walk
 // cannot take are appended to the defer list for ort_trace_exact.
-// Waves per SIMD (minimum, amdgpu_waves_per_eu): the per-lane trace kernels run at 8 (57 / 60
-// VGPRs, spill-free); the persistent kernel at 6 (79 VGPRs) -- forced to 8 it spills and C5
-// runs 11 % slower, at 7 no faster (tools/ab_stream.py).
+// Waves per SIMD (minimum, amdgpu_waves_per_eu): the per-lane trace kernels run at 8 (56-60
+// VGPRs, spill-free; tools/kernel_resources.py); the persistent kernel's hint is 5 and the
+// compiler lands at 79 VGPRs / 6 waves for the 96-bit (depth > 8) walk and at 71 VGPRs /
+// 7 waves for the 64-bit one -- forced to 8 the 96-bit walk spills and C5 runs 11 % slower,
+// at 7 no faster (tools/ab_stream.py).
 #ifndef ORT_PERSISTENT_WAVES
 #define ORT_PERSISTENT_WAVES 5
 #endif
@@ -862,7 +864,9 @@ struct ort_ctx {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     static constexpr int kRing = 64;           // trace-kernel timing of the last 64 frames
-    hipEvent_t tr0[kRing] = {}, tr1[kRing] = {};
+    static constexpr int kSeg = 16;            // ... of their first 16 trace launches each
+    hipEvent_t tr0[kRing][kSeg] = {}, tr1[kRing][kSeg] = {};  // segment 0 created up front, others lazily
+    int tseg[kRing] = {};                      // trace launches timed in each frame slot
     long long frames = 0;                      // frames whose first trace kernel was timed
     bool timed = false;
     std::string err;
@@ -1342,7 +1346,8 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     const int qblocks = (mode == 0 && ctx->wave_queue) ? queue_blocks(ctx, dcounters != nullptr, lds, blocks) : 0;
     hipError_t e;
     HIPCHK(ctx, hipEventRecord(ctx->ev0, s));
-    bool first_trace = true;
+    const int fslot = (int)(ctx->frames % ort_ctx::kRing);  // this frame's timing slot
+    ctx->tseg[fslot] = 0;
     for (int smp = 0; smp < ns; ++smp) {
         a.sample = smp;
         a.rays_stored = pers_all && pblocks > 0;
@@ -1358,17 +1363,22 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
             a.last = (b == bounces - 1);
             if (!a.nobounce) {
                 HIPCHK(ctx, hipMemsetAsync(ctx->defer_count.p, 0, 64, s));
-                const int slot = (int)(ctx->frames % ort_ctx::kRing);
-                if (first_trace) HIPCHK(ctx, hipEventRecord(ctx->tr0[slot], s));
+                const int slot = fslot;
+                const int seg = ctx->tseg[slot];
+                const bool timed = seg < ort_ctx::kSeg;  // every trace launch of the frame, up to kSeg
+                if (timed && !ctx->tr0[slot][seg]) {
+                    HIPCHK(ctx, hipEventCreate(&ctx->tr0[slot][seg]));
+                    HIPCHK(ctx, hipEventCreate(&ctx->tr1[slot][seg]));
+                }
+                if (timed) HIPCHK(ctx, hipEventRecord(ctx->tr0[slot][seg], s));
                 const bool prim = (b == 0) && !a.rays_stored;
                 const int pb = (pers_all || (pers_bounce && b > 0)) ? pblocks : 0;
                 e = dcounters ? launch_trace<true>(mode, prim, a, (int)blocks, pb, lds, s, ctx->packet != 0, fuse, qblocks)
                               : launch_trace<false>(mode, prim, a, (int)blocks, pb, lds, s, ctx->packet != 0, fuse, qblocks);
                 if (e != hipSuccess) return hip_fail(ctx, e, "trace kernel launch");
-                if (first_trace) {
-                    HIPCHK(ctx, hipEventRecord(ctx->tr1[slot], s));
-                    ctx->frames += 1;
-                    first_trace = false;
+                if (timed) {
+                    HIPCHK(ctx, hipEventRecord(ctx->tr1[slot][seg], s));
+                    ctx->tseg[slot] = seg + 1;
                 }
                 if (mode == 0) {
                     const bool prim = (b == 0) && !a.rays_stored;
@@ -1402,6 +1412,7 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
             }
         }
     }
+    if (ctx->tseg[fslot] > 0) ctx->frames += 1;
     if (!direct) {
         hipLaunchKernelGGL(ort_finalize_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, s, a);
         if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "ort_finalize_kernel launch");
@@ -1440,7 +1451,7 @@ int ort_create(int device, ort_ctx** out) {
         return rc;
     }
     for (int i = 0; i < ort_ctx::kRing; ++i) {
-        if ((e = hipEventCreate(&c->tr0[i])) != hipSuccess || (e = hipEventCreate(&c->tr1[i])) != hipSuccess) {
+        if ((e = hipEventCreate(&c->tr0[i][0])) != hipSuccess || (e = hipEventCreate(&c->tr1[i][0])) != hipSuccess) {
             const int rc = hip_fail(nullptr, e, "ort_create: events");
             ort_destroy(c);
             return rc;
@@ -1475,10 +1486,11 @@ int ort_destroy(ort_ctx* ctx) {
     for (DevBuf* b : pipe) free_buf(*b);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
-    for (int i = 0; i < ort_ctx::kRing; ++i) {
-        if (ctx->tr0[i]) (void)hipEventDestroy(ctx->tr0[i]);
-        if (ctx->tr1[i]) (void)hipEventDestroy(ctx->tr1[i]);
-    }
+    for (int i = 0; i < ort_ctx::kRing; ++i)
+        for (int j = 0; j < ort_ctx::kSeg; ++j) {
+            if (ctx->tr0[i][j]) (void)hipEventDestroy(ctx->tr0[i][j]);
+            if (ctx->tr1[i][j]) (void)hipEventDestroy(ctx->tr1[i][j]);
+        }
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return ORT_OK;
@@ -1651,9 +1663,29 @@ int ort_trace_times_ms(ort_ctx* ctx, int n, float* ms) {
     const int k = (int)std::min<long long>(n, have);
     for (int i = 0; i < k; ++i) {
         const int slot = (int)((ctx->frames - k + i) % ort_ctx::kRing);
-        if (hipEventSynchronize(ctx->tr1[slot]) != hipSuccess ||
-            hipEventElapsedTime(&ms[i], ctx->tr0[slot], ctx->tr1[slot]) != hipSuccess)
+        if (hipEventSynchronize(ctx->tr1[slot][0]) != hipSuccess ||
+            hipEventElapsedTime(&ms[i], ctx->tr0[slot][0], ctx->tr1[slot][0]) != hipSuccess)
             return -ORT_ERR_HIP;
+    }
+    return k;
+}
+
+int ort_frame_trace_times_ms(ort_ctx* ctx, int n, float* ms, int32_t* launches) {
+    if (!ctx || !ms || n < 0) return -ORT_ERR_INVALID_ARG;
+    const long long have = std::min<long long>(ctx->frames, ort_ctx::kRing);
+    const int k = (int)std::min<long long>(n, have);
+    for (int i = 0; i < k; ++i) {
+        const int slot = (int)((ctx->frames - k + i) % ort_ctx::kRing);
+        float sum = 0.0f;
+        for (int j = 0; j < ctx->tseg[slot]; ++j) {
+            float t = 0.0f;
+            if (hipEventSynchronize(ctx->tr1[slot][j]) != hipSuccess ||
+                hipEventElapsedTime(&t, ctx->tr0[slot][j], ctx->tr1[slot][j]) != hipSuccess)
+                return -ORT_ERR_HIP;
+            sum += t;
+        }
+        ms[i] = sum;
+        if (launches) launches[i] = ctx->tseg[slot];
     }
     return k;
 }

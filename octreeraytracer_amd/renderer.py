@@ -217,8 +217,13 @@ class Renderer:
             self._check(self._lib.ort_render(self._ctx, C.byref(p), C.byref(t), out.ctypes.data_as(C.c_void_p), 0, s))
             return out
         ptr = out.data_ptr() if hasattr(out, "data_ptr") else int(out)
-        if hasattr(out, "numel"):
-            assert out.numel() >= tile.rows * tile.width * 3 and out.is_contiguous()
+        if hasattr(out, "numel"):  # a torch tensor: float32, contiguous, on this context's GPU
+            import torch
+            if out.dtype != torch.float32 or not out.is_contiguous() or out.numel() < tile.rows * tile.width * 3:
+                raise ValueError(f"render: out must be a contiguous float32 tensor of >= {tile.rows * tile.width * 3} "
+                                 f"elements (got {out.dtype}, {out.numel()}, contiguous={out.is_contiguous()})")
+            if out.device.type != "cuda" or out.device.index != self.device:
+                raise ValueError(f"render: out is on {out.device}, the context renders on cuda:{self.device}")
         self._check(self._lib.ort_render(self._ctx, C.byref(p), C.byref(t), C.c_void_p(ptr), 1, s))
         return out
 
@@ -240,6 +245,15 @@ class Renderer:
         if k < 0:
             L.check(-k, self._ctx)
         return [buf[i] for i in range(k)]
+
+    def frame_trace_times_ms(self, n: int):
+        """Per frame (last n <= 64, oldest first): (summed ms of all its trace kernels, launches)."""
+        buf = (C.c_float * max(1, n))()
+        nl = (C.c_int32 * max(1, n))()
+        k = self._lib.ort_frame_trace_times_ms(self._ctx, int(n), buf, nl)
+        if k < 0:
+            L.check(-k, self._ctx)
+        return [(buf[i], nl[i]) for i in range(k)]
 
     def count_traffic(self, params: FrameParams, tile: Tile | None = None) -> dict:
         tile = tile or Tile.full(params)

@@ -117,3 +117,34 @@ def test_partition_covers_every_row_once():
                           for t in tiles])
             f = assemble(g, H, world)
             assert np.array_equal(f[:, 0, 0], np.arange(H, dtype=np.float32))
+
+
+def _bench_line(out: str) -> dict:
+    import json
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_self_launch(world):
+    """`bench.py --gpus N` with no launcher starts its own N ranks (torch.distributed.run as a
+    child process) and prints rank 0's line only; --emulate renders on the host and gathers
+    with gloo.  The assembled frame equals the oracle's single-process frame."""
+    import hashlib
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, str(root / "bench.py"), "--gpus", str(world), "--emulate", "--config", "c1",
+                        "--steps", "1", "--warmup", "0"], capture_output=True, text=True, env=env, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = _bench_line(r.stdout)
+    assert line["n_gpus"] == world and "EMULATION" in line["data"]
+    import octreeraytracer_amd as ort
+    from oracle import oracle
+    s = ort.random_spheres(100, 42)
+    t = ort.build_octree(s, 4, 0)
+    ref = oracle.render(s, t, ort.FrameParams.default_camera(256, 256))
+    assert line["frame_sha256"] == hashlib.sha256(np.ascontiguousarray(ref).tobytes()).hexdigest()

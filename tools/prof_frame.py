@@ -1,8 +1,9 @@
-"""Render N frames of a bench config with only the production kernel (no counting pass):
-the command profiled by tools/profile_box.sh under rocprofv3 PMC passes."""
+"""Render N frames of a bench config with only the production kernels, then (untimed) the
+counting pass: the command profiled by tools/profile_box.sh under rocprofv3 PMC passes.
+--meta writes {frames, traversals_per_frame, lib_sha} for tools/summarize_profile.py."""
 import argparse
+import json
 import sys
-import time
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
@@ -18,6 +19,7 @@ ap.add_argument("--config", default="c3")
 ap.add_argument("--frames", type=int, default=3)
 ap.add_argument("--layout", type=int, default=-1)
 ap.add_argument("--both", action="store_true", help="render with the packet walk on, then off")
+ap.add_argument("--meta", default="", help="write frames / traversals / build id here (JSON)")
 a = ap.parse_args()
 W, H, N, D, M, NS, MD = bench.CONFIGS[a.config]
 s = ort.random_spheres(N, 42)
@@ -40,3 +42,9 @@ if a.both:
         r.render(p, out=out)
         ms.append(r.last_kernel_ms())
     print(f"{a.config} per-lane walk kernel ms: {['%.3f' % m for m in ms]}", flush=True)
+if a.meta:
+    counts = r.count_traffic(p)  # COUNT=true kernel instances: excluded from the PMC sums by name
+    Path(a.meta).write_text(json.dumps({"config": a.config, "frames": a.frames * (2 if a.both else 1),
+                                        "traversals_per_frame": counts["traversals"], "counts": counts,
+                                        "lib_sha": bench.lib_sha(), "tile_rows": H}))
+r.close()

@@ -1,82 +1,147 @@
-"""Summarise a tools/profile_box.sh output directory into profiles/<tag>.json + .md.
-usage: python tools/summarize_profile.py gpurun_out/<tag> profiles/<name>"""
+"""Summarise a tools/profile_box.sh output directory into profiles/<name>.json + .md and the
+PMC record bench.py reads (profiles/pmc_<config>.json).
+
+usage: python tools/summarize_profile.py gpurun_out/<tag> profiles/<name> <config> [--no-record]
+
+Trace kernels = the production (COUNT=false) instances of the walk kernels that
+ort_frame_trace_times_ms times: ort_trace_compact[_deep][_q], ort_trace_persistent,
+ort_trace_packet, ort_trace_kernel.  Per-frame figures = the sum over a frame's launches."""
 import csv
 import json
+import re
 import sys
 from collections import defaultdict
 from pathlib import Path
 
-src, dst = Path(sys.argv[1]), Path(sys.argv[2])
-KERNEL = sys.argv[3] if len(sys.argv) > 3 else "ort_trace_compact<false, true, true>"
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
+src, dst, cfg = Path(args[0]), Path(args[1]), args[2]
+record = "--no-record" not in sys.argv
+TRACE_RE = re.compile(r"ort_trace_(compact_deep_q|compact_q|compact_deep|compact|persistent|packet|kernel)<(false|0)")
 
+
+def short(name):
+    n = name.replace("(anonymous namespace)::", "").replace("void ", "")
+    return n.split("(")[0]
+
+
+def is_trace(name):
+    return bool(TRACE_RE.search(short(name)))
+
+
+meta = json.loads((src / "meta.json").read_text())
+bargs = json.loads((src / "bench_args.json").read_text()) if (src / "bench_args.json").exists() else {}
+bench_frames = bargs.get("steps", 10) + bargs.get("warmup", 3)
+
+# kernel trace of bench.py: per-kernel stats and per-frame trace-kernel time
 stats = {}
-ks = next(src.glob("trace/*kernel_stats.csv"), None)
+ks = next(src.glob("trace/**/*kernel_stats.csv"), None)
 if ks:
     for r in csv.DictReader(open(ks)):
         stats[r["Name"]] = {k: r[k] for k in ("Calls", "AverageNs", "MinNs", "MaxNs", "Percentage")}
+trace_ns_total = 0.0
+trace_launches = 0
+kt = next(src.glob("trace/**/*kernel_trace.csv"), None)
+if kt:
+    for r in csv.DictReader(open(kt)):
+        if is_trace(r["Kernel_Name"]):
+            trace_ns_total += float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
+            trace_launches += 1
+else:  # from the stats: production trace kernels' total time
+    for n, st in stats.items():
+        if is_trace(n):
+            trace_ns_total += float(st["AverageNs"]) * int(st["Calls"])
+            trace_launches += int(st["Calls"])
 
-pmc = defaultdict(list)
-for f in src.glob("pmc_*/pmc_counter_collection.csv"):
+# PMC passes over tools/prof_frame.py (meta["frames"] production frames + one counting pass)
+per_kernel = defaultdict(lambda: defaultdict(float))
+launches = defaultdict(lambda: defaultdict(int))
+for f in src.glob("pmc_*/**/pmc_counter_collection.csv"):
     for r in csv.DictReader(open(f)):
-        if KERNEL in r["Kernel_Name"]:
-            pmc[r["Counter_Name"]].append(float(r["Counter_Value"]))
-per_launch = {k: sum(v) / len(v) for k, v in pmc.items()}
+        n = short(r["Kernel_Name"])
+        per_kernel[n][r["Counter_Name"]] += float(r["Counter_Value"])
+        launches[n][r["Counter_Name"]] += 1
+frames = meta["frames"]
+kernels = {}
+for n, cs in per_kernel.items():
+    k = {"trace": is_trace(n)}
+    for c, v in cs.items():
+        k[c + "_per_frame"] = v / frames
+    k["launches_per_frame"] = max(launches[n].values()) / frames
+    kernels[n] = k
 
-res = {"kernel": KERNEL, "kernel_stats": stats, "pmc_per_launch": per_launch}
-avg_ns = None
-for name, st in stats.items():
-    if KERNEL in name:
-        avg_ns = float(st["AverageNs"])
-res["avg_ns"] = avg_ns
-d = {}
-if "FETCH_SIZE" in per_launch and "WRITE_SIZE" in per_launch:
+
+def tsum(counter):
+    return sum(k.get(counter + "_per_frame", 0.0) for k in kernels.values() if k["trace"])
+
+
+trace = {
+    "kernels": sorted(n for n, k in kernels.items() if k["trace"]),
+    "valu_insts_per_frame": tsum("SQ_INSTS_VALU"),
+    "salu_insts_per_frame": tsum("SQ_INSTS_SALU"),
+    "waves_per_frame": tsum("SQ_WAVES"),
+    "trace_ms_per_frame": trace_ns_total / bench_frames / 1e6 if trace_ns_total else None,
+    "trace_launches_per_frame": trace_launches / bench_frames,
+}
+w = max(1.0, trace["waves_per_frame"])
+trace["valu_insts_per_wave"] = trace["valu_insts_per_frame"] / w
+trace["salu_insts_per_wave"] = trace["salu_insts_per_frame"] / w
+act = tsum("SQ_ACTIVE_INST_VALU")
+trace["valu_lane_utilization"] = tsum("SQ_THREAD_CYCLES_VALU") / max(1.0, 64 * act)
+if any("FETCH_SIZE_per_frame" in k for k in kernels.values()):
     # MI355X_MICROARCH.md HBM: FETCH_SIZE (KB) reads 1/2 of wide streaming reads on gfx950 -> x2
-    d["hbm_bytes_per_launch"] = per_launch["FETCH_SIZE"] * 1024 * 2 + per_launch["WRITE_SIZE"] * 1024
-    d["fetch_bytes_raw"] = per_launch["FETCH_SIZE"] * 1024
-    d["write_bytes"] = per_launch["WRITE_SIZE"] * 1024
-    if avg_ns:
-        d["hbm_GBs"] = d["hbm_bytes_per_launch"] / avg_ns
-if "TCC_HIT_sum" in per_launch:
-    h, m = per_launch["TCC_HIT_sum"], per_launch["TCC_MISS_sum"]
-    d["l2_hit_rate"] = h / max(1.0, h + m)
-if "TCC_EA0_RDREQ_DRAM_sum" in per_launch:
-    d["dram_read_frac_of_ea_reads"] = per_launch["TCC_EA0_RDREQ_DRAM_sum"] / max(1.0, per_launch["TCC_EA0_RDREQ_sum"])
-if "SQ_THREAD_CYCLES_VALU" in per_launch:
-    d["valu_lane_utilization"] = per_launch["SQ_THREAD_CYCLES_VALU"] / max(1.0, 64 * per_launch["SQ_ACTIVE_INST_VALU"])
-if "SQ_INSTS_VALU" in per_launch:
-    w = per_launch.get("SQ_WAVES", 1.0)
-    d["valu_insts_per_wave"] = per_launch["SQ_INSTS_VALU"] / w
-    d["lds_insts_per_wave"] = per_launch.get("SQ_INSTS_LDS", 0) / w
-    d["vmem_rd_insts_per_wave"] = per_launch.get("SQ_INSTS_VMEM_RD", 0) / w
-    d["salu_insts_per_wave"] = per_launch.get("SQ_INSTS_SALU", 0) / w
-if "SQ_WAVE_CYCLES" in per_launch and "SQ_WAIT_ANY" in per_launch:
-    wc = per_launch["SQ_WAVE_CYCLES"]
-    d["wait_any_frac"] = per_launch["SQ_WAIT_ANY"] / wc
-    d["wait_inst_frac"] = per_launch["SQ_WAIT_INST_ANY"] / wc
-    d["active_inst_frac"] = per_launch["SQ_ACTIVE_INST_ANY"] / wc
-if "GRBM_GUI_ACTIVE" in per_launch and avg_ns:
-    d["effective_clock_GHz"] = per_launch["GRBM_GUI_ACTIVE"] / 8 / avg_ns
-res["derived"] = d
+    trace["hbm_bytes_per_frame"] = tsum("FETCH_SIZE") * 1024 * 2 + tsum("WRITE_SIZE") * 1024
+wc = tsum("SQ_WAVE_CYCLES")
+if wc:
+    trace["wait_any_frac"] = tsum("SQ_WAIT_ANY") / wc
+    trace["wait_inst_frac"] = tsum("SQ_WAIT_INST_ANY") / wc
+    trace["active_inst_frac"] = tsum("SQ_ACTIVE_INST_ANY") / wc
+h, m = tsum("TCC_HIT_sum"), tsum("TCC_MISS_sum")
+if h + m:
+    trace["l2_hit_rate"] = h / (h + m)
+if trace["trace_ms_per_frame"]:
+    t = trace["trace_ms_per_frame"] * 1e-3
+    peak = 1024 * 2.4e9 / 2  # VALU wave-instruction issue peak (bench.py)
+    trace["valu_issue_frac"] = trace["valu_insts_per_frame"] / t / peak
+    trace["useful_lane_frac"] = trace["valu_issue_frac"] * trace["valu_lane_utilization"]
+    if "hbm_bytes_per_frame" in trace:
+        trace["hbm_GBs"] = trace["hbm_bytes_per_frame"] / t / 1e9
+        trace["hbm_frac"] = trace["hbm_GBs"] / 8000.0
+    g = tsum("GRBM_GUI_ACTIVE")
+    if g:
+        # GRBM_GUI_ACTIVE: summed over the 8 XCDs (MI355X_MICROARCH.md DVFS); PMC-run clock
+        trace["grbm_clock_GHz_vs_trace_time"] = g / 8 / (trace["trace_ms_per_frame"] * 1e6)
+
+res = {"config": cfg, "source": str(src), "lib_sha": meta.get("lib_sha", ""), "frames_profiled": frames,
+       "bench_frames": bench_frames, "traversals_per_frame": meta["traversals_per_frame"], "tile_rows": meta["tile_rows"],
+       "trace": trace, "kernels": kernels, "kernel_stats": stats}
 dst.parent.mkdir(parents=True, exist_ok=True)
-# traffic record consumed by bench.py (roofline.traffic) for the bench config
-if len(sys.argv) > 4 and "hbm_bytes_per_launch" in d:
-    cfg, rows = sys.argv[4].split(":")
-    (dst.parent / "pmc_traffic.json").write_text(json.dumps({
-        "config": cfg, "tile_rows": int(rows), "kernel": KERNEL,
-        "hbm_bytes_per_launch": d["hbm_bytes_per_launch"],
-        "method": "rocprofv3 separate --pmc passes: FETCH_SIZE*1024*2 (gfx950: FETCH_SIZE reads 1/2 of the "
-                  "bytes, MI355X_MICROARCH.md HBM) + WRITE_SIZE*1024, averaged over launches",
-        "source": str(src)}, indent=1))
 Path(str(dst) + ".json").write_text(json.dumps(res, indent=1))
-lines = [f"# rocprofv3 summary: {src.name}", "", "## kernel stats (kernel trace of bench.py)", "",
-         "| kernel | calls | avg ns | min ns | max ns | % |", "|---|---|---|---|---|---|"]
-for n, st in stats.items():
-    lines.append(f"| `{n[:90]}` | {st['Calls']} | {float(st['AverageNs']):.0f} | {st['MinNs']} | {st['MaxNs']} | "
+if record:
+    (dst.parent / f"pmc_{cfg}.json").write_text(json.dumps({
+        "config": cfg, "tile_rows": meta["tile_rows"], "lib_sha": meta.get("lib_sha", ""),
+        "traversals_per_frame": meta["traversals_per_frame"], "trace": trace,
+        "method": "rocprofv3 separate --pmc passes over tools/prof_frame.py (production kernels only), summed over "
+                  "each frame's trace-kernel launches; FETCH_SIZE*1024*2 (gfx950: FETCH_SIZE reads 1/2 of the "
+                  "bytes, MI355X_MICROARCH.md HBM) + WRITE_SIZE*1024; trace time from the kernel trace of bench.py",
+        "summary": str(dst) + ".md"}, indent=1))
+
+lines = [f"# rocprofv3 summary: {src.name} ({cfg})", "",
+         f"build {meta.get('lib_sha', '')}; kernel trace of `bench.py --config {cfg}` ({bench_frames} frames) and "
+         f"PMC passes of `tools/prof_frame.py` ({frames} frames).", "",
+         "## trace kernels per frame (the roofline's kernels)", "", "| quantity | value |", "|---|---|"]
+lines += [f"| {k} | {v:.6g} |" if isinstance(v, float) else f"| {k} | {v} |" for k, v in trace.items()]
+lines += ["", "## kernel stats (kernel trace of bench.py)", "",
+          "| kernel | calls | avg ns | min ns | max ns | % |", "|---|---|---|---|---|---|"]
+for n, st in sorted(stats.items(), key=lambda kv: -float(kv[1]["Percentage"])):
+    lines.append(f"| `{short(n)[:90]}` | {st['Calls']} | {float(st['AverageNs']):.0f} | {st['MinNs']} | {st['MaxNs']} | "
                  f"{float(st['Percentage']):.2f} |")
-lines += ["", f"## PMC per launch of `{KERNEL}` (tools/prof_frame.py, separate passes)", "",
-          "| counter | value |", "|---|---|"]
-lines += [f"| {k} | {v:.6g} |" for k, v in sorted(per_launch.items())]
-lines += ["", "## derived", "", "| quantity | value |", "|---|---|"]
-lines += [f"| {k} | {v:.6g} |" for k, v in d.items()]
+lines += ["", "## PMC per frame, per kernel (tools/prof_frame.py, separate passes)", ""]
+cols = sorted({c for k in kernels.values() for c in k if c.endswith("_per_frame")})
+lines += ["| kernel | " + " | ".join(c.replace("_per_frame", "") for c in cols) + " |",
+          "|---|" + "---|" * len(cols)]
+for n, k in sorted(kernels.items(), key=lambda kv: -kv[1].get("SQ_INSTS_VALU_per_frame", 0)):
+    if k.get("SQ_INSTS_VALU_per_frame", 0) < 1e5 and not k["trace"]:
+        continue
+    lines.append(f"| `{n[:70]}` | " + " | ".join(f"{k.get(c, 0):.4g}" for c in cols) + " |")
 Path(str(dst) + ".md").write_text("\n".join(lines) + "\n")
-print("\n".join(lines))
+print("\n".join(lines[:40]))
