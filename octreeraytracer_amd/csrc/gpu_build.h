@@ -13,6 +13,7 @@ namespace ort {
 struct GpuTree {
     int32_t n_nodes = 0;
     int64_t n_indices = 0;
+    int32_t n_spheres = 0;              // spheres the tree was built over
     int depth = 0;                      // deepest node level (root = 0)
     std::vector<int64_t> level_start;   // BFS index of the first node of each level (+ end)
     float* node_min = nullptr;          // 3 per node

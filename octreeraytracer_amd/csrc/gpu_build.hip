@@ -229,7 +229,8 @@ __global__ void k_keys_to_idx(const unsigned long long* keys, int64_t n, int32_t
 }
 
 // ---- compact / explicit layouts on the device (see layout.h for the compact format) ----
-__global__ void k_compact_nodes(const int32_t* co, const int32_t* oo, const int32_t* cnt, int64_t n, uint2* node) {
+__global__ void k_compact_nodes(const int32_t* co, const int32_t* oo, const int32_t* cnt, const int32_t* idx, int64_t n,
+                                int64_t ni, uint2* node) {
     for (int64_t i = blockIdx.x * (int64_t)kB + threadIdx.x; i < n; i += (int64_t)gridDim.x * kB) {
         const int32_t c = co[i];
         if (c != -1) {
@@ -245,14 +246,17 @@ __global__ void k_compact_nodes(const int32_t* co, const int32_t* oo, const int3
             node[i] = make_uint2((uint32_t)c, 0x80000000u | (leafkids ? 0x40000000u : 0u) | mask);
         } else {
             const int32_t v = cnt[i] > 0 ? cnt[i] : 0;
-            node[i] = make_uint2(v > 0 ? (uint32_t)oo[i] : 0u, (uint32_t)v);
+            // one-sphere leaves point into the per-sphere tail (layout.h)
+            node[i] = make_uint2(v == 1 ? (uint32_t)(ni + idx[oo[i]]) : (v > 0 ? (uint32_t)oo[i] : 0u), (uint32_t)v);
         }
     }
 }
 
-__global__ void k_leaf_gather(const int32_t* idx, int64_t n, const float4* sp, float4* leaf_sph, int32_t* leaf_idx) {
+// entries 0..ni-1: objectIndices; ni..ni+nsph-1: the per-sphere tail (layout.h)
+__global__ void k_leaf_gather(const int32_t* idx, int64_t ni, int64_t n, const float4* sp, float4* leaf_sph,
+                              int32_t* leaf_idx) {
     for (int64_t e = blockIdx.x * (int64_t)kB + threadIdx.x; e < n; e += (int64_t)gridDim.x * kB) {
-        const int32_t s = idx[e];
+        const int32_t s = e < ni ? idx[e] : (int32_t)(e - ni);
         const float4 v = sp[s];
         leaf_sph[e] = make_float4(v.x, v.y, v.z, v.w * v.w);  // radius^2 (layout.h)
         leaf_idx[e] = s;
@@ -537,6 +541,7 @@ std::string gpuBuildOctree(const float4* sp, int32_t n, int32_t maxDepth, int32_
     }
     // objectIndices: leaf keys sorted by (BFS node, sphere)
     out.n_indices = leaf_n;
+    out.n_spheres = n;
     if (!(err = dalloc(out.idx, leaf_n)).empty()) {
         freeGpuTree(out);
         return err;
@@ -572,7 +577,8 @@ bool gpuCompactLayout(const GpuTree& t, const float4* sp, int maxDepth, hipStrea
         why = "tree deeper than the compact layout supports";
         return false;
     }
-    if (8 * (uint64_t)t.n_nodes >= ((uint64_t)1 << 32) || 16 * (uint64_t)t.n_indices >= ((uint64_t)1 << 32)) {
+    if (8 * (uint64_t)t.n_nodes >= ((uint64_t)1 << 32) ||
+        16 * ((uint64_t)t.n_indices + (uint64_t)t.n_spheres) >= ((uint64_t)1 << 32)) {
         why = "compact buffers exceed 4 GiB";
         return false;
     }
@@ -584,16 +590,16 @@ bool gpuCompactLayout(const GpuTree& t, const float4* sp, int maxDepth, hipStrea
         out = CompactDev();
         return false;
     };
-    const int64_t n = t.n_nodes, ni = t.n_indices;
+    const int64_t n = t.n_nodes, ni = t.n_indices, ne = t.n_indices + t.n_spheres;
     const int D = t.depth;
     const int64_t np = 3 * (((int64_t)1 << D) + 1);
     std::string e;
-    if (!(e = dalloc(out.node, n)).empty() || !(e = dalloc(out.leaf_sph, ni)).empty() ||
-        !(e = dalloc(out.leaf_idx, ni)).empty() || !(e = dalloc(out.planes, np)).empty())
+    if (!(e = dalloc(out.node, n)).empty() || !(e = dalloc(out.leaf_sph, ne)).empty() ||
+        !(e = dalloc(out.leaf_idx, ne)).empty() || !(e = dalloc(out.planes, np)).empty())
         return fail(e);
     out.node_bytes = (size_t)n * 8;
-    out.leaf_bytes = (size_t)std::max<int64_t>(ni, 1) * 16;
-    out.idx_bytes = (size_t)std::max<int64_t>(ni, 1) * 4;
+    out.leaf_bytes = (size_t)std::max<int64_t>(ne, 1) * 16;
+    out.idx_bytes = (size_t)std::max<int64_t>(ne, 1) * 4;
     out.plane_bytes = (size_t)np * 4;
     int* bad;
     if (!(e = dalloc(bad, 1)).empty()) return fail(e);
@@ -601,9 +607,10 @@ bool gpuCompactLayout(const GpuTree& t, const float4* sp, int maxDepth, hipStrea
         int* p;
         ~Free() { (void)hipFree(p); }
     } fb{bad};
-    hipLaunchKernelGGL(k_compact_nodes, dim3(grid_for(n)), dim3(kB), 0, s, t.co, t.oo, t.cnt, n, out.node);
-    if (ni > 0)
-        hipLaunchKernelGGL(k_leaf_gather, dim3(grid_for(ni)), dim3(kB), 0, s, t.idx, ni, sp, out.leaf_sph, out.leaf_idx);
+    hipLaunchKernelGGL(k_compact_nodes, dim3(grid_for(n)), dim3(kB), 0, s, t.co, t.oo, t.cnt, t.idx, n, ni, out.node);
+    if (ne > 0)
+        hipLaunchKernelGGL(k_leaf_gather, dim3(grid_for(ne)), dim3(kB), 0, s, t.idx, ni, ne, sp, out.leaf_sph,
+                           out.leaf_idx);
     hipLaunchKernelGGL(k_fill_nan, dim3(grid_for(np)), dim3(kB), 0, s, out.planes, np);
     if (hipMemsetAsync(bad, 0, 4, s) != hipSuccess) return fail("hipMemsetAsync");
     for (int d = 0; d <= D; ++d) {

@@ -61,7 +61,8 @@ bool buildCompactLayout(const SceneInput& in, int maxDepth, CompactLayout& out, 
     const int32_t n = in.n_nodes;
     if (n <= 0) { why = "no nodes"; return false; }
     // the kernel addresses node records and leaf spheres with 32-bit byte offsets
-    if (8 * (uint64_t)n >= ((uint64_t)1 << 32) || 16 * (uint64_t)in.n_indices >= ((uint64_t)1 << 32)) {
+    if (8 * (uint64_t)n >= ((uint64_t)1 << 32) ||
+        16 * ((uint64_t)in.n_indices + (uint64_t)in.n_spheres) >= ((uint64_t)1 << 32)) {
         why = "compact buffers exceed 4 GiB";
         return false;
     }
@@ -139,15 +140,18 @@ bool buildCompactLayout(const SceneInput& in, int maxDepth, CompactLayout& out, 
             out.node[2 * (size_t)i + 1] = ORT_INTERNAL_FLAG_HOST | (leafkids ? ORT_LEAFKIDS_FLAG_HOST : 0u) | mask;
         } else {
             const int32_t cntv = in.cnt[i] > 0 ? in.cnt[i] : 0;
-            out.node[2 * (size_t)i] = cntv > 0 ? (uint32_t)in.oo[i] : 0u;
+            // one-sphere leaves point into the per-sphere tail (layout.h)
+            out.node[2 * (size_t)i] = cntv == 1 ? (uint32_t)(in.n_indices + in.indices[in.oo[i]])
+                                               : (cntv > 0 ? (uint32_t)in.oo[i] : 0u);
             out.node[2 * (size_t)i + 1] = (uint32_t)cntv;
         }
     }
-    // Leaf entries.
-    out.leaf_sph.resize(4 * (size_t)in.n_indices);
-    out.leaf_idx.resize((size_t)in.n_indices);
-    for (int64_t e = 0; e < in.n_indices; ++e) {
-        const int32_t s = in.indices[e];
+    // Leaf entries, then the per-sphere tail (entry n_indices + s = sphere s).
+    const int64_t ne = in.n_indices + in.n_spheres;
+    out.leaf_sph.resize(4 * (size_t)ne);
+    out.leaf_idx.resize((size_t)ne);
+    for (int64_t e = 0; e < ne; ++e) {
+        const int32_t s = e < in.n_indices ? in.indices[e] : (int32_t)(e - in.n_indices);
         std::memcpy(&out.leaf_sph[4 * (size_t)e], in.sph_cr + 4 * (size_t)s, 12);
         const float rad = in.sph_cr[4 * (size_t)s + 3];
         out.leaf_sph[4 * (size_t)e + 3] = rad * rad;  // the kernel's r * r, rounded once (fp32)

@@ -14,6 +14,12 @@
 //   leaf_sph[e] = spheres[objectIndices[e]] with .w = radius * radius (16 B): one gather
 //   instead of index + sphere, and the sphere test's r * r precomputed (rounded as it would be).
 //   leaf_idx[e] = objectIndices[e], read only for the final hit (material lookup).
+//   Both arrays carry a per-sphere TAIL after the n_indices entries: entry n_indices + s is
+//   sphere s.  A leaf holding exactly one sphere s records objectsOffset = n_indices + s, so
+//   its test reads the sphere table (16 B x spheres: cache-resident even at 1M spheres)
+//   instead of its own copy inside the n_indices-entry array (2.8 GB at C5, where each
+//   sphere sits in ~170 leaves and the copies are HBM misses for scattered bounce rays).
+//   Same sphere, same order, same hit: the records only point elsewhere.
 //   planes[a][k], k = 0..2^D: coordinate of the axis-a split plane at dyadic position
 //     k / 2^D.  The reference builder derives every child box from its parent by
 //     mid = (min+max)*0.5f and copies min/mid/max verbatim (src/octree.cpp:97-187, 197),
