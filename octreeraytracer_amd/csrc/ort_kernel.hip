@@ -1794,10 +1794,23 @@ int ort_debug_emulate_render(const float* cr, const float* ma, const float* fr, 
                 if (y >= p->height) { o[0] = o[1] = o[2] = 0.0f; continue; }
                 ort::Counters cc;
                 for (int k = 0; k < 6; ++k) cc.v[k] = 0;
-                ort::V3 v;
-                if (mode == 0) v = ort::shade_pixel<0, true>(pp, S, fplanes.data(), rank_lut, lf, nullptr, nullptr, t->x0 + c, y, cc);
-                else if (mode == 1) v = ort::shade_pixel<1, true>(pp, S, nullptr, nullptr, lf, snode.data(), stmin.data(), t->x0 + c, y, cc);
-                else v = ort::shade_pixel<2, true>(pp, S, nullptr, nullptr, lf, nullptr, nullptr, t->x0 + c, y, cc);
+                ort::V3 v, vc;
+                // pixels from the production walk (COUNT=false: with the rejected-sphere skip),
+                // counters from the counting walk (the reference's work, no skip) -- and the two
+                // pixels must agree bit for bit
+                if (mode == 0) {
+                    v = ort::shade_pixel<0, false>(pp, S, fplanes.data(), rank_lut, lf, nullptr, nullptr, t->x0 + c, y, cc);
+                    vc = ort::shade_pixel<0, true>(pp, S, fplanes.data(), rank_lut, lf, nullptr, nullptr, t->x0 + c, y, cc);
+                } else if (mode == 1) {
+                    v = ort::shade_pixel<1, false>(pp, S, nullptr, nullptr, lf, snode.data(), stmin.data(), t->x0 + c, y, cc);
+                    vc = ort::shade_pixel<1, true>(pp, S, nullptr, nullptr, lf, snode.data(), stmin.data(), t->x0 + c, y, cc);
+                } else {
+                    v = ort::shade_pixel<2, false>(pp, S, nullptr, nullptr, lf, nullptr, nullptr, t->x0 + c, y, cc);
+                    vc = ort::shade_pixel<2, true>(pp, S, nullptr, nullptr, lf, nullptr, nullptr, t->x0 + c, y, cc);
+                }
+                if (ort::f2u(v.x) != ort::f2u(vc.x) || ort::f2u(v.y) != ort::f2u(vc.y) || ort::f2u(v.z) != ort::f2u(vc.z))
+                    return fail(nullptr, ORT_ERR_INTERNAL, "emulation: production and counting walks differ at pixel (" +
+                                                               std::to_string(t->x0 + c) + ", " + std::to_string(y) + ")");
                 o[0] = v.x; o[1] = v.y; o[2] = v.z;
                 cc.v[4] = 1;
                 for (int k = 0; k < 6; ++k) total.v[k] += cc.v[k];
