@@ -11,7 +11,7 @@ HIPFLAGS := -O3 -std=c++17 --offload-arch=$(ARCH) -ffp-contract=off -fno-fast-ma
 
 HOST_SRCS := octree.cpp scene.cpp host_abi.cpp layout.cpp raytracer.cpp
 HOST_OBJS := $(addprefix $(OBJ)/,$(HOST_SRCS:.cpp=.o))
-HIP_OBJS := $(OBJ)/ort_kernel.o $(OBJ)/gpu_build.o
+HIP_OBJS := $(OBJ)/ort_kernel.o $(OBJ)/gpu_build.o $(OBJ)/group.o
 HDRS := $(wildcard $(SRC)/*.h) $(SRC)/prebuilt_scene.inc include/ort.h include/ort_math.h
 
 .PHONY: all lib oracle ref examples clean
@@ -31,9 +31,13 @@ $(OBJ)/gpu_build.o: $(SRC)/gpu_build.hip $(SRC)/gpu_build.h
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -Wno-unused-result -c $< -o $@
 
+$(OBJ)/group.o: $(SRC)/group.hip $(SRC)/group_map.h $(SRC)/ort_internal.h include/ort.h
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
 $(LIB): $(HOST_OBJS) $(HIP_OBJS)
 	@mkdir -p $(dir $(LIB))
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -Wl,-soname,libort.so
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -ldl -Wl,-soname,libort.so
 
 examples: build/ort_main
 

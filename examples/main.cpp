@@ -33,6 +33,14 @@ int main(int argc, char** argv) {
         else if (!std::strcmp(argv[i], "--gpu-build")) cfg.gpuBuild = true;
         else if (!std::strcmp(argv[i], "--seed")) cfg.seed = (uint32_t)std::strtoul(next(), nullptr, 10);
         else if (!std::strcmp(argv[i], "--device")) cfg.device = std::atoi(next());
+        else if (!std::strcmp(argv[i], "--devices")) {  // e.g. 0,1,2,3,4,5,6,7: one ort_group (RCCL gather)
+            cfg.devices.clear();
+            for (const char* q = next(); *q;) {
+                cfg.devices.push_back(std::atoi(q));
+                while (*q && *q != ',') ++q;
+                if (*q == ',') ++q;
+            }
+        }
         else if (!std::strcmp(argv[i], "--stats")) { cfg.collectStats = true; cfg.outputFile = next(); }
         else if (!std::strcmp(argv[i], "--ppm")) ppm = next();
         else { std::fprintf(stderr, "unknown argument %s\n", argv[i]); return 2; }

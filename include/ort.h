@@ -191,6 +191,47 @@ int ort_frame_trace_times_ms(ort_ctx* ctx, int n, float* ms, int32_t* launches);
  * pixels, the reference-layout work counters ORT_COUNT_* (counts[ORT_COUNT_N]). */
 int ort_count_traffic(ort_ctx* ctx, const ort_params* params, const ort_tile* tile, uint64_t* counts);
 
+/* ---- several GPUs, one process --------------------------------------
+ * The reference renders on one GL context; a caller of Raytracer::render() reaches the 8-GPU
+ * configs through a group: one context per listed device (scene replicated), the frame cut
+ * into 16-row bands dealt round-robin (rank r renders bands r, r+N, ...; every rank the same
+ * number of rows), ONE exchange -- the bands gathered to devices[0] -- and a de-interleave
+ * kernel there.  Pixels equal a single-context render bit for bit (they depend only on the
+ * global pixel and the frame size).  Transports:
+ *   ORT_GROUP_TRANSPORT_RCCL  ncclSend/ncclRecv fused in one ncclGroupStart/End over
+ *                             communicators from ncclCommInitAll (RCCL over xGMI); devices
+ *                             must be distinct; RCCL is dlopen'ed (RTLD_LOCAL) on demand.
+ *   ORT_GROUP_TRANSPORT_COPY  hipMemcpyPeerAsync (testing; a device may be listed twice).
+ * Calls on one group are not thread-safe. */
+typedef struct ort_group ort_group;
+#define ORT_GROUP_MAX_DEVICES 64
+#define ORT_GROUP_TRANSPORT_RCCL 0
+#define ORT_GROUP_TRANSPORT_COPY 1
+int ort_group_create(const int32_t* devices, int32_t n_devices, int32_t transport, ort_group** out);
+int ort_group_destroy(ort_group* group);
+/* Last error of the group (or of the calling thread when group == NULL).  Never NULL. */
+const char* ort_group_last_error(const ort_group* group);
+int ort_group_size(const ort_group* group);
+/* The context of rank `rank` (owned by the group), e.g. for ort_scene_get_info. */
+int ort_group_context(ort_group* group, int32_t rank, ort_ctx** ctx);
+/* ort_set_option on every context. */
+int ort_group_set_option(ort_group* group, int option, int value);
+/* ort_upload_scene / ort_build_scene on every context (same arguments). */
+int ort_group_upload_scene(ort_group* group, const float* sphere_center_radius, const float* sphere_mat_albedo,
+                           const float* sphere_fuzz_ri, int32_t n_spheres, const float* node_min,
+                           const float* node_max, const int32_t* children_offset, const int32_t* objects_offset,
+                           const int32_t* object_count, int32_t n_nodes, const int32_t* object_indices,
+                           int64_t n_indices);
+int ort_group_build_scene(ort_group* group, const float* sphere_center_radius, const float* sphere_mat_albedo,
+                          const float* sphere_fuzz_ri, int32_t n_spheres, int32_t max_depth,
+                          int32_t max_spheres_per_node);
+/* One full frame (width x height RGB floats, row 0 = bottom) into rgb_out: host memory, or
+ * (out_is_device != 0) device memory on devices[0].  Synchronous. */
+int ort_group_render(ort_group* group, const ort_params* params, float* rgb_out, int32_t out_is_device);
+/* Device time of the last ort_group_render on devices[0]'s stream: renders, gather and
+ * assembly (HIP events). */
+int ort_group_last_frame_ms(ort_group* group, float* ms);
+
 /* ---- host scene-build stage (kept reference API, src/raytracer.cpp + src/octree.cpp) -- */
 
 /* Raytracer::generateRandomSpheres (src/raytracer.cpp:254-337) with std::mt19937(seed)

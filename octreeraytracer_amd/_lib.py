@@ -42,7 +42,12 @@ EXPORTED_SYMBOLS = (
     "ort_count_traffic", "ort_scene_random", "ort_scene_prebuilt", "ort_scene_debug",
     "ort_octree_build", "ort_octree_sizes", "ort_octree_export", "ort_octree_nodes",
     "ort_octree_indices", "ort_octree_free", "ort_camera_view", "ort_version",
+    "ort_group_create", "ort_group_destroy", "ort_group_last_error", "ort_group_size", "ort_group_context",
+    "ort_group_set_option", "ort_group_upload_scene", "ort_group_build_scene", "ort_group_render",
+    "ort_group_last_frame_ms",
 )
+ORT_GROUP_TRANSPORT_RCCL = 0
+ORT_GROUP_TRANSPORT_COPY = 1
 
 
 class OrtParams(C.Structure):
@@ -111,6 +116,19 @@ def _declare(lib):
         "ort_octree_free": (None, [_vp]),
         "ort_camera_view": (C.c_int, [_fp, _fp, C.c_float, C.c_float, _fp]),
         "ort_version": (C.c_char_p, []),
+        "ort_group_create": (C.c_int, [_ip, C.c_int32, C.c_int32, C.POINTER(_vp)]),
+        "ort_group_destroy": (C.c_int, [_vp]),
+        "ort_group_last_error": (C.c_char_p, [_vp]),
+        "ort_group_size": (C.c_int, [_vp]),
+        "ort_group_context": (C.c_int, [_vp, C.c_int32, C.POINTER(_vp)]),
+        "ort_group_set_option": (C.c_int, [_vp, C.c_int, C.c_int]),
+        "ort_group_upload_scene": (C.c_int, [_vp, _fp, _fp, _fp, C.c_int32, _fp, _fp, _ip, _ip, _ip, C.c_int32, _ip,
+                                             C.c_int64]),
+        "ort_group_build_scene": (C.c_int, [_vp, _fp, _fp, _fp, C.c_int32, C.c_int32, C.c_int32]),
+        "ort_group_render": (C.c_int, [_vp, C.POINTER(OrtParams), _vp, C.c_int32]),
+        "ort_group_last_frame_ms": (C.c_int, [_vp, _fp]),
+        "ort_debug_group_emulate": (C.c_int, [_fp, _fp, _fp, C.c_int32, _fp, _fp, _ip, _ip, _ip, C.c_int32, _ip, C.c_int64,
+                                              C.c_int32, C.POINTER(OrtParams), _fp]),
         "ort_debug_emulate_render": (C.c_int, [_fp, _fp, _fp, C.c_int32, _fp, _fp, _ip, _ip, _ip, C.c_int32, _ip,
                                                C.c_int64, C.c_int32, C.POINTER(OrtParams), C.POINTER(OrtTile),
                                                _fp, _u64p]),

@@ -1,0 +1,398 @@
+// group.hip -- several GPUs behind the C ABI (include/ort.h ort_group_*): the multi-GPU
+// path of SURVEY.md 8(e) for a single host process, the shape a caller of
+// Raytracer::render() (src/raytracer.cpp:491-499 sits where that call sits) needs to reach
+// the 8-GPU configs without torch.distributed.
+//
+//   * one ort_ctx per listed device (scene replicated: every context builds or receives it);
+//   * the frame cut into 16-row bands dealt round-robin -- rank r renders bands r, r+N, ...
+//     (identical to octreeraytracer_amd/distributed.py rank_tile), every rank the same
+//     number of rows, so every message has the same size;
+//   * one exchange step: the bands go to devices[0] -- RCCL (ncclSend/ncclRecv fused in one
+//     ncclGroupStart/End, communicators from ncclCommInitAll) or, for testing, device copies
+//     (hipMemcpyPeerAsync; works with one device listed several times) -- and one
+//     de-interleave kernel on devices[0] writes the frame.
+// RCCL is loaded with dlopen(RTLD_LOCAL) when a group asks for it, so libort.so has no link
+// dependency on it and never interposes a second librccl into a process that has its own
+// (torch ships one).
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <new>
+#include <string>
+#include <type_traits>
+#include <vector>
+
+#include "../../include/ort.h"
+#include "group_map.h"
+#include "ort_internal.h"
+
+namespace {
+
+struct Rccl {
+    void* so = nullptr;
+    ncclResult_t (*commInitAll)(ncclComm_t*, int, const int*) = nullptr;
+    ncclResult_t (*commDestroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*groupStart)() = nullptr;
+    ncclResult_t (*groupEnd)() = nullptr;
+    const char* (*errorString)(ncclResult_t) = nullptr;
+};
+
+// Loaded once per process; failures leave so == nullptr and a message.
+const Rccl& rccl(std::string& err) {
+    static Rccl r;
+    static std::string why;
+    static bool tried = false;
+    if (!tried) {
+        tried = true;
+        const char* names[] = {"librccl.so.1", "/opt/rocm/lib/librccl.so.1", "librccl.so"};
+        for (const char* n : names)
+            if ((r.so = dlopen(n, RTLD_NOW | RTLD_LOCAL))) break;
+        if (!r.so) {
+            why = std::string("RCCL not loadable: ") + dlerror();
+        } else {
+            bool ok = true;
+            auto sym = [&](auto& f, const char* name) {
+                f = reinterpret_cast<std::remove_reference_t<decltype(f)>>(dlsym(r.so, name));
+                ok = ok && f;
+            };
+            sym(r.commInitAll, "ncclCommInitAll");
+            sym(r.commDestroy, "ncclCommDestroy");
+            sym(r.send, "ncclSend");
+            sym(r.recv, "ncclRecv");
+            sym(r.groupStart, "ncclGroupStart");
+            sym(r.groupEnd, "ncclGroupEnd");
+            sym(r.errorString, "ncclGetErrorString");
+            if (!ok) {
+                why = "RCCL lacks a needed symbol";
+                r.so = nullptr;
+            }
+        }
+    }
+    err = why;
+    return r;
+}
+
+// de-interleave: frame row y <- row group_src_row(y) of its rank's band tile
+struct SrcTable {
+    const float* tile[ORT_GROUP_MAX_DEVICES];
+};
+__global__ void __launch_bounds__(256) k_assemble(SrcTable src, int world, int width, int height, float* out) {
+    const int y = blockIdx.x;
+    if (y >= height) return;
+    int rank, trow;
+    ort::group_src_row(y, world, rank, trow);
+    const size_t n = 3 * (size_t)width;
+    const float* s = src.tile[rank] + (size_t)trow * n;
+    float* d = out + (size_t)y * n;
+    for (size_t i = threadIdx.x; i < n; i += blockDim.x) d[i] = s[i];
+}
+
+}  // namespace
+
+struct ort_group {
+    int n = 0;
+    int transport = ORT_GROUP_TRANSPORT_RCCL;
+    std::vector<int> dev;
+    std::vector<ort_ctx*> ctx;
+    std::vector<hipStream_t> stream;   // each context's own stream
+    std::vector<ncclComm_t> comm;
+    std::vector<float*> tile;          // per rank, on its device: rows x W x 3
+    std::vector<float*> recv;          // on devices[0]: the band tiles of ranks 1..n-1
+    size_t tile_floats = 0;
+    float* frame = nullptr;            // devices[0]: the assembled frame (host output path)
+    size_t frame_floats = 0;
+    std::vector<hipEvent_t> done;      // per rank: its tile has been sent / copied
+    hipEvent_t t0 = nullptr, t1 = nullptr;
+    bool timed = false;
+    std::string err;
+};
+
+namespace {
+
+int gfail(ort_group* g, int code, const std::string& msg) {
+    if (g) g->err = msg;
+    ort::set_thread_error(msg);
+    return code;
+}
+
+#define GCHK(g, expr)                                                                             \
+    do {                                                                                          \
+        hipError_t _e = (expr);                                                                   \
+        if (_e != hipSuccess)                                                                     \
+            return gfail(g, _e == hipErrorOutOfMemory ? ORT_ERR_OUT_OF_MEMORY : ORT_ERR_HIP,      \
+                         std::string(#expr) + ": " + hipGetErrorString(_e));                      \
+    } while (0)
+
+int each(ort_group* g, int rc, int r) {
+    if (rc != ORT_OK) return gfail(g, rc, "device " + std::to_string(g->dev[r]) + ": " + ort_last_error(g->ctx[r]));
+    return ORT_OK;
+}
+
+void free_buffers(ort_group* g) {
+    for (int r = 0; r < (int)g->tile.size(); ++r)
+        if (g->tile[r]) {
+            (void)hipSetDevice(g->dev[r]);
+            (void)hipFree(g->tile[r]);
+        }
+    g->tile.assign(g->n, nullptr);
+    (void)hipSetDevice(g->dev.empty() ? 0 : g->dev[0]);
+    for (float* p : g->recv)
+        if (p) (void)hipFree(p);
+    g->recv.assign(g->n, nullptr);
+    if (g->frame) (void)hipFree(g->frame);
+    g->frame = nullptr;
+    g->tile_floats = 0;
+    g->frame_floats = 0;
+}
+
+int ensure_buffers(ort_group* g, size_t tile_floats, size_t frame_floats) {
+    if (tile_floats > g->tile_floats) {
+        free_buffers(g);
+        for (int r = 0; r < g->n; ++r) {
+            GCHK(g, hipSetDevice(g->dev[r]));
+            GCHK(g, hipMalloc(&g->tile[r], tile_floats * sizeof(float)));
+        }
+        GCHK(g, hipSetDevice(g->dev[0]));
+        for (int r = 1; r < g->n; ++r) GCHK(g, hipMalloc(&g->recv[r], tile_floats * sizeof(float)));
+        g->tile_floats = tile_floats;
+    }
+    if (frame_floats > g->frame_floats) {
+        GCHK(g, hipSetDevice(g->dev[0]));
+        if (g->frame) (void)hipFree(g->frame);
+        g->frame = nullptr;
+        GCHK(g, hipMalloc(&g->frame, frame_floats * sizeof(float)));
+        g->frame_floats = frame_floats;
+    }
+    return ORT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ort_group_create(const int32_t* devices, int32_t n_devices, int32_t transport, ort_group** out) {
+    if (!out || !devices || n_devices < 1 || n_devices > ORT_GROUP_MAX_DEVICES)
+        return gfail(nullptr, ORT_ERR_INVALID_ARG, "ort_group_create: need 1.." + std::to_string(ORT_GROUP_MAX_DEVICES) +
+                                                       " devices and an out pointer");
+    if (transport != ORT_GROUP_TRANSPORT_RCCL && transport != ORT_GROUP_TRANSPORT_COPY)
+        return gfail(nullptr, ORT_ERR_INVALID_ARG, "ort_group_create: unknown transport");
+    *out = nullptr;
+    if (transport == ORT_GROUP_TRANSPORT_RCCL)
+        for (int i = 0; i < n_devices; ++i)
+            for (int j = 0; j < i; ++j)
+                if (devices[i] == devices[j])
+                    return gfail(nullptr, ORT_ERR_INVALID_ARG,
+                                 "ort_group_create: RCCL needs distinct devices (ORT_GROUP_TRANSPORT_COPY allows repeats)");
+    ort_group* g = new (std::nothrow) ort_group();
+    if (!g) return gfail(nullptr, ORT_ERR_OUT_OF_MEMORY, "ort_group_create: out of host memory");
+    g->n = n_devices;
+    g->transport = transport;
+    g->dev.assign(devices, devices + n_devices);
+    g->ctx.assign(n_devices, nullptr);
+    g->stream.assign(n_devices, nullptr);
+    g->tile.assign(n_devices, nullptr);
+    g->recv.assign(n_devices, nullptr);
+    g->done.assign(n_devices, nullptr);
+    auto bail = [&](int rc) {
+        const std::string m = g->err.empty() ? std::string(ort_last_error(nullptr)) : g->err;
+        ort_group_destroy(g);
+        ort::set_thread_error(m);
+        return rc;
+    };
+    for (int r = 0; r < n_devices; ++r) {
+        int rc = ort_create(devices[r], &g->ctx[r]);
+        if (rc != ORT_OK) return bail(rc);
+        void* s = nullptr;
+        ort_get_stream(g->ctx[r], &s);
+        g->stream[r] = (hipStream_t)s;
+        if (hipSetDevice(devices[r]) != hipSuccess || hipEventCreateWithFlags(&g->done[r], hipEventDisableTiming) != hipSuccess)
+            return bail(gfail(g, ORT_ERR_HIP, "ort_group_create: events"));
+    }
+    if (hipSetDevice(devices[0]) != hipSuccess || hipEventCreate(&g->t0) != hipSuccess || hipEventCreate(&g->t1) != hipSuccess)
+        return bail(gfail(g, ORT_ERR_HIP, "ort_group_create: timing events"));
+    if (transport == ORT_GROUP_TRANSPORT_RCCL) {
+        std::string why;
+        const Rccl& R = rccl(why);
+        if (!R.so) return bail(gfail(g, ORT_ERR_UNSUPPORTED, "ort_group_create: " + why));
+        g->comm.assign(n_devices, nullptr);
+        const ncclResult_t e = R.commInitAll(g->comm.data(), n_devices, g->dev.data());
+        if (e != ncclSuccess) {
+            g->comm.clear();
+            return bail(gfail(g, ORT_ERR_HIP, std::string("ncclCommInitAll: ") + R.errorString(e)));
+        }
+    }
+    *out = g;
+    return ORT_OK;
+}
+
+int ort_group_destroy(ort_group* g) {
+    if (!g) return ORT_OK;
+    for (int r = 0; r < g->n; ++r)
+        if (g->ctx[r]) {
+            (void)hipSetDevice(g->dev[r]);
+            (void)hipStreamSynchronize(g->stream[r]);
+        }
+    if (!g->comm.empty()) {
+        std::string why;
+        const Rccl& R = rccl(why);
+        for (ncclComm_t c : g->comm)
+            if (c && R.so) (void)R.commDestroy(c);
+    }
+    free_buffers(g);
+    for (int r = 0; r < g->n; ++r) {
+        if (g->done[r]) {
+            (void)hipSetDevice(g->dev[r]);
+            (void)hipEventDestroy(g->done[r]);
+        }
+        if (g->ctx[r]) ort_destroy(g->ctx[r]);
+    }
+    if (!g->dev.empty()) (void)hipSetDevice(g->dev[0]);
+    if (g->t0) (void)hipEventDestroy(g->t0);
+    if (g->t1) (void)hipEventDestroy(g->t1);
+    delete g;
+    return ORT_OK;
+}
+
+const char* ort_group_last_error(const ort_group* g) { return g ? g->err.c_str() : ort::thread_error(); }
+
+int ort_group_size(const ort_group* g) { return g ? g->n : 0; }
+
+int ort_group_context(ort_group* g, int32_t rank, ort_ctx** ctx) {
+    if (!g || !ctx || rank < 0 || rank >= g->n) return gfail(g, ORT_ERR_INVALID_ARG, "ort_group_context: bad rank");
+    *ctx = g->ctx[rank];
+    return ORT_OK;
+}
+
+int ort_group_set_option(ort_group* g, int option, int value) {
+    if (!g) return gfail(nullptr, ORT_ERR_INVALID_ARG, "ort_group_set_option: null group");
+    for (int r = 0; r < g->n; ++r) {
+        const int rc = each(g, ort_set_option(g->ctx[r], option, value), r);
+        if (rc) return rc;
+    }
+    return ORT_OK;
+}
+
+int ort_group_upload_scene(ort_group* g, const float* cr, const float* ma, const float* fr, int32_t n_spheres,
+                           const float* node_min, const float* node_max, const int32_t* children_offset,
+                           const int32_t* objects_offset, const int32_t* object_count, int32_t n_nodes,
+                           const int32_t* object_indices, int64_t n_indices) {
+    if (!g) return gfail(nullptr, ORT_ERR_INVALID_ARG, "ort_group_upload_scene: null group");
+    for (int r = 0; r < g->n; ++r) {
+        const int rc = each(g, ort_upload_scene(g->ctx[r], cr, ma, fr, n_spheres, node_min, node_max, children_offset,
+                                                objects_offset, object_count, n_nodes, object_indices, n_indices), r);
+        if (rc) return rc;
+    }
+    return ORT_OK;
+}
+
+int ort_group_build_scene(ort_group* g, const float* cr, const float* ma, const float* fr, int32_t n_spheres,
+                          int32_t max_depth, int32_t max_spheres_per_node) {
+    if (!g) return gfail(nullptr, ORT_ERR_INVALID_ARG, "ort_group_build_scene: null group");
+    for (int r = 0; r < g->n; ++r) {
+        const int rc = each(g, ort_build_scene(g->ctx[r], cr, ma, fr, n_spheres, max_depth, max_spheres_per_node, 0), r);
+        if (rc) return rc;
+    }
+    return ORT_OK;
+}
+
+int ort_group_render(ort_group* g, const ort_params* p, float* rgb_out, int32_t out_is_device) {
+    if (!g || !p) return gfail(g, ORT_ERR_INVALID_ARG, "ort_group_render: null argument");
+    if (!rgb_out) return gfail(g, ORT_ERR_INVALID_ARG, "ort_group_render: null output");
+    if (p->width <= 0 || p->height <= 0) return gfail(g, ORT_ERR_INVALID_ARG, "ort_group_render: width/height must be positive");
+    const int W = p->width, H = p->height, N = g->n;
+    const ort_tile t0 = ort::group_tile(W, H, 0, N);
+    const size_t tile_floats = (size_t)t0.rows * W * 3, frame_floats = (size_t)H * W * 3;
+    int rc;
+    if ((rc = ensure_buffers(g, tile_floats, out_is_device ? 0 : frame_floats))) return rc;
+    GCHK(g, hipSetDevice(g->dev[0]));
+    GCHK(g, hipEventRecord(g->t0, g->stream[0]));
+    // 1. every rank renders its bands on its own stream (asynchronous)
+    for (int r = 0; r < N; ++r) {
+        const ort_tile t = ort::group_tile(W, H, r, N);
+        if ((rc = each(g, ort_render(g->ctx[r], p, &t, g->tile[r], 1, g->stream[r]), r))) return rc;
+    }
+    // 2. the one exchange: bands of ranks 1..N-1 to devices[0]
+    if (N > 1) {
+        if (g->transport == ORT_GROUP_TRANSPORT_RCCL) {
+            std::string why;
+            const Rccl& R = rccl(why);
+            ncclResult_t e = R.groupStart();
+            for (int r = 1; r < N && e == ncclSuccess; ++r) {
+                e = R.send(g->tile[r], tile_floats, ncclFloat32, 0, g->comm[r], g->stream[r]);
+                if (e == ncclSuccess) e = R.recv(g->recv[r], tile_floats, ncclFloat32, r, g->comm[0], g->stream[0]);
+            }
+            const ncclResult_t e2 = R.groupEnd();
+            if (e != ncclSuccess || e2 != ncclSuccess)
+                return gfail(g, ORT_ERR_HIP, std::string("RCCL gather: ") + R.errorString(e != ncclSuccess ? e : e2));
+        } else {
+            for (int r = 1; r < N; ++r) {
+                GCHK(g, hipSetDevice(g->dev[r]));
+                GCHK(g, hipMemcpyPeerAsync(g->recv[r], g->dev[0], g->tile[r], g->dev[r], tile_floats * sizeof(float),
+                                           g->stream[r]));
+                GCHK(g, hipEventRecord(g->done[r], g->stream[r]));
+                GCHK(g, hipSetDevice(g->dev[0]));
+                GCHK(g, hipStreamWaitEvent(g->stream[0], g->done[r], 0));
+            }
+        }
+    }
+    // 3. de-interleave on devices[0]
+    GCHK(g, hipSetDevice(g->dev[0]));
+    SrcTable src{};
+    src.tile[0] = g->tile[0];
+    for (int r = 1; r < N; ++r) src.tile[r] = g->recv[r];
+    float* dst = out_is_device ? rgb_out : g->frame;
+    hipLaunchKernelGGL(k_assemble, dim3((unsigned)H), dim3(256), 0, g->stream[0], src, N, W, H, dst);
+    GCHK(g, hipGetLastError());
+    GCHK(g, hipEventRecord(g->t1, g->stream[0]));
+    g->timed = true;
+    if (!out_is_device) GCHK(g, hipMemcpyAsync(rgb_out, g->frame, frame_floats * sizeof(float), hipMemcpyDeviceToHost,
+                                               g->stream[0]));
+    // synchronous, like ort_render without a stream: every rank's stream has passed the frame
+    for (int r = 0; r < N; ++r) {
+        GCHK(g, hipSetDevice(g->dev[r]));
+        GCHK(g, hipStreamSynchronize(g->stream[r]));
+    }
+    GCHK(g, hipSetDevice(g->dev[0]));
+    return ORT_OK;
+}
+
+int ort_group_last_frame_ms(ort_group* g, float* ms) {
+    if (!g || !ms) return gfail(g, ORT_ERR_INVALID_ARG, "ort_group_last_frame_ms: null argument");
+    if (!g->timed) return gfail(g, ORT_ERR_NO_SCENE, "no frame rendered yet");
+    GCHK(g, hipSetDevice(g->dev[0]));
+    GCHK(g, hipEventSynchronize(g->t1));
+    GCHK(g, hipEventElapsedTime(ms, g->t0, g->t1));
+    return ORT_OK;
+}
+
+// TEST-ONLY (no GPU): the group's partition and assembly with an in-memory transport -- every
+// rank's band tile rendered by the host emulation of the kernel (ort_debug_emulate_render),
+// one after another, then assembled by the same row map the device kernel uses.
+int ort_debug_group_emulate(const float* cr, const float* ma, const float* fr, int32_t n_spheres, const float* node_min,
+                            const float* node_max, const int32_t* co, const int32_t* oo, const int32_t* cnt,
+                            int32_t n_nodes, const int32_t* idx, int64_t n_indices, int32_t world,
+                            const ort_params* p, float* rgb_out) {
+    if (!p || !rgb_out || world < 1 || world > ORT_GROUP_MAX_DEVICES)
+        return gfail(nullptr, ORT_ERR_INVALID_ARG, "ort_debug_group_emulate: bad arguments");
+    const int W = p->width, H = p->height;
+    const ort_tile t0 = ort::group_tile(W, H, 0, world);
+    std::vector<std::vector<float>> tiles(world, std::vector<float>((size_t)t0.rows * W * 3));
+    for (int r = 0; r < world; ++r) {
+        const ort_tile t = ort::group_tile(W, H, r, world);
+        const int rc = ort_debug_emulate_render(cr, ma, fr, n_spheres, node_min, node_max, co, oo, cnt, n_nodes, idx,
+                                                n_indices, ORT_LAYOUT_COMPACT, p, &t, tiles[r].data(), nullptr);
+        if (rc != ORT_OK) return rc;
+    }
+    for (int y = 0; y < H; ++y) {
+        int rank, trow;
+        ort::group_src_row(y, world, rank, trow);
+        std::memcpy(rgb_out + (size_t)y * W * 3, tiles[rank].data() + (size_t)trow * W * 3, (size_t)W * 3 * sizeof(float));
+    }
+    return ORT_OK;
+}
+
+}  // extern "C"

@@ -20,6 +20,14 @@ int ort_debug_emulate_render(const float* sphere_center_radius, const float* sph
                              const int32_t* objects_offset, const int32_t* object_count, int32_t n_nodes,
                              const int32_t* object_indices, int64_t n_indices, int32_t layout,
                              const ort_params* params, const ort_tile* tile, float* rgb_out, uint64_t* counts);
+// TEST-ONLY: the ort_group partition and assembly with an in-memory transport: each of the
+// `world` band tiles rendered by ort_debug_emulate_render, then assembled by the device
+// kernel's row map (group_map.h).  Full frame into rgb_out (host).
+int ort_debug_group_emulate(const float* sphere_center_radius, const float* sphere_mat_albedo,
+                            const float* sphere_fuzz_ri, int32_t n_spheres, const float* node_min,
+                            const float* node_max, const int32_t* children_offset, const int32_t* objects_offset,
+                            const int32_t* object_count, int32_t n_nodes, const int32_t* object_indices,
+                            int64_t n_indices, int32_t world, const ort_params* params, float* rgb_out);
 // ANALYSIS-ONLY: lane overlap of sampled 8x8 primary-ray blocks (tools/wave_stats.py).
 int ort_debug_wave_stats(const float* sphere_center_radius, const float* sphere_mat_albedo,
                          const float* sphere_fuzz_ri, int32_t n_spheres, const float* node_min,

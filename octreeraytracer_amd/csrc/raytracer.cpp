@@ -29,7 +29,20 @@ Raytracer::Raytracer(const RaytracerConfig& c)
 Raytracer::~Raytracer() { cleanupBuffers(); }
 
 bool Raytracer::initialize() {
-    if (ctx) return true;
+    if (ctx || group) return true;
+    if (cfg.devices.size() > 1) {  // several GPUs: one context each inside an ort_group
+        // RCCL over distinct devices; a device listed twice (testing on one GPU) gathers by copies
+        bool distinct = true;
+        for (size_t i = 0; i < cfg.devices.size(); ++i)
+            for (size_t j = 0; j < i; ++j) distinct = distinct && cfg.devices[i] != cfg.devices[j];
+        const int32_t transport = distinct ? ORT_GROUP_TRANSPORT_RCCL : ORT_GROUP_TRANSPORT_COPY;
+        if (ort_group_create(cfg.devices.data(), (int32_t)cfg.devices.size(), transport, &group) != ORT_OK) {
+            std::cerr << "Failed to create the MI355X device group: " << ort_group_last_error(nullptr) << std::endl;
+            group = nullptr;
+            return false;
+        }
+        return true;
+    }
     if (ort_create(cfg.device, &ctx) != ORT_OK) {
         std::cerr << "Failed to create the MI355X context: " << ort_last_error(nullptr) << std::endl;
         ctx = nullptr;
@@ -38,7 +51,7 @@ bool Raytracer::initialize() {
     return true;
 }
 
-const char* Raytracer::lastError() const { return ort_last_error(ctx); }
+const char* Raytracer::lastError() const { return group ? ort_group_last_error(group) : ort_last_error(ctx); }
 
 std::vector<Sphere> Raytracer::generatePreBuiltSpheres() { return ort::generatePreBuiltSpheres(); }
 std::vector<Sphere> Raytracer::generateRandomSpheres() { return ort::generateRandomSpheres(cfg.numSpheres, cfg.seed); }
@@ -63,25 +76,32 @@ void Raytracer::setupBuffers() {
     // SoA packing of src/raytracer.cpp:87-101, then one upload (replaces 7x glBufferData)
     std::vector<float> cr(4 * spheres.size()), ma(4 * spheres.size()), fr(4 * spheres.size());
     ort::packSpheres(spheres, cr.data(), ma.data(), fr.data());
-    int rc;
-    if (cfg.gpuBuild && !cfg.debug) {
-        rc = ort_build_scene(ctx, cr.data(), ma.data(), fr.data(), (int32_t)spheres.size(), octree.getMaxDepth(),
-                             octree.getMaxSpheresPerNode(), 0);
-        float ms = 0.0f;
-        if (rc == ORT_OK) ort_last_build_ms(ctx, &ms);
-        gpuBuildSeconds = ms * 1e-3;
-    } else {
-        rc = ort_upload_octree_nodes(ctx, cr.data(), ma.data(), fr.data(), (int32_t)spheres.size(),
-                                     octree.flattenedTree.data(), (int32_t)octree.flattenedTree.size(),
-                                     octree.objectIndices.data(), (int64_t)octree.objectIndices.size());
+    int rc = ORT_OK;
+    const int ranks = group ? ort_group_size(group) : 1;
+    for (int r = 0; r < ranks && rc == ORT_OK; ++r) {  // every device holds the whole scene
+        ort_ctx* c = ctx;
+        if (group) ort_group_context(group, r, &c);
+        if (cfg.gpuBuild && !cfg.debug) {
+            rc = ort_build_scene(c, cr.data(), ma.data(), fr.data(), (int32_t)spheres.size(), octree.getMaxDepth(),
+                                 octree.getMaxSpheresPerNode(), 0);
+            float ms = 0.0f;
+            if (rc == ORT_OK) ort_last_build_ms(c, &ms);
+            gpuBuildSeconds = ms * 1e-3;
+        } else {
+            rc = ort_upload_octree_nodes(c, cr.data(), ma.data(), fr.data(), (int32_t)spheres.size(),
+                                         octree.flattenedTree.data(), (int32_t)octree.flattenedTree.size(),
+                                         octree.objectIndices.data(), (int64_t)octree.objectIndices.size());
+        }
+        if (rc != ORT_OK) std::cerr << "scene upload failed: " << ort_last_error(c) << std::endl;
     }
-    if (rc != ORT_OK) std::cerr << "scene upload failed: " << ort_last_error(ctx) << std::endl;
     sceneReady = rc == ORT_OK;
 }
 
 void Raytracer::cleanupBuffers() {
     if (ctx) ort_destroy(ctx);
+    if (group) ort_group_destroy(group);
     ctx = nullptr;
+    group = nullptr;
     sceneReady = false;
 }
 
@@ -103,7 +123,8 @@ ort_params Raytracer::frameParams(const Camera& cam) const {
 }
 
 int Raytracer::render(const Camera& cam, const ort_tile& tile, float* out, bool outIsDevice, void* stream) {
-    if (!ctx && !initialize()) return ORT_ERR_HIP;
+    if (!ctx && !group && !initialize()) return ORT_ERR_HIP;
+    if (group) return ORT_ERR_UNSUPPORTED;  // a group renders whole frames (render(cam, rgb))
     if (!sceneReady) {
         setupScene();
         setupBuffers();
@@ -114,6 +135,16 @@ int Raytracer::render(const Camera& cam, const ort_tile& tile, float* out, bool 
 }
 
 int Raytracer::render(const Camera& cam, float* rgb) {
+    if (!ctx && !group && !initialize()) return ORT_ERR_HIP;
+    if (group) {
+        if (!sceneReady) {
+            setupScene();
+            setupBuffers();
+            if (!sceneReady) return ORT_ERR_INVALID_ARG;
+        }
+        const ort_params p = frameParams(cam);
+        return ort_group_render(group, &p, rgb, 0);
+    }
     ort_tile t{0, width, 0, height, 0, 0};
     return render(cam, t, rgb, false, nullptr);
 }

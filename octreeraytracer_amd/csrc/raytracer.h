@@ -37,6 +37,9 @@ struct RaytracerConfig {
     // new knobs
     uint32_t seed = 42;            // replaces std::random_device in generateRandomSpheres
     int device = 0;                // HIP device of the context
+    std::vector<int> devices;      // several GPUs: an ort_group over these (bands dealt round-robin,
+                                   // RCCL gather to devices[0]; a device listed twice
+                                   // gathers by device copies instead); empty = `device` only
     int frames = 50;               // frames of run() (the reference stops after 50 with stats)
     int warmupFrames = 15;         // src/raytracer.cpp:455
     bool gpuBuild = false;         // build the octree on the GPU (ort_build_scene, same tree) instead
@@ -59,7 +62,8 @@ public:
     // first use.  Returns ORT_OK or an ORT_ERR_* code (message: lastError()).
     int render(const Camera& cam, float* rgb);
     // A tile (see ort_tile in include/ort.h) into host or device memory, optionally
-    // stream-ordered on a caller hipStream_t.
+    // stream-ordered on a caller hipStream_t.  Single-device configurations only (a group
+    // renders whole frames: ORT_ERR_UNSUPPORTED).
     int render(const Camera& cam, const ort_tile& tile, float* out, bool outIsDevice, void* stream);
 
     Camera camera;  // the reference keeps a global Camera (src/main.cpp:18); pose set like main()
@@ -73,6 +77,7 @@ private:
     RaytracerConfig cfg;
     int width, height;
     ort_ctx* ctx;
+    ort_group* group = nullptr;    // cfg.devices.size() > 1
     bool sceneReady;
     std::vector<Sphere> spheres;
     Octree octree;

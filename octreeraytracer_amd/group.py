@@ -1,0 +1,110 @@
+"""Several GPUs in one process behind the C ABI (include/ort.h ort_group_*): one context per
+device, the frame cut into 16-row bands dealt round-robin, ONE exchange -- the bands gathered
+to devices[0] over RCCL (or device copies) -- and a de-interleave kernel there (SURVEY.md
+8(e)).  The one-process-per-GPU path of bench.py (torch.distributed) partitions the frame
+identically (octreeraytracer_amd/distributed.py)."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib as L
+from .renderer import FrameParams
+from .scene import FlatOctree, SphereSet
+
+TRANSPORT_RCCL = L.ORT_GROUP_TRANSPORT_RCCL
+TRANSPORT_COPY = L.ORT_GROUP_TRANSPORT_COPY
+
+
+class RenderGroup:
+    def __init__(self, devices, transport: int = TRANSPORT_RCCL):
+        self._lib = L.lib()
+        self._g = C.c_void_p()
+        devs = (C.c_int32 * len(devices))(*[int(d) for d in devices])
+        rc = self._lib.ort_group_create(devs, len(devices), int(transport), C.byref(self._g))
+        if rc != L.ORT_OK:
+            raise L.OrtError(rc, self._lib.ort_group_last_error(None).decode())
+        self.devices = list(devices)
+
+    def _check(self, rc):
+        if rc != L.ORT_OK:
+            raise L.OrtError(rc, self._lib.ort_group_last_error(self._g).decode())
+
+    def close(self):
+        if self._g:
+            self._lib.ort_group_destroy(self._g)
+            self._g = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_option(self, option: int, value: int):
+        self._check(self._lib.ort_group_set_option(self._g, int(option), int(value)))
+
+    def build_scene(self, spheres: SphereSet, max_depth: int, max_spheres_per_node: int):
+        cr, ma, fr = (np.ascontiguousarray(a, np.float32) for a in (spheres.center_radius, spheres.mat_albedo,
+                                                                      spheres.fuzz_ri))
+        self._check(self._lib.ort_group_build_scene(self._g, L.fptr(cr), L.fptr(ma), L.fptr(fr), spheres.n,
+                                                    int(max_depth), int(max_spheres_per_node)))
+
+    def upload(self, spheres: SphereSet, tree: FlatOctree):
+        cr, ma, fr = (np.ascontiguousarray(a, np.float32) for a in (spheres.center_radius, spheres.mat_albedo,
+                                                                      spheres.fuzz_ri))
+        t = [np.ascontiguousarray(a, d) for a, d in (
+            (tree.node_min, np.float32), (tree.node_max, np.float32), (tree.children_offset, np.int32),
+            (tree.objects_offset, np.int32), (tree.object_count, np.int32), (tree.object_indices, np.int32))]
+        self._check(self._lib.ort_group_upload_scene(self._g, L.fptr(cr), L.fptr(ma), L.fptr(fr), spheres.n,
+                                                     L.fptr(t[0]), L.fptr(t[1]), L.iptr(t[2]), L.iptr(t[3]),
+                                                     L.iptr(t[4]), tree.n_nodes, L.iptr(t[5]), tree.n_indices))
+
+    def render(self, params: FrameParams, out=None):
+        """Full frame: a new (H, W, 3) float32 numpy array, a numpy array, or a float32 torch
+        tensor on devices[0] (device output)."""
+        p = params.to_c()
+        n = params.height * params.width * 3
+        if out is None:
+            out = np.empty((params.height, params.width, 3), np.float32)
+        if isinstance(out, np.ndarray):
+            if out.dtype != np.float32 or not out.flags.c_contiguous or out.size < n:
+                raise ValueError("render: out must be a contiguous float32 array of H*W*3 elements")
+            self._check(self._lib.ort_group_render(self._g, C.byref(p), out.ctypes.data_as(C.c_void_p), 0))
+            return out
+        import torch
+        if out.dtype != torch.float32 or not out.is_contiguous() or out.numel() < n:
+            raise ValueError("render: out must be a contiguous float32 tensor of H*W*3 elements")
+        if out.device.type != "cuda" or out.device.index != self.devices[0]:
+            raise ValueError(f"render: out is on {out.device}, the group assembles on cuda:{self.devices[0]}")
+        self._check(self._lib.ort_group_render(self._g, C.byref(p), C.c_void_p(out.data_ptr()), 1))
+        return out
+
+    def last_frame_ms(self) -> float:
+        ms = C.c_float()
+        self._check(self._lib.ort_group_last_frame_ms(self._g, C.byref(ms)))
+        return ms.value
+
+
+def emulate_group_host(spheres: SphereSet, tree: FlatOctree, params: FrameParams, world: int) -> np.ndarray:
+    """TEST-ONLY (no GPU): the group's partition and row map with an in-memory transport, each
+    band tile rendered by the host emulation of the kernel (ort_debug_group_emulate)."""
+    lib = L.lib()
+    out = np.empty((params.height, params.width, 3), np.float32)
+    cr, ma, fr = (np.ascontiguousarray(a, np.float32) for a in (spheres.center_radius, spheres.mat_albedo,
+                                                                  spheres.fuzz_ri))
+    t = [np.ascontiguousarray(a, d) for a, d in (
+        (tree.node_min, np.float32), (tree.node_max, np.float32), (tree.children_offset, np.int32),
+        (tree.objects_offset, np.int32), (tree.object_count, np.int32), (tree.object_indices, np.int32))]
+    p = params.to_c()
+    L.check(lib.ort_debug_group_emulate(L.fptr(cr), L.fptr(ma), L.fptr(fr), spheres.n, L.fptr(t[0]), L.fptr(t[1]),
+                                        L.iptr(t[2]), L.iptr(t[3]), L.iptr(t[4]), tree.n_nodes, L.iptr(t[5]),
+                                        tree.n_indices, int(world), C.byref(p), L.fptr(out)))
+    return out

@@ -37,3 +37,20 @@ def test_main_renders_and_writes_stats(ort, oracle, tmp_path, gpu_build):
     ref = oracle.render(s, t, ort.FrameParams.default_camera(64, 48))
     from octreeraytracer_amd.image import to_srgb8
     assert np.array_equal(read_ppm(ppm), to_srgb8(ref)[::-1])
+
+
+@pytest.mark.gpu
+def test_main_device_group(ort, oracle, tmp_path):
+    """Raytracer over an ort_group (cfg.devices): the frame is banded over the group's contexts
+    and gathered to devices[0]; on a one-GPU box device 0 is listed three times (the group then
+    gathers by device copies -- RCCL needs distinct devices)."""
+    ppm = tmp_path / "frame.ppm"
+    cmd = [str(EXE), "--spheres", "1000", "--depth", "5", "--per-node", "1", "--samples", "2", "--bounces", "3",
+           "--width", "160", "--height", "100", "--frames", "2", "--warmup", "1", "--devices", "0,0,0", "--ppm", str(ppm)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    s = ort.random_spheres(1000, 42)
+    t = ort.build_octree(s, 5, 1)
+    ref = oracle.render(s, t, ort.FrameParams.default_camera(160, 100, num_samples=2, max_depth=3))
+    from octreeraytracer_amd.image import to_srgb8
+    assert np.array_equal(read_ppm(ppm), to_srgb8(ref)[::-1])
