@@ -14,7 +14,7 @@ HOST_OBJS := $(addprefix $(OBJ)/,$(HOST_SRCS:.cpp=.o))
 HIP_OBJS := $(OBJ)/ort_kernel.o $(OBJ)/gpu_build.o $(OBJ)/group.o
 HDRS := $(wildcard $(SRC)/*.h) $(SRC)/prebuilt_scene.inc include/ort.h include/ort_math.h
 
-.PHONY: all lib oracle ref examples clean
+.PHONY: all lib oracle ref examples san clean
 all: lib oracle examples
 
 lib: $(LIB)
@@ -39,13 +39,51 @@ $(LIB): $(HOST_OBJS) $(HIP_OBJS)
 	@mkdir -p $(dir $(LIB))
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -ldl -Wl,-soname,libort.so
 
-examples: build/ort_main
+examples: build/ort_main build/stats_row
+
+build/stats_row: tests/cpp/stats_row.cpp $(LIB) $(HDRS)
+	$(CXX) -O2 -std=c++17 -I$(SRC) -o $@ tests/cpp/stats_row.cpp -L$(dir $(LIB)) -lort -Wl,-rpath,'$$ORIGIN/../$(dir $(LIB))'
 
 build/ort_main: examples/main.cpp $(LIB) $(HDRS)
 	$(CXX) -O2 -std=c++17 -I$(SRC) -o $@ examples/main.cpp -L$(dir $(LIB)) -lort -Wl,-rpath,'$$ORIGIN/../$(dir $(LIB))'
 
 oracle:
 	$(MAKE) -C oracle all
+
+# Host AddressSanitizer + UndefinedBehaviorSanitizer build (CPU only; GPU sanitizers are not
+# available): every host object -- scene stage, octree builder, layout compilers, host ABI,
+# the kernel's per-pixel code compiled for the host, the group row map, the oracle -- built
+# with clang and instrumented, linked into build/san/san_check (tests/cpp/san_check.cpp),
+# which renders small frames through the emulation and the oracle and compares bits.
+SAN := -fsanitize=address,undefined -fno-sanitize-recover=undefined -fno-omit-frame-pointer -g -O1
+SANOBJ := build/san
+CLANGXX := /opt/rocm/bin/amdclang++
+CLANG := /opt/rocm/bin/amdclang
+SAN_HOST := $(addprefix $(SANOBJ)/,$(HOST_SRCS:.cpp=.o))
+SAN_HIP := $(SANOBJ)/ort_kernel.o $(SANOBJ)/gpu_build.o $(SANOBJ)/group.o
+HIP_SAN := $(foreach f,address undefined,-Xarch_host -fsanitize=$(f)) -Xarch_host -fno-sanitize-recover=undefined
+
+san: build/san/san_check
+	ASAN_OPTIONS=detect_leaks=1:abort_on_error=1 UBSAN_OPTIONS=print_stacktrace=1 ./build/san/san_check
+
+$(SANOBJ)/%.o: $(SRC)/%.cpp $(HDRS)
+	@mkdir -p $(SANOBJ)
+	$(CLANGXX) $(SAN) -std=c++17 -ffp-contract=off -fno-fast-math -c $< -o $@
+
+$(SANOBJ)/%.o: $(SRC)/%.hip $(HDRS) $(SRC)/gpu_build.h $(SRC)/group_map.h
+	@mkdir -p $(SANOBJ)
+	$(HIPCC) -O1 -g -std=c++17 --offload-arch=$(ARCH) -ffp-contract=off -fno-fast-math -fno-slp-vectorize -Wno-unused-result $(HIP_SAN) -c $< -o $@
+
+$(SANOBJ)/ort_oracle.o: oracle/ort_oracle.c oracle/ort_oracle.h include/ort_math.h
+	@mkdir -p $(SANOBJ)
+	$(CLANG) $(SAN) -std=c11 -ffp-contract=off -fno-fast-math -c $< -o $@
+
+$(SANOBJ)/san_check.o: tests/cpp/san_check.cpp $(HDRS) oracle/ort_oracle.h
+	@mkdir -p $(SANOBJ)
+	$(CLANGXX) $(SAN) -std=c++17 -I$(SRC) -Ioracle -c $< -o $@
+
+build/san/san_check: $(SANOBJ)/san_check.o $(SAN_HOST) $(SAN_HIP) $(SANOBJ)/ort_oracle.o
+	$(HIPCC) --offload-arch=$(ARCH) $(SAN) -o $@ $^ -ldl
 
 ref:
 	$(MAKE) -C oracle ref

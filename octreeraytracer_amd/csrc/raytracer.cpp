@@ -5,6 +5,9 @@
 #include <cmath>
 #include <fstream>
 #include <iostream>
+#include <sstream>
+
+#include <sched.h>
 
 #include "scene.h"
 
@@ -168,21 +171,16 @@ void Raytracer::run() {
             frameCount++;
         }
     }
-    if (cfg.collectStats) saveStats();
+    if (cfg.collectStats) {
+        if (cfg.extendedStats && !countWork()) std::cerr << "counting the frame's work failed: " << lastError() << std::endl;
+        saveStats();
+    }
 }
 
 // saveStats (src/raytracer.cpp:359-449): 2.5-sigma z-score filter, one ';' row.
-void Raytracer::saveStats() {
-    if (renderTimes.empty()) {
-        std::cout << "No render times recorded." << std::endl;
-        return;
-    }
-    std::ofstream outFile(statsFilename, std::ios::out | std::ios::app);
-    if (!outFile || !outFile.is_open()) {
-        std::cerr << "Error opening file for writing: " << statsFilename << std::endl;
-        return;
-    }
-    const std::vector<double>& all = renderTimes;
+std::string Raytracer::statsRow(const RaytracerConfig& cfg, const std::vector<double>& all, double buildSeconds,
+                                const StatsWork* w) {
+    if (all.empty()) return std::string();
     double sum = 0.0;
     for (double t : all) sum += t;
     const double mean = sum / all.size();
@@ -205,7 +203,7 @@ void Raytracer::saveStats() {
         mx = std::max(mx, t);
         fpsTotal += 1.0 / t;
     }
-    if (clean.empty()) {
+    if (clean.empty()) {  // every sample an outlier (all equal: stdDev 0, z NaN): the unfiltered data
         clean = all;
         total = sum;
         for (double t : clean) {
@@ -216,8 +214,49 @@ void Raytracer::saveStats() {
     }
     const double avg = total / clean.size();
     const double fpsAvg = fpsTotal / clean.size();
-    outFile << cfg.useOctree << ";" << cfg.numSpheres << ";" << cfg.maxDepth << ";" << cfg.maxSpheresPerNode << ";"
-            << cfg.numSamples << ";" << cfg.maxRaysDepth << ";" << cfg.width << ";" << cfg.height << ";" << mn << ";" << mx
-            << ";" << avg << ";" << 1.0 / mx << ";" << 1.0 / mn << ";" << fpsAvg << ";"
-            << ((cfg.gpuBuild && !cfg.debug) ? gpuBuildSeconds : octree.buildTime) << std::endl;
+    std::ostringstream row;
+    row << cfg.useOctree << ";" << cfg.numSpheres << ";" << cfg.maxDepth << ";" << cfg.maxSpheresPerNode << ";"
+        << cfg.numSamples << ";" << cfg.maxRaysDepth << ";" << cfg.width << ";" << cfg.height << ";" << mn << ";" << mx
+        << ";" << avg << ";" << 1.0 / mx << ";" << 1.0 / mn << ";" << fpsAvg << ";" << buildSeconds;
+    if (w) {
+        const double mrays = (double)w->traversals / avg / 1e6;
+        const double bytesPerRay = w->traversals ? w->algorithmicBytes / (double)w->traversals : 0.0;
+        const double hbmPeakBytes = 8.0e12;  // MI355X HBM3E
+        row << ";" << mrays << ";" << bytesPerRay << ";" << mrays * 1e6 * bytesPerRay / hbmPeakBytes << ";" << w->gpus
+            << ";" << w->hostCores;
+    }
+    return row.str();
+}
+
+void Raytracer::saveStats() {
+    if (renderTimes.empty()) {
+        std::cout << "No render times recorded." << std::endl;
+        return;
+    }
+    std::ofstream outFile(statsFilename, std::ios::out | std::ios::app);
+    if (!outFile || !outFile.is_open()) {
+        std::cerr << "Error opening file for writing: " << statsFilename << std::endl;
+        return;
+    }
+    const double build = (cfg.gpuBuild && !cfg.debug) ? gpuBuildSeconds : octree.buildTime;
+    outFile << statsRow(cfg, renderTimes, build, cfg.extendedStats ? &work : nullptr) << std::endl;
+}
+
+// The frame's work for the extended columns: the counting variant of the kernel over the
+// full frame (untimed; on devices[0]'s context for a group, which holds the same scene).
+bool Raytracer::countWork() {
+    ort_ctx* c = ctx;
+    if (group && ort_group_context(group, 0, &c) != ORT_OK) return false;
+    const ort_params p = frameParams(camera);
+    const ort_tile t{0, width, 0, height, 0, 0};
+    uint64_t n[ORT_COUNT_N] = {0};
+    if (ort_count_traffic(c, &p, &t, n) != ORT_OK) return false;
+    work.traversals = n[ORT_COUNT_TRAVERSALS];
+    work.algorithmicBytes = 36.0 * n[ORT_COUNT_NODES_POPPED] + 32.0 * n[ORT_COUNT_CHILD_RECORDS] +
+                            20.0 * n[ORT_COUNT_LEAF_OBJECTS] + 32.0 * n[ORT_COUNT_ACCEPTED_HITS] +
+                            12.0 * n[ORT_COUNT_PIXELS];
+    work.gpus = group ? ort_group_size(group) : 1;
+    cpu_set_t set;
+    work.hostCores = sched_getaffinity(0, sizeof(set), &set) == 0 ? CPU_COUNT(&set) : 1;
+    return true;
 }

@@ -44,6 +44,17 @@ struct RaytracerConfig {
     int warmupFrames = 15;         // src/raytracer.cpp:455
     bool gpuBuild = false;         // build the octree on the GPU (ort_build_scene, same tree) instead
                                    // of Octree::build on the host; getOctree() then stays empty
+    bool extendedStats = false;    // saveStats appends 5 throughput columns to the reference's 15
+                                   // (see StatsWork / Raytracer::statsRow)
+};
+
+// Work of one frame for the extended stats columns: ort_count_traffic over the full frame
+// (reference-layout counters), plus the device and host-core counts.
+struct StatsWork {
+    uint64_t traversals = 0;       // octree walks per frame (all samples and bounces)
+    double algorithmicBytes = 0;   // 36/node popped + 32/child record + 20/leaf object + 32/hit + 12/pixel
+    int gpus = 1;
+    int hostCores = 1;
 };
 
 class Raytracer {
@@ -73,6 +84,18 @@ public:
     const std::vector<double>& getRenderTimes() const { return renderTimes; }
     const char* lastError() const;
 
+    // The saveStats row for these frame times (seconds), without the newline: the reference's
+    // 15 ';'-separated columns (src/raytracer.cpp:441-446: useOctree, numSpheres, maxDepth,
+    // maxSpheresPerNode, numSamples, maxRaysDepth, width, height, min, max, avg, minFPS,
+    // maxFPS, fpsAvg, buildTime) after its 2.5-sigma z-score filter (:372-434), then, when
+    // `work` is given, mrays_per_s (traversals / avg frame time), bytes_per_ray (algorithmic
+    // reference-layout bytes / traversal), roofline_fraction (mrays_per_s x bytes_per_ray /
+    // 8 TB/s: SURVEY.md 8(d)'s algorithmic fraction -- it can exceed 1, the scene being
+    // cache-resident; bench.py reports the measured VALU-issue roofline), gpus, host_cores.
+    // Returns "" for no frames.
+    static std::string statsRow(const RaytracerConfig& cfg, const std::vector<double>& frameSeconds,
+                                double buildSeconds, const StatsWork* work);
+
 private:
     RaytracerConfig cfg;
     int width, height;
@@ -86,6 +109,7 @@ private:
     std::vector<double> renderTimes;
     std::vector<float> frame;
     double gpuBuildSeconds = 0.0;
+    StatsWork work;               // counted after the timed frames when cfg.extendedStats
 
     void setupScene();
     void setupBuffers();
@@ -94,5 +118,6 @@ private:
     std::vector<Sphere> generatePreBuiltSpheres();
     std::vector<Sphere> generateRandomSpheres();
     void saveStats();
+    bool countWork();
     ort_params frameParams(const Camera& cam) const;
 };

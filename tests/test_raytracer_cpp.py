@@ -54,3 +54,24 @@ def test_main_device_group(ort, oracle, tmp_path):
     ref = oracle.render(s, t, ort.FrameParams.default_camera(160, 100, num_samples=2, max_depth=3))
     from octreeraytracer_amd.image import to_srgb8
     assert np.array_equal(read_ppm(ppm), to_srgb8(ref)[::-1])
+
+
+@pytest.mark.gpu
+def test_sweep_extended_rows(tmp_path):
+    """tools/sweep.py drives ort_main over grid points; each run appends a 20-column row."""
+    import sys
+    sys.path.insert(0, str(ROOT / "tools"))
+    import sweep
+    csv = tmp_path / "stats.csv"
+    for grid in ("bench", "runner"):  # C1 (octree) and the runner's first point (brute force, 4 spp x 4 bounces)
+        rc = sweep.main(["--grid", grid, "--limit", "1", "--frames", "4", "--warmup", "1", "--out", str(csv),
+                         "--timeout", "120"])
+        assert rc == 0
+    rows = sweep.parse_stats(csv)
+    assert len(rows) == 2 and all(len(r) == 20 for r in rows)
+    c1, bf = rows
+    assert (c1["Uses Octree"], c1["Spheres"], c1["Screen Width"]) == (1, 100, 256)
+    assert c1["mrays_per_s"] * 1e6 * c1["Avg"] == pytest.approx(256 * 256, rel=1e-3)  # one traversal per pixel
+    assert c1["bytes_per_ray"] > 12 and c1["gpus"] == 1 and c1["host_cores"] >= 1
+    assert (bf["Uses Octree"], bf["Max Octree Depth"], bf["Num Samples"]) == (0, -1, 4)
+    assert bf["mrays_per_s"] > 0
