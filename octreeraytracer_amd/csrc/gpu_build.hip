@@ -234,7 +234,7 @@ __global__ void k_compact_nodes(const int32_t* co, const int32_t* oo, const int3
     for (int64_t i = blockIdx.x * (int64_t)kB + threadIdx.x; i < n; i += (int64_t)gridDim.x * kB) {
         const int32_t c = co[i];
         if (c != -1) {
-            uint32_t mask = 0;
+            uint32_t mask = 0, leaves = 0;
             bool leafkids = true;
             for (int k = 0; k < 8; ++k) {
                 const int64_t j = (int64_t)c + k;
@@ -242,8 +242,10 @@ __global__ void k_compact_nodes(const int32_t* co, const int32_t* oo, const int3
                 if (co[j] != -1) leafkids = false;
                 if (co[j] == -1 && oo[j] == -1) continue;  // empty leaf, glsl:467
                 mask |= 1u << k;
+                if (co[j] == -1) leaves |= 1u << k;
             }
-            node[i] = make_uint2((uint32_t)c, 0x80000000u | (leafkids ? 0x40000000u : 0u) | mask);
+            // bits 8-15: the existing children that are leaves (render_core.h ORT_LEAFMASK_SHIFT)
+            node[i] = make_uint2((uint32_t)c, 0x80000000u | (leafkids ? 0x40000000u : 0u) | (leaves << 8) | mask);
         } else {
             const int32_t v = cnt[i] > 0 ? cnt[i] : 0;
             // one-sphere leaves point into the per-sphere tail (layout.h)

@@ -127,7 +127,7 @@ bool buildCompactLayout(const SceneInput& in, int maxDepth, CompactLayout& out, 
     for (int32_t i = 0; i < n; ++i) {
         const int32_t co = in.co[i];
         if (co != -1) {
-            uint32_t mask = 0;
+            uint32_t mask = 0, leaves = 0;
             bool leafkids = true;
             for (int k = 0; k < 8; ++k) {
                 const int64_t c = (int64_t)co + k;
@@ -135,9 +135,11 @@ bool buildCompactLayout(const SceneInput& in, int maxDepth, CompactLayout& out, 
                 if (in.co[c] != -1) leafkids = false;
                 if (in.co[c] == -1 && in.oo[c] == -1) continue;  // empty leaf, glsl:467
                 mask |= 1u << k;
+                if (in.co[c] == -1) leaves |= 1u << k;
             }
             out.node[2 * (size_t)i] = (uint32_t)co;
-            out.node[2 * (size_t)i + 1] = ORT_INTERNAL_FLAG_HOST | (leafkids ? ORT_LEAFKIDS_FLAG_HOST : 0u) | mask;
+            out.node[2 * (size_t)i + 1] = ORT_INTERNAL_FLAG_HOST | (leafkids ? ORT_LEAFKIDS_FLAG_HOST : 0u) |
+                                          (leaves << ORT_LEAFMASK_SHIFT_HOST) | mask;
         } else {
             const int32_t cntv = in.cnt[i] > 0 ? in.cnt[i] : 0;
             // one-sphere leaves point into the per-sphere tail (layout.h)

@@ -6,8 +6,10 @@
 // 32 B per child box examined (glsl:318-324, 459-462).
 //
 // Compact layout (MI355X):
-//   node[i] (8 B):  internal -> {childrenOffset, 0x80000000 | leafKids << 30 | childMask}
+//   node[i] (8 B):  internal -> {childrenOffset, 0x80000000 | leafKids << 30 | leafMask << 8 | childMask}
 //     leafKids: every existing child is a leaf (the kernel then tests them inline)
+//     leafMask bit k = child k is in childMask and is a leaf (deep walks test a node's leading
+//     leaf children inline: render_core.h fast_step)
 //                   leaf     -> {objectsOffset, objectCount}
 //     childMask bit k = child (childrenOffset + k) is in range and is not an empty leaf
 //     (the glsl:456 and glsl:467 skip tests, precomputed).

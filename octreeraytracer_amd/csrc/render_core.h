@@ -45,6 +45,8 @@
 #define ORT_MAX_STACK 200
 #define ORT_INTERNAL_FLAG 0x80000000u
 #define ORT_LEAFKIDS_FLAG 0x40000000u  // internal node whose existing children are all leaves
+// internal record bits 8-15: which existing (pushable) children are leaves, octant space
+#define ORT_LEAFMASK_SHIFT 8
 #define ORT_MAXFLOAT 3.402823466e+38f
 
 namespace ort {
@@ -564,6 +566,8 @@ struct Masks64 {  // levels 0..7: trees of depth <= 8
     // test the leaf children of a LEAFKIDS node inline (fast_step); pays for its registers on
     // depth <= 8 trees (all leaves at the bottom level with maxSpheresPerNode 0), not deeper
     static constexpr bool kInlineLeaves = true;
+    // test a node's LEADING leaf children inline (see fast_step): deep trees
+    static constexpr bool kLeadLeaves = false;
     static constexpr bool kRevPlanes = true;  // depth <= 8: reversed plane tables (fast_rev_planes)
     static constexpr bool kKeepNear = true;   // keep the node's near-plane pointers (FastStateT::nA..)
     uint64_t m;
@@ -591,6 +595,10 @@ struct Masks64 {  // levels 0..7: trees of depth <= 8
 };
 struct Masks96 {  // levels 0..11
     static constexpr bool kInlineLeaves = false;
+#ifndef ORT_LEAD_LEAVES_DEEP
+#define ORT_LEAD_LEAVES_DEEP 1
+#endif
+    static constexpr bool kLeadLeaves = ORT_LEAD_LEAVES_DEEP;
     static constexpr bool kRevPlanes = false;
     static constexpr bool kKeepNear = true;
     uint64_t lo;
@@ -702,6 +710,12 @@ using FastState = FastStateT<Masks96>;
 // the near-plane pointers cost occupancy, so it re-derives them from cP.
 struct Masks96Lean : Masks96 {
     static constexpr bool kKeepNear = false;
+    // leading leaf children inline: C5 camera rays (deep kernel) 19.45 -> 17.62 ms, but the
+    // persistent bounce kernel 4.8 ms slower per frame (tools/ab_stream.py): off there
+#ifndef ORT_LEAD_LEAVES_PERSISTENT
+#define ORT_LEAD_LEAVES_PERSISTENT 0
+#endif
+    static constexpr bool kLeadLeaves = ORT_LEAD_LEAVES_PERSISTENT;
 };
 // Depth <= 8 walk without the inline leaf children: the persistent bounce kernel's walk
 // (inline leaves pay off on coherent camera rays, not on scattered bounce rays).
@@ -915,6 +929,16 @@ ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks
             // Every existing child is a leaf, so the reference pops the surviving ones next,
             // consecutively in rank order (a leaf pushes nothing): test them right here.
             if (leaf_kids<COUNT>(S, st, co, keep, tNA, tMA, tNB, tMB, nN, nF, cnt)) return true;
+        } else if (Masks::kLeadLeaves) {
+            // The surviving leaf children ranked before every surviving internal child are the
+            // nodes the reference pops next, consecutively (a leaf pushes nothing): test them
+            // here, push the rest.  Reversed rank bits: "before" = higher bits.
+            const uint32_t rl = rank_lut[((st.otab & 7u) << 8) | ((rec.y >> ORT_LEAFMASK_SHIFT) & 0xffu)];
+            const uint32_t kl = keep & rl, ki = keep & ~rl;
+            const uint32_t lead = ki ? kl & ~((2u << (31 - __builtin_clz(ki))) - 1u) : kl;
+            st.masks.put(st.depth, keep ^ lead);
+            fr.setCo(st.depth, co);
+            if (lead && leaf_kids<COUNT>(S, st, co, lead, tNA, tMA, tNB, tMB, nN, nF, cnt)) return true;
         } else {
             // level depth holds nothing yet (every deeper level is empty), so both writes are
             // harmless when no child survives
