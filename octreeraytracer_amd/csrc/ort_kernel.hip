@@ -879,7 +879,10 @@ struct ort_ctx {
     int xcd_swizzle = 2;  // ORT_OPT_XCD_SWIZZLE: workgroup -> tile order (block_tile)
     int wave_queue = 0;  // ORT_OPT_WAVE_QUEUE: per-lane walk from a wave-level block queue (opt-in)
     int packet = 0;     // ORT_OPT_PACKET: wave-level walk for camera rays (SALU-bound so far: off)
-    int sort_paths = 1; // ORT_OPT_SORT_PATHS: coherence-sort the alive paths between bounces
+    // ORT_OPT_SORT_PATHS: coherence-sort the alive paths between bounces.  Off by default: with the
+    // shade kernels in slot order the bounce traces gain ~0.7 ms per C5 frame from the sort but
+    // the keys + radix sort of every slot cost ~3 ms (frame 62.6 sorted vs 60.7 ms, A/B)
+    int sort_paths = 0;
     float root_lo[3] = {0, 0, 0}, root_hi[3] = {0, 0, 0};  // root box (coherence-sort key)
     DevBuf lut;         // rank LUT (global copy, for the packet kernel)
     ort::GpuTree tree;  // reference-layout tree of the last ort_build_scene(keep_tree)
@@ -1393,7 +1396,13 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                 }
             }
             if (!fuse) {
-                e = launch_shade(mode, b == 0, direct, a, (int)blocks, s);
+                // every slot in slot order (a dead path returns after reading its pd.w), not the
+                // trace's compacted list: the sorted list scatters the path-state reads and
+                // writes; in slot order they coalesce (C5 frame 65.4 -> 63.0 ms, A/B)
+                PipeArgs a2 = a;
+                a2.qlist = nullptr;
+                a2.qcount = nullptr;
+                e = launch_shade(mode, b == 0, direct, a2, (int)blocks, s);
                 if (e != hipSuccess) return hip_fail(ctx, e, "ort_shade_kernel launch");
             }
             if (compact && !a.nobounce && b + 1 < bounces) {  // the next bounce walks only the alive paths
