@@ -57,13 +57,6 @@ std::string gpuExplicitLayout(const GpuTree& t, hipStream_t s, ExplicitDev& out)
 }  // namespace ort
 
 namespace ort {
-// Path compaction between bounces (ort_kernel.hip): the indices i < n with pd[i].w != 0
-// (alive paths), in increasing order, and their number (device-side, no host sync).
-size_t selectAliveTempBytes(int n);
-hipError_t selectAlive(void* temp, size_t temp_bytes, const float4* pd, int n, int* out, int* count, hipStream_t s);
-}  // namespace ort
-
-namespace ort {
 // Coherence sort of the alive paths (ORT_OPT_SORT_PATHS): key = direction octant (3 bits) |
 // Morton code of the origin in the root box (7 bits per axis) | 2 bits per axis of the
 // normalised direction magnitude; dead slots get the largest

@@ -649,25 +649,6 @@ std::string gpuExplicitLayout(const GpuTree& t, hipStream_t s, ExplicitDev& out)
     return "";
 }
 
-namespace {
-struct AliveFlag {
-    __host__ __device__ bool operator()(const float4& v) const { return v.w != 0.0f; }
-};
-}  // namespace
-
-size_t selectAliveTempBytes(int n) {
-    size_t tb = 0;
-    auto flags = rocprim::make_transform_iterator((const float4*)nullptr, AliveFlag());
-    (void)rocprim::select(nullptr, tb, rocprim::counting_iterator<int>(0), flags, (int*)nullptr, (int*)nullptr,
-                          (size_t)std::max(n, 1));
-    return tb;
-}
-
-hipError_t selectAlive(void* temp, size_t temp_bytes, const float4* pd, int n, int* out, int* count, hipStream_t s) {
-    auto flags = rocprim::make_transform_iterator(pd, AliveFlag());
-    return rocprim::select(temp, temp_bytes, rocprim::counting_iterator<int>(0), flags, out, count, (size_t)n, s);
-}
-
 #ifndef ORT_SORT_KEY
 #define ORT_SORT_KEY 3  // 1: octant | origin Morton (9 bits/axis); 2: + direction bits (C5: 2% faster);
                         // 3: the Morton bits dealt to the axes by extent (anisotropic root boxes)

@@ -56,6 +56,8 @@ struct PipeArgs {
     const uint8_t* lut;  // global copy of the rank LUT (ort::rank_lut_entry), 8 x 256 bytes
     const int* qlist;    // bounce >= 1: the alive path slots (compacted, increasing), or null = all
     const int* qcount;   // their number (device)
+    int* qnext;          // shade kernels: append the paths that go on here (next bounce's list), or null
+    int* qnext_count;
     int2* hit;        // per path: {entry (-1 miss), t bits}
     int* defer_list;
     int* sync;        // [0] deferred count, [1] work cursor of the persistent trace
@@ -754,12 +756,12 @@ __global__ void __launch_bounds__(kBlock) ort_trace_exact(PipeArgs A) {
     flush_counts<COUNT>(cnt, A.counters);
 }
 
-// Bounce shading (glsl:607-627).  FIRST: bounce 0 (c = 1, importance = 1).
-// DIRECT (1 sample, 1 bounce): writes the final pixel.
+// Bounce shading (glsl:607-627) of path slot k.  FIRST: bounce 0 (c = 1, importance = 1).
+// DIRECT (1 sample, 1 bounce): writes the final pixel.  Returns true when the path goes on
+// to the next bounce.
 template <int MODE, bool FIRST, bool DIRECT>
-__global__ void __launch_bounds__(kBlock) ort_shade_kernel(PipeArgs A) {
-    int k = blockIdx.x * kBlock + threadIdx.x;
-    if (!FIRST && !list_slot(A, k)) return;
+__device__ __forceinline__ bool shade_slot(const PipeArgs& A, int k) {
+    if (!FIRST && !list_slot(A, k)) return false;
     int col, row;
     const bool in_tile = slot_coords(A, k, col, row);
     const int y = in_tile ? tile_row_to_y(A.tm, row) : 0;
@@ -770,7 +772,7 @@ __global__ void __launch_bounds__(kBlock) ort_shade_kernel(PipeArgs A) {
             o[0] = 0.0f; o[1] = 0.0f; o[2] = 0.0f;
         }
         if (FIRST && !DIRECT) A.pd[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // never alive (compaction)
-        return;
+        return false;
     }
     bool alive = true;
     ort::Ray ray;
@@ -786,7 +788,7 @@ __global__ void __launch_bounds__(kBlock) ort_shade_kernel(PipeArgs A) {
         ray = ort::primary_ray(A.pp, A.tm.x0 + col, y, A.sample, st);
     } else {
         ray = load_ray(A, k, alive);
-        if (!alive) return;
+        if (!alive) return false;
         const float2 r2 = A.prng[k];
         st.x = r2.x;
         st.y = r2.y;
@@ -830,6 +832,37 @@ __global__ void __launch_bounds__(kBlock) ort_shade_kernel(PipeArgs A) {
         }
         A.prng[k] = make_float2(st.x, st.y);
     }
+    return !DIRECT && !done;
+}
+
+// Appends slot k (where go) to list / count: one atomic per workgroup, the workgroup's slots
+// kept in increasing order.  Every thread of the workgroup must call it.
+__device__ inline void append_slots(bool go, int k, int* list, int* count) {
+    __shared__ int wcnt[kBlock / 64];
+    __shared__ int wbase;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const unsigned long long m = __ballot(go);
+    if (lane == 0) wcnt[w] = __popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int t = 0;
+        for (int i = 0; i < kBlock / 64; ++i) t += wcnt[i];
+        wbase = t ? atomicAdd(count, t) : 0;
+    }
+    __syncthreads();
+    int off = wbase;
+    for (int i = 0; i < w; ++i) off += wcnt[i];
+    const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    if (go) list[off + __popcll(m & below)] = k;
+}
+
+// Shades every path slot of its workgroup (slot order); with A.qnext, the paths that go on
+// are appended to the next bounce's list (the compaction, without a separate select pass).
+template <int MODE, bool FIRST, bool DIRECT>
+__global__ void __launch_bounds__(kBlock) ort_shade_kernel(PipeArgs A) {
+    const int k = blockIdx.x * kBlock + threadIdx.x;
+    const bool go = shade_slot<MODE, FIRST, DIRECT>(A, k);
+    if (!DIRECT && A.qnext) append_slots(go, k, A.qnext, A.qnext_count);
 }
 
 // col / ns, gamma (glsl:659-661) for the multi-sample / multi-bounce case.
@@ -1308,7 +1341,7 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     const bool sorted = compact && ctx->sort_paths;
     size_t qtemp_bytes = 0;
     if (compact) {
-        qtemp_bytes = sorted ? ort::sortAliveTempBytes((int)slots) : ort::selectAliveTempBytes((int)slots);
+        qtemp_bytes = sorted ? ort::sortAliveTempBytes((int)slots) : 0;
         if ((rc = ensure(ctx, ctx->qlist, 4 * slots)) || (rc = ensure(ctx, ctx->qcount, 64)) ||
             (rc = ensure(ctx, ctx->qtemp, std::max<size_t>(qtemp_bytes, 16))))
             return rc;
@@ -1402,6 +1435,14 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                 PipeArgs a2 = a;
                 a2.qlist = nullptr;
                 a2.qcount = nullptr;
+                if (compact && !sorted && !a.nobounce && b + 1 < bounces) {
+                    // the compaction: the shade kernel appends the paths that go on, one atomic
+                    // per workgroup (a separate rocprim::select pass over the slots cost 0.55 ms
+                    // per C5 bounce); this bounce's list has been read by now
+                    HIPCHK(ctx, hipMemsetAsync(ctx->qcount.p, 0, sizeof(int), s));
+                    a2.qnext = (int*)ctx->qlist.p;
+                    a2.qnext_count = (int*)ctx->qcount.p;
+                }
                 e = launch_shade(mode, b == 0, direct, a2, (int)blocks, s);
                 if (e != hipSuccess) return hip_fail(ctx, e, "ort_shade_kernel launch");
             }
@@ -1411,11 +1452,8 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                                               (int*)ctx->qlist.p};
                     e = ort::sortAlive(ctx->qtemp.p, qtemp_bytes, (const float4*)ctx->po.p, (const float4*)ctx->pd.p,
                                        (int)slots, ctx->root_lo, ctx->root_hi, sb, (int*)ctx->qcount.p, s);
-                } else {
-                    e = ort::selectAlive(ctx->qtemp.p, qtemp_bytes, (const float4*)ctx->pd.p, (int)slots,
-                                         (int*)ctx->qlist.p, (int*)ctx->qcount.p, s);
-                }
-                if (e != hipSuccess) return hip_fail(ctx, e, "path compaction");
+                    if (e != hipSuccess) return hip_fail(ctx, e, "path compaction");
+                }  // else the shade kernel appended them
                 a.qlist = (const int*)ctx->qlist.p;
                 a.qcount = (const int*)ctx->qcount.p;
             }
