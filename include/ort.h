@@ -97,6 +97,9 @@ typedef struct ort_scene_info {
                                       runs of consecutive raster tiles (about 1/15 of a tile row, a power
                                       of two: 16 at 3840 px); 1: each XCD renders 128x128-pixel
                                       super-tiles; 0: raster order (tile b on XCD b % 8) */
+#define ORT_OPT_KID_SKIP 9         /* 1 (default): a lane skips one-sphere leaf children holding the sphere it
+                                      last rejected at a tmin <= theirs (they cannot end the walk; same
+                                      pixels, kid_table.h); 0: walk them as the reference does */
 
 /* Traffic counters (ort_count_traffic), in the REFERENCE layout's terms. */
 #define ORT_COUNT_NODES_POPPED 0

@@ -30,6 +30,7 @@ ORT_OPT_PACKET = 5
 ORT_OPT_SORT_PATHS = 6
 ORT_OPT_WAVE_QUEUE = 7
 ORT_OPT_XCD_SWIZZLE = 8
+ORT_OPT_KID_SKIP = 9
 ORT_LAYOUT_COMPACT_EXACT_EMULATION = 2
 ORT_COUNT_N = 6
 COUNT_NAMES = ("nodes_popped", "child_records", "leaf_objects", "accepted_hits", "pixels", "traversals")

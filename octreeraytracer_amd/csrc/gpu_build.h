@@ -39,6 +39,7 @@ std::string gpuBuildOctree(const float4* spheres, int32_t n, int32_t maxDepth, i
 // tree does not fit the compact layout (depth, 4 GiB offsets, plane check).
 struct CompactDev {
     uint2* node = nullptr;
+    uint2* kid = nullptr;  // rejected-sphere skip entries (kid_table.h), one per node
     float4* leaf_sph = nullptr;
     int32_t* leaf_idx = nullptr;
     float* planes = nullptr;

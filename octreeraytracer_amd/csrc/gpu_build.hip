@@ -29,6 +29,7 @@
 #include <rocprim/rocprim.hpp>
 
 #include "gpu_build.h"
+#include "kid_table.h"
 
 namespace ort {
 namespace {
@@ -230,7 +231,7 @@ __global__ void k_keys_to_idx(const unsigned long long* keys, int64_t n, int32_t
 
 // ---- compact / explicit layouts on the device (see layout.h for the compact format) ----
 __global__ void k_compact_nodes(const int32_t* co, const int32_t* oo, const int32_t* cnt, const int32_t* idx, int64_t n,
-                                int64_t ni, uint2* node) {
+                                int64_t ni, uint2* node, uint2* kid) {
     for (int64_t i = blockIdx.x * (int64_t)kB + threadIdx.x; i < n; i += (int64_t)gridDim.x * kB) {
         const int32_t c = co[i];
         if (c != -1) {
@@ -246,7 +247,16 @@ __global__ void k_compact_nodes(const int32_t* co, const int32_t* oo, const int3
             }
             // bits 8-15: the existing children that are leaves (render_core.h ORT_LEAFMASK_SHIFT)
             node[i] = make_uint2((uint32_t)c, 0x80000000u | (leafkids ? 0x40000000u : 0u) | (leaves << 8) | mask);
+            int32_t sid[8];
+            for (int k = 0; k < 8; ++k) {
+                const int64_t j = (int64_t)c + k;
+                sid[k] = (j < n && co[j] == -1 && cnt[j] == 1) ? idx[oo[j]] : -1;
+            }
+            uint32_t w0, w1;
+            kid_entry(sid, w0, w1);  // rejected-sphere skip entry (kid_table.h)
+            kid[i] = make_uint2(w0, w1);
         } else {
+            kid[i] = make_uint2(0u, 0u);
             const int32_t v = cnt[i] > 0 ? cnt[i] : 0;
             // one-sphere leaves point into the per-sphere tail (layout.h)
             node[i] = make_uint2(v == 1 ? (uint32_t)(ni + idx[oo[i]]) : (v > 0 ? (uint32_t)oo[i] : 0u), (uint32_t)v);
@@ -586,7 +596,7 @@ bool gpuCompactLayout(const GpuTree& t, const float4* sp, int maxDepth, hipStrea
     }
     auto fail = [&](const std::string& e) {
         why = e;
-        void* all[] = {out.node, out.leaf_sph, out.leaf_idx, out.planes};
+        void* all[] = {out.node, out.leaf_sph, out.leaf_idx, out.planes, out.kid};
         for (void* p : all)
             if (p) (void)hipFree(p);
         out = CompactDev();
@@ -596,7 +606,7 @@ bool gpuCompactLayout(const GpuTree& t, const float4* sp, int maxDepth, hipStrea
     const int D = t.depth;
     const int64_t np = 3 * (((int64_t)1 << D) + 1);
     std::string e;
-    if (!(e = dalloc(out.node, n)).empty() || !(e = dalloc(out.leaf_sph, ne)).empty() ||
+    if (!(e = dalloc(out.node, n)).empty() || !(e = dalloc(out.kid, n)).empty() || !(e = dalloc(out.leaf_sph, ne)).empty() ||
         !(e = dalloc(out.leaf_idx, ne)).empty() || !(e = dalloc(out.planes, np)).empty())
         return fail(e);
     out.node_bytes = (size_t)n * 8;
@@ -609,7 +619,8 @@ bool gpuCompactLayout(const GpuTree& t, const float4* sp, int maxDepth, hipStrea
         int* p;
         ~Free() { (void)hipFree(p); }
     } fb{bad};
-    hipLaunchKernelGGL(k_compact_nodes, dim3(grid_for(n)), dim3(kB), 0, s, t.co, t.oo, t.cnt, t.idx, n, ni, out.node);
+    hipLaunchKernelGGL(k_compact_nodes, dim3(grid_for(n)), dim3(kB), 0, s, t.co, t.oo, t.cnt, t.idx, n, ni, out.node,
+                       out.kid);
     if (ne > 0)
         hipLaunchKernelGGL(k_leaf_gather, dim3(grid_for(ne)), dim3(kB), 0, s, t.idx, ni, ne, sp, out.leaf_sph,
                            out.leaf_idx);

@@ -3,6 +3,7 @@
 
 #include <cstring>
 
+#include "kid_table.h"
 #include "render_core_flags.h"
 
 namespace ort {
@@ -122,8 +123,9 @@ bool buildCompactLayout(const SceneInput& in, int maxDepth, CompactLayout& out, 
             const uint32_t qnan = 0x7fc00000u;
             std::memcpy(&out.planes[k], &qnan, 4);
         }
-    // Node records.
+    // Node records, and the rejected-sphere skip entries (kid_table.h).
     out.node.assign(2 * (size_t)n, 0u);
+    out.kid.assign(2 * (size_t)n, 0u);
     for (int32_t i = 0; i < n; ++i) {
         const int32_t co = in.co[i];
         if (co != -1) {
@@ -140,6 +142,12 @@ bool buildCompactLayout(const SceneInput& in, int maxDepth, CompactLayout& out, 
             out.node[2 * (size_t)i] = (uint32_t)co;
             out.node[2 * (size_t)i + 1] = ORT_INTERNAL_FLAG_HOST | (leafkids ? ORT_LEAFKIDS_FLAG_HOST : 0u) |
                                           (leaves << ORT_LEAFMASK_SHIFT_HOST) | mask;
+            int32_t sid[8];
+            for (int k = 0; k < 8; ++k) {
+                const int64_t c = (int64_t)co + k;
+                sid[k] = (c < n && in.co[c] == -1 && in.cnt[c] == 1) ? in.indices[in.oo[c]] : -1;
+            }
+            kid_entry(sid, out.kid[2 * (size_t)i], out.kid[2 * (size_t)i + 1]);
         } else {
             const int32_t cntv = in.cnt[i] > 0 ? in.cnt[i] : 0;
             // one-sphere leaves point into the per-sphere tail (layout.h)

@@ -16,6 +16,7 @@
 //   leaf_sph[e] = spheres[objectIndices[e]] with .w = radius * radius (16 B): one gather
 //   instead of index + sphere, and the sphere test's r * r precomputed (rounded as it would be).
 //   leaf_idx[e] = objectIndices[e], read only for the final hit (material lookup).
+//   kid[i] (8 B): internal node i's rejected-sphere skip entry (kid_table.h).
 //   Both arrays carry a per-sphere TAIL after the n_indices entries: entry n_indices + s is
 //   sphere s.  A leaf holding exactly one sphere s records objectsOffset = n_indices + s, so
 //   its test reads the sphere table (16 B x spheres: cache-resident even at 1M spheres)
@@ -58,6 +59,7 @@ struct CompactLayout {
     std::vector<uint32_t> node;    // 2 per node
     std::vector<float> leaf_sph;   // 4 per index entry
     std::vector<int32_t> leaf_idx; // 1 per index entry
+    std::vector<uint32_t> kid;     // 2 per node: rejected-sphere skip entries (kid_table.h)
     // Every reachable box has min <= max and no NaN coordinate: then the plane tables are
     // monotone and the kernel's sign-decided fast walk applies; otherwise every ray takes
     // the exact (GLSL min/max) walk.

@@ -233,13 +233,13 @@ __global__ void __launch_bounds__(kBlock) ort_raygen_kernel(PipeArgs A) {
 // chunk, MI355X_MICROARCH.md 'dequeue') and hands the next slots of its chunk to lanes
 // that finished, so the wave stays full until the queue drains.  Rays the fast walk
 // cannot take are appended to the defer list for ort_trace_exact.
-// Waves per SIMD (minimum, amdgpu_waves_per_eu): the per-lane trace kernels run at 8 (56-60
-// VGPRs, spill-free; tools/kernel_resources.py); the persistent kernel's hint is 5 and the
-// compiler lands at 79 VGPRs / 6 waves for the 96-bit (depth > 8) walk and at 71 VGPRs /
-// 7 waves for the 64-bit one -- forced to 8 the 96-bit walk spills and C5 runs 11 % slower,
-// at 7 no faster (tools/ab_stream.py).
+// Waves per SIMD (minimum, amdgpu_waves_per_eu): the per-lane trace kernels run at 8 (59-64
+// VGPRs, spill-free; tools/kernel_resources.py).  The persistent bounce kernel is asked for 6:
+// with the rejected-sphere skip its 96-bit walk needs 87 VGPRs unconstrained (5 waves), at 6
+// waves it fits 80 with 5 spilled (C5 frame -2.4 % vs 5 waves, tools/ab_stream.py); the LDS
+// image (24.6 KB per workgroup at depth 10) caps it at 6 anyway.
 #ifndef ORT_PERSISTENT_WAVES
-#define ORT_PERSISTENT_WAVES 5
+#define ORT_PERSISTENT_WAVES 6
 #endif
 #ifndef ORT_TRACE_WAVES
 #define ORT_TRACE_WAVES 8
@@ -910,6 +910,7 @@ struct ort_ctx {
     void* wclock = nullptr;  // ort_debug_wave_clock
     long long wclock_n = 0;
     int xcd_swizzle = 2;  // ORT_OPT_XCD_SWIZZLE: workgroup -> tile order (block_tile)
+    int kid_skip = 1;     // ORT_OPT_KID_SKIP: rejected-sphere skip of one-sphere leaf children
     int wave_queue = 0;  // ORT_OPT_WAVE_QUEUE: per-lane walk from a wave-level block queue (opt-in)
     int packet = 0;     // ORT_OPT_PACKET: wave-level walk for camera rays (SALU-bound so far: off)
     // ORT_OPT_SORT_PATHS: coherence-sort the alive paths between bounces.  Off by default: with the
@@ -927,7 +928,7 @@ struct ort_ctx {
     int32_t n_spheres = 0, n_nodes = 0;
     int64_t n_indices = 0;
     DevBuf sph_cr, sph_ma, sph_fr;
-    DevBuf node, leaf_sph, leaf_idx, planes;    // compact
+    DevBuf node, leaf_sph, leaf_idx, planes, kid;  // compact
     DevBuf lds_img;                              // compact: the workgroup LDS image (k_lds_image)
     DevBuf nodeA, nodeB, cnt, indices;           // explicit
     DevBuf scratch_out, counters;
@@ -963,7 +964,7 @@ void free_buf(DevBuf& b) {
 }
 
 void free_scene(ort_ctx* c) {
-    DevBuf* all[] = {&c->sph_cr, &c->sph_ma, &c->sph_fr, &c->node, &c->leaf_sph, &c->leaf_idx,
+    DevBuf* all[] = {&c->sph_cr, &c->sph_ma, &c->sph_fr, &c->node, &c->kid, &c->leaf_sph, &c->leaf_idx,
                      &c->planes, &c->lds_img, &c->nodeA, &c->nodeB, &c->cnt, &c->indices};
     for (DevBuf* b : all) free_buf(*b);
     ort::freeGpuTree(c->tree);
@@ -1061,6 +1062,7 @@ int build_impl(ort_ctx* ctx, const float* cr, const float* ma, const float* fr, 
     if (compact_ok) {
         ctx->layout = ORT_LAYOUT_COMPACT;
         ctx->node = {cd.node, cd.node_bytes};
+        ctx->kid = {cd.kid, cd.node_bytes};
         ctx->leaf_sph = {cd.leaf_sph, cd.leaf_bytes};
         ctx->leaf_idx = {cd.leaf_idx, cd.idx_bytes};
         ctx->planes = {cd.planes, cd.plane_bytes};
@@ -1117,6 +1119,7 @@ int upload_impl(ort_ctx* ctx, const ort::SceneInput& in) {
             ctx->depth = cl.depth;
             ctx->ordered = cl.ordered;
             if ((rc = upload(ctx, ctx->node, cl.node.data(), 4 * cl.node.size()))) return rc;
+            if ((rc = upload(ctx, ctx->kid, cl.kid.data(), 4 * cl.kid.size()))) return rc;
             if ((rc = upload(ctx, ctx->leaf_sph, cl.leaf_sph.data(), 4 * cl.leaf_sph.size()))) return rc;
             if ((rc = upload(ctx, ctx->leaf_idx, cl.leaf_idx.data(), 4 * cl.leaf_idx.size()))) return rc;
             if ((rc = upload(ctx, ctx->planes, cl.planes.data(), 4 * cl.planes.size()))) return rc;
@@ -1156,6 +1159,8 @@ ort::KScene device_scene(const ort_ctx* c) {
     S.n_spheres = c->n_spheres;
     S.n_nodes = c->n_nodes;
     S.node = (const uint2*)c->node.p;
+    S.kid = c->kid_skip ? (const uint2*)c->kid.p : nullptr;
+    S.tail_base = (uint32_t)c->n_indices;
     S.leaf_sph = (const float4*)c->leaf_sph.p;
     S.node_bytes = (uint32_t)c->node.bytes;
     S.leaf_bytes = (uint32_t)c->leaf_sph.bytes;
@@ -1561,6 +1566,10 @@ int ort_set_option(ort_ctx* ctx, int option, int value) {
         ctx->packet = value ? 1 : 0;
         return ORT_OK;
     }
+    if (option == ORT_OPT_KID_SKIP) {
+        ctx->kid_skip = value ? 1 : 0;
+        return ORT_OK;
+    }
     if (option == ORT_OPT_XCD_SWIZZLE) {
         if (value < 0 || value > 2) return fail(ctx, ORT_ERR_INVALID_ARG, "xcd swizzle must be 0, 1 or 2");
         ctx->xcd_swizzle = value;
@@ -1634,7 +1643,7 @@ int ort_scene_get_info(const ort_ctx* ctx, ort_scene_info* info) {
     info->n_indices = ctx->n_indices;
     info->layout = ctx->layout;
     info->tree_depth = ctx->depth;
-    const DevBuf* all[] = {&ctx->sph_cr, &ctx->sph_ma, &ctx->sph_fr, &ctx->node, &ctx->leaf_sph, &ctx->leaf_idx,
+    const DevBuf* all[] = {&ctx->sph_cr, &ctx->sph_ma, &ctx->sph_fr, &ctx->node, &ctx->kid, &ctx->leaf_sph, &ctx->leaf_idx,
                            &ctx->planes, &ctx->lds_img, &ctx->nodeA, &ctx->nodeB, &ctx->cnt, &ctx->indices};
     int64_t b = 0;
     for (const DevBuf* d : all) b += (int64_t)d->bytes;
@@ -1800,6 +1809,8 @@ int ort_debug_emulate_render(const float* cr, const float* ma, const float* fr, 
                     return fail(nullptr, ORT_ERR_UNSUPPORTED, why);
                 mode = 0;
                 S.node = (const uint2*)cl.node.data();
+                S.kid = (const uint2*)cl.kid.data();
+                S.tail_base = (uint32_t)in.n_indices;
                 S.leaf_sph = (const float4*)cl.leaf_sph.data();
                 S.leaf_idx = cl.leaf_idx.data();
                 S.planes = cl.planes.data();
@@ -1899,6 +1910,8 @@ int ort_debug_wave_stats(const float* cr, const float* ma, const float* fr, int3
         S.n_spheres = n_spheres;
         S.n_nodes = n_nodes;
         S.node = (const uint2*)cl.node.data();
+        S.kid = (const uint2*)cl.kid.data();
+        S.tail_base = (uint32_t)in.n_indices;
         S.leaf_sph = (const float4*)cl.leaf_sph.data();
         S.leaf_idx = cl.leaf_idx.data();
         S.planes = cl.planes.data();
@@ -2005,6 +2018,8 @@ int64_t ort_debug_walk_steps(const float* cr, const float* ma, const float* fr, 
         S.n_spheres = n_spheres;
         S.n_nodes = n_nodes;
         S.node = (const uint2*)cl.node.data();
+        S.kid = (const uint2*)cl.kid.data();
+        S.tail_base = (uint32_t)in.n_indices;
         S.leaf_sph = (const float4*)cl.leaf_sph.data();
         S.leaf_idx = cl.leaf_idx.data();
         S.planes = cl.planes.data();

@@ -102,6 +102,8 @@ struct KScene {
     int depth;               // tree depth D (root = 0)
     uint32_t node_bytes;     // buffer sizes for the range-checked buffer loads (< 2^32)
     uint32_t leaf_bytes;
+    const uint2* kid;        // per node: rejected-sphere skip entry (kid_table.h), or null (off)
+    uint32_t tail_base;      // = n_indices: a one-sphere leaf's objectsOffset is tail_base + sphere
     // explicit (reference) layout
     const float4* nodeA;     // min.xyz, int bits of childrenOffset (binding 3)
     const float4* nodeB;     // max.xyz, int bits of objectsOffset  (binding 4)
@@ -548,6 +550,15 @@ ORT_FN uint2 fetch_node(const KScene& S, int i) {
     return S.node[i];
 #endif
 }
+ORT_FN uint2 fetch_kid(const KScene& S, int i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)S.kid, 0, (int)S.node_bytes, 0x00020000);
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, (uint32_t)i * 8u, 0, 0);
+    return make_uint2(v[0], v[1]);
+#else
+    return S.kid[i];
+#endif
+}
 ORT_FN float4 fetch_sphere(const KScene& S, int e) {
 #if defined(__HIP_DEVICE_COMPILE__)
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)S.leaf_sph, 0, (int)S.leaf_bytes, 0x00020000);
@@ -570,6 +581,9 @@ struct Masks64 {  // levels 0..7: trees of depth <= 8
     static constexpr bool kLeadLeaves = false;
     static constexpr bool kRevPlanes = true;  // depth <= 8: reversed plane tables (fast_rev_planes)
     static constexpr bool kKeepNear = true;   // keep the node's near-plane pointers (FastStateT::nA..)
+    // rejected-sphere skip (kid_table.h): off in the camera-ray walks, whose inline leaf
+    // children already avoid most leaf pops (C3 5 % slower with it), on in the bounce walks
+    static constexpr bool kKidSkip = false;
     uint64_t m;
     ORT_FN void clear() { m = 0; }
     ORT_FN bool empty() const { return m == 0; }
@@ -601,6 +615,7 @@ struct Masks96 {  // levels 0..11
     static constexpr bool kLeadLeaves = ORT_LEAD_LEAVES_DEEP;
     static constexpr bool kRevPlanes = false;
     static constexpr bool kKeepNear = true;
+    static constexpr bool kKidSkip = false;
     uint64_t lo;
     uint32_t hi;
     ORT_FN void clear() { lo = 0; hi = 0; }
@@ -679,6 +694,9 @@ struct FastStateT {
                      // overlaps the pop's plane reads instead of opening the next step)
     float closest;   // (t_min is kFastTMin)
     int hitEntry;    // -1: no hit yet
+    // the last rejected one-sphere leaf: its sphere and tmin (kid_table.h; ~0u = none)
+    uint32_t kc_id;
+    float kc_e;
     Masks masks;
     ORT_FN bool hit() const { return hitEntry >= 0; }
     ORT_FN float pl(const float* p, int s, int idx) const {
@@ -716,11 +734,13 @@ struct Masks96Lean : Masks96 {
 #define ORT_LEAD_LEAVES_PERSISTENT 0
 #endif
     static constexpr bool kLeadLeaves = ORT_LEAD_LEAVES_PERSISTENT;
+    static constexpr bool kKidSkip = true;
 };
 // Depth <= 8 walk without the inline leaf children: the persistent bounce kernel's walk
 // (inline leaves pay off on coherent camera rays, not on scattered bounce rays).
 struct Masks64Plain : Masks64 {
     static constexpr bool kInlineLeaves = false;
+    static constexpr bool kKidSkip = true;
 };
 
 // Root test and state setup (glsl:296-311).  Returns false when the root box is missed.
@@ -784,6 +804,8 @@ ORT_FN bool fast_begin(const KScene& S, const float* planes, const uint8_t* rank
     st.depth = 0;
     st.closest = t_max;
     st.hitEntry = -1;
+    st.kc_id = ~0u;
+    st.kc_e = 0.0f;
     st.masks.clear();
     return fmin3(st.tFA, st.tFB, st.tFC) >= fmax3(st.tNA, st.tNB, st.tNC);
 }
@@ -803,6 +825,11 @@ ORT_FN bool leaf_tests(const KScene& S, FastStateT<Masks>& st, int off, int n, f
             st.hitEntry = off + i;
             if (COUNT) cnt.v[3] += 1;
         }
+    }
+    if (!COUNT && Masks::kKidSkip) {  // a rejected one-sphere leaf: remember its sphere (kid_table.h)
+        const bool rej = n == 1 && !st.hit();
+        st.kc_id = rej ? (uint32_t)off - S.tail_base : st.kc_id;
+        st.kc_e = rej ? ntmin : st.kc_e;
     }
     return st.hit();
 }
@@ -924,7 +951,18 @@ ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks
         // exit - entry is never NaN and is +0 when equal: its sign bit is "drop".  The drop
         // bits are shifted in rank order (rank 0 ends at bit 7: the reversed layout) -- one
         // v_max3 + v_min3 + v_sub + v_alignbit per child, no compare/select.
-        const uint32_t keep = rcm & ~child_drops(tNA, tNB, tMA, tMB, tFA, tFB, nN, nF, cN, cF) & 0xffu;
+        // rejected-sphere skip (kid_table.h): one-sphere leaf children holding the sphere this
+        // lane last rejected, at a tmin <= this node's (<= theirs), cannot end the walk; not
+        // in the counting kernels, which count the reference walk's work
+        uint32_t skip = 0;
+        if (!COUNT && Masks::kKidSkip && S.kid) {
+            const uint2 kd = fetch_kid(S, st.node);
+            const uint32_t m = (((kd.x & 0xffffffu) == st.kc_id) ? (kd.x >> 24) : 0u) |
+                               (((kd.y & 0xffffffu) == st.kc_id) ? (kd.y >> 24) : 0u);
+            const float ptmin = fmax_tmin(fmax3(tNA, tNB, tNC));
+            skip = st.kc_e <= ptmin ? (uint32_t)rank_lut[((st.otab & 7u) << 8) | m] : 0u;
+        }
+        const uint32_t keep = rcm & ~skip & ~child_drops(tNA, tNB, tMA, tMB, tFA, tFB, nN, nF, cN, cF) & 0xffu;
         if (Masks::kInlineLeaves && (rec.y & ORT_LEAFKIDS_FLAG)) {
             // Every existing child is a leaf, so the reference pops the surviving ones next,
             // consecutively in rank order (a leaf pushes nothing): test them right here.
@@ -1305,9 +1343,11 @@ ORT_FN Ray primary_ray(const PixelParams& P, int px, int py, int s, ort_rng& st)
 // 1 explicit octree, 2 brute force.  With MODE 0 and allow_defer, a ray the fast walk
 // cannot take (some 1/d component not finite) is reported as DEFER instead of walking
 // it exactly here, so the exact walk's registers stay out of the hot kernel.
+// bounce: the ray of a bounce >= 1 -- walked like the GPU's bounce kernel does (Masks64Plain /
+// Masks96Lean: no inline leaf children, the rejected-sphere skip), same result.
 template <int MODE, bool COUNT, class Frames>
 ORT_FN int trace_ray(const KScene& S, const float* planes, const uint8_t* rank_lut, const Ray& r, bool allow_defer,
-                     float& t, int& entry, Frames& fr, int* snode, float* stmin, Counters& cnt) {
+                     float& t, int& entry, Frames& fr, int* snode, float* stmin, Counters& cnt, bool bounce = false) {
     bool hit;
     entry = -1;
     t = 0.0f;
@@ -1315,7 +1355,12 @@ ORT_FN int trace_ray(const KScene& S, const float* planes, const uint8_t* rank_l
         const V3 inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
         if (rank_lut && fast_path_ok(r, inv, 0.001f, ORT_MAXFLOAT)) {
             if (COUNT) cnt.v[5] += 1;
-            hit = traverse_fast<COUNT>(S, planes, rank_lut, r, inv, 0.001f, ORT_MAXFLOAT, entry, t, fr, cnt);
+            if (!bounce)
+                hit = traverse_fast<COUNT>(S, planes, rank_lut, r, inv, 0.001f, ORT_MAXFLOAT, entry, t, fr, cnt);
+            else if (S.depth <= 8)
+                hit = traverse_fast_t<COUNT, Masks64Plain>(S, planes, rank_lut, r, inv, 0.001f, ORT_MAXFLOAT, entry, t, fr, cnt);
+            else
+                hit = traverse_fast_t<COUNT, Masks96Lean>(S, planes, rank_lut, r, inv, 0.001f, ORT_MAXFLOAT, entry, t, fr, cnt);
         } else if (allow_defer) {
             return ORT_TRACE_DEFER;
         } else {
@@ -1407,7 +1452,7 @@ ORT_FN V3 shade_pixel(const PixelParams& P, const KScene& S, const float* planes
             if (importance < 0.01f) break;
             float t;
             int entry;
-            const int tr = trace_ray<MODE, COUNT>(S, planes, rank_lut, ray, false, t, entry, fr, snode, stmin, cnt);
+            const int tr = trace_ray<MODE, COUNT>(S, planes, rank_lut, ray, false, t, entry, fr, snode, stmin, cnt, b > 0);
             HitRec h;
             if (tr == ORT_TRACE_HIT) h = hit_record<MODE>(S, ray, t, entry);
             const bool hit = tr == ORT_TRACE_HIT;

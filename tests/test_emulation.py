@@ -31,7 +31,8 @@ def test_bounces_and_samples(ort, oracle, scene_c1):
     assert same_bits(img, ref) and c == rc
 
 
-@pytest.mark.parametrize("n,d,m,seed", [(1, 4, 0, 1), (3, 0, 0, 2), (200, 7, 0, 3), (1000, 5, 1, 4), (300, 10, 0, 5)])
+@pytest.mark.parametrize("n,d,m,seed", [(1, 4, 0, 1), (3, 0, 0, 2), (200, 7, 0, 3), (1000, 5, 1, 4), (300, 10, 0, 5),
+                                        (4000, 10, 1, 6), (4000, 8, 1, 7)])
 def test_scene_shapes(ort, oracle, n, d, m, seed):
     s = ort.random_spheres(n, seed)
     t = ort.build_octree(s, d, m)
@@ -39,6 +40,20 @@ def test_scene_shapes(ort, oracle, n, d, m, seed):
     ref = oracle.render(s, t, p)
     img, _ = emulate_render_host(s, t, p)
     assert same_bits(img, ref)
+
+
+@pytest.mark.parametrize("d", [8, 10])
+def test_rejected_sphere_skip_bounces(ort, oracle, d):
+    """Bounce rays walk like the GPU bounce kernel (Masks64Plain / Masks96Lean) with the
+    rejected-sphere skip (kid_table.h): on maxSpheresPerNode-1 trees, where a sphere sits in
+    many leaves, every skip must leave the pixels bit-identical and the counted reference
+    work unchanged (the counting walk never skips)."""
+    s = ort.random_spheres(6000, 11)
+    t = ort.build_octree(s, d, 1)
+    p = ort.FrameParams.default_camera(80, 48, num_samples=2, max_depth=5)
+    ref, rc = oracle.render(s, t, p, counts=True)
+    img, c = emulate_render_host(s, t, p)
+    assert same_bits(img, ref) and c == rc
 
 
 def test_debug_and_prebuilt_scenes(ort, oracle):

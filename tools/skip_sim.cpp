@@ -184,4 +184,100 @@ void skip_sim_run(const float* nmin, const float* nmax, const int32_t* co, const
         if (res[0] != res[1] || rhit[0] != rhit[1]) stats[10] += 1;  // must never happen
     }
 }
+// Push-time variant: an internal node does not push a leaf child that holds exactly one
+// sphere s when the lane's rejection cache (the last `cache` rejected spheres, LRU) has s with
+// e <= the child's pushed tmin -- the child is never popped.  A parent can name at most
+// `kids_k` distinct such spheres (the record's budget); others are pushed as usual.
+// stats: [0] rays, [1] pops (reference), [2] pops with push skips, [3] leaf children skipped,
+// [4] sphere tests with skips, [5] rays whose result differs (must be 0)
+// per_ray (2 per ray): pops reference, pops with skips
+static int kids_k_parent = 0;
+void skip_sim_push_parent(int v) { kids_k_parent = v; }
+void skip_sim_push(const float* nmin, const float* nmax, const int32_t* co, const int32_t* oo, const int32_t* cnt,
+                   const int32_t* idx, int32_t n, const float* sph, int cache, int kids_k, const float* rays,
+                   int64_t nrays, int64_t* stats, int32_t* per_ray) {
+    std::vector<int32_t> stk(512);
+    std::vector<float> stt(512);
+    for (int64_t r = 0; r < nrays; ++r) {
+        const V3 o = {rays[6 * r], rays[6 * r + 1], rays[6 * r + 2]};
+        const V3 d = {rays[6 * r + 3], rays[6 * r + 4], rays[6 * r + 5]};
+        const V3 inv = {1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+        stats[0] += 1;
+        float t0, t1;
+        if (!ray_box(o, inv, nmin, nmax, t0, t1)) continue;
+        int ord[8];
+        order_for(d, ord);
+        float res[2] = {0, 0};
+        bool rhit[2] = {false, false};
+        for (int pass = 0; pass < 2; ++pass) {
+            const bool skip = pass == 1;
+            int32_t cid[8];
+            float ce[8];
+            int cn = 0;
+            auto cache_find = [&](int32_t s) { for (int j = 0; j < cn; ++j) if (cid[j] == s) return j; return -1; };
+            auto cache_put = [&](int32_t s, float e) {
+                int j = cache_find(s);
+                if (j >= 0) { for (int q = j; q + 1 < cn; ++q) { cid[q] = cid[q + 1]; ce[q] = ce[q + 1]; } --cn; }
+                if (cn == cache) { for (int q = 0; q + 1 < cn; ++q) { cid[q] = cid[q + 1]; ce[q] = ce[q + 1]; } --cn; }
+                if (cache > 0) { cid[cn] = s; ce[cn] = e; ++cn; }
+            };
+            int sp = 0;
+            stk[0] = 0;
+            stt[0] = 0.001f;
+            float closest = 3.402823466e+38f;
+            bool hit = false;
+            int64_t pops = 0, kskip = 0, tests = 0;
+            while (sp >= 0) {
+                const int32_t ni = stk[sp];
+                const float ntmin = stt[sp];
+                --sp;
+                ++pops;
+                if (co[ni] == -1) {
+                    for (int j = 0; j < cnt[ni]; ++j) {
+                        const int32_t s = idx[oo[ni] + j];
+                        ++tests;
+                        float t;
+                        if (sphere_hit(o, d, sph + 4 * s, ntmin, closest, t)) { closest = t; hit = true; sp = -1; }
+                        else if (skip) cache_put(s, ntmin);
+                    }
+                } else {
+                    // distinct one-sphere-leaf spheres among the children (the parent's budget)
+                    int32_t ks[8];
+                    int kn = 0;
+                    for (int i = 0; i < 8; ++i) {
+                        const int64_t c = (int64_t)co[ni] + i;
+                        if (c >= n || co[c] != -1 || cnt[c] != 1) continue;
+                        const int32_t s = idx[oo[c]];
+                        bool seen = false;
+                        for (int q = 0; q < kn; ++q) seen = seen || ks[q] == s;
+                        if (!seen) ks[kn++] = s;
+                    }
+                    for (int i = 7; i >= 0; --i) {
+                        const int64_t c = (int64_t)co[ni] + ord[i];
+                        if (c >= n) continue;
+                        float cmin, cmax;
+                        if (!ray_box(o, inv, nmin + 3 * c, nmax + 3 * c, cmin, cmax) || cmax < ntmin || cmin > closest ||
+                            (co[c] == -1 && oo[c] == -1))
+                            continue;
+                        const float ct = fmaxr(cmin, ntmin);
+                        if (skip && co[c] == -1 && cnt[c] == 1) {
+                            const int32_t s = idx[oo[c]];
+                            int pos = -1;
+                            for (int q = 0; q < kn; ++q) if (ks[q] == s) pos = q;
+                            const int qc = cache_find(s);
+                            if (pos >= 0 && pos < kids_k && qc >= 0 && ce[qc] <= (kids_k_parent ? ntmin : ct)) { ++kskip; continue; }
+                        }
+                        if (sp < 510) { ++sp; stk[sp] = (int32_t)c; stt[sp] = ct; }
+                    }
+                }
+            }
+            res[pass] = closest;
+            rhit[pass] = hit;
+            if (per_ray) per_ray[2 * r + pass] = (int32_t)pops;
+            if (!skip) stats[1] += pops;
+            else { stats[2] += pops; stats[3] += kskip; stats[4] += tests; }
+        }
+        if (res[0] != res[1] || rhit[0] != rhit[1]) stats[5] += 1;
+    }
+}
 }
