@@ -905,7 +905,7 @@ struct ort_ctx {
     std::string err;
     int force_layout = -1;
     int exact_only = 0;
-    int refill = 8;  // ORT_OPT_REFILL: C5 +1.4 % vs 16 (4: -1 %, 32: -2.6 %; tools/ab_stream.py)
+    int refill = 12;  // ORT_OPT_REFILL: C5 12 ~ 16 > 8 (-1.5 %) > 24 (-1.7 %) > 32 (-4.4 %) with the rejected-sphere skip (tools/ab_stream.py)
     int persistent = 2;  // ORT_OPT_PERSISTENT: 0 off, 1 every trace, 2 bounce >= 1 traces (default)
     void* wclock = nullptr;  // ort_debug_wave_clock
     long long wclock_n = 0;
