@@ -83,7 +83,7 @@ typedef struct ort_scene_info {
 /* Options (ort_set_option). */
 #define ORT_OPT_FORCE_LAYOUT 1     /* -1 auto (default), or ORT_LAYOUT_* */
 #define ORT_OPT_EXACT_TRAVERSAL 2  /* 1: disable the sign-specialised fast walk (A/B testing; same pixels) */
-#define ORT_OPT_REFILL 3           /* persistent trace: refill a wave when >= value of its 64 lanes idle (12) */
+#define ORT_OPT_REFILL 3           /* persistent trace: refill a wave when >= value of its 64 lanes idle (16) */
 #define ORT_OPT_PERSISTENT 4       /* persistent trace kernel with per-lane ray refill: 0 off, 1 every
                                       trace, 2 (default) bounce >= 1 traces only: their incoherent
                                       rays gain from refilling idle lanes (C5 -4.5 %) */

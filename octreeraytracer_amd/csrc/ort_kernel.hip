@@ -247,7 +247,14 @@ __global__ void __launch_bounds__(kBlock) ort_raygen_kernel(PipeArgs A) {
 #ifndef ORT_TRACE_WAVES_DEEP  // 96-bit masks, no inline leaf children: 64 VGPRs, spill-free
 #define ORT_TRACE_WAVES_DEEP 8
 #endif
-constexpr int kChunk = 256;
+// Items a wave takes from the global cursor at a time.  The resident waves then work on a
+// window of about (waves x kChunk) consecutive list items -- neighbouring paths, overlapping
+// node sets, one L2 working set: C5 frame 58.2 (256) -> 56.7 (128) -> 55.8 ms (64; 32: 56.0)
+// in A/B.  (One queue per XCD over 8 contiguous list ranges measured no better: -0.4 %.)
+#ifndef ORT_CHUNK
+#define ORT_CHUNK 64
+#endif
+constexpr int kChunk = ORT_CHUNK;
 
 // DEEP: trees deeper than 8 levels (96-bit masks, lean state); depth <= 8 takes the
 // primary-ray walk's 64-bit masks and reversed plane tables (71 VGPRs, 7 waves/SIMD).
@@ -738,8 +745,9 @@ __global__ void __launch_bounds__(kBlock) ort_trace_kernel(PipeArgs A) {
 template <bool COUNT, bool PRIMARY, bool FUSE>
 __global__ void __launch_bounds__(kBlock) ort_trace_exact(PipeArgs A) {
     extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];  // plane tables: 1 KiB-aligned
-    LdsView L = setup_lds<false>(smem, A.S);
     const int n = *A.sync;
+    if ((int)(blockIdx.x * kBlock) >= n) return;  // usually no deferred ray at all: skip the LDS image copy
+    LdsView L = setup_lds<false>(smem, A.S);
     ort::Counters cnt;
     for (int q = 0; q < 6; ++q) cnt.v[q] = 0;
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
@@ -905,7 +913,7 @@ struct ort_ctx {
     std::string err;
     int force_layout = -1;
     int exact_only = 0;
-    int refill = 12;  // ORT_OPT_REFILL: C5 12 ~ 16 > 8 (-1.5 %) > 24 (-1.7 %) > 32 (-4.4 %) with the rejected-sphere skip (tools/ab_stream.py)
+    int refill = 16;  // ORT_OPT_REFILL: C5 (64-item chunks) 16 > 12 (-0.6 %) > 8 (-1.2 %); tools/ab_stream.py
     int persistent = 2;  // ORT_OPT_PERSISTENT: 0 off, 1 every trace, 2 bounce >= 1 traces (default)
     void* wclock = nullptr;  // ort_debug_wave_clock
     long long wclock_n = 0;

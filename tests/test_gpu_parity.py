@@ -181,7 +181,7 @@ def test_kernel_variants_identical(ort, oracle, renderer, scene_c2, persistent, 
     finally:
         renderer.set_persistent(2)  # the default
         renderer.set_exact_traversal(False)
-        renderer.set_refill(12)  # the default
+        renderer.set_refill(16)  # the default
         renderer.set_packet(False)
         renderer.set_wave_queue(False)
 
