@@ -88,9 +88,11 @@ typedef struct ort_scene_info {
                                       trace, 2 (default) bounce >= 1 traces only: their incoherent
                                       rays gain from refilling idle lanes (C5 -4.5 %) */
 #define ORT_OPT_PACKET 5           /* 1: wave-level walk for camera rays; 0 (default): per-lane walk (same pixels) */
-#define ORT_OPT_SORT_PATHS 6       /* 1: sort the alive paths by direction octant + origin cell between
-                                      bounces (coherence; same pixels); 0 (default): keep them in slot
-                                      order (the sort costs more than it saves: C5 -3 %) */
+#define ORT_OPT_SORT_PATHS 6       /* order of the alive paths between bounces (coherence; same pixels):
+                                      2 (default) radix-sort the compacted list by direction octant +
+                                      origin cell + direction (reads the list's length back: the host
+                                      waits once per bounce); 1 sort every slot's key (no host wait);
+                                      0 slot order */
 #define ORT_OPT_WAVE_QUEUE 7       /* 1: resident workgroups whose waves take 64-slot blocks from a queue;
                                       0 (default): one workgroup per 16x16 tile (same pixels) */
 #define ORT_OPT_XCD_SWIZZLE 8      /* workgroup -> tile order (same pixels): 2 (default) each XCD renders

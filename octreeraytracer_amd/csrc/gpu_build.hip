@@ -691,6 +691,40 @@ __device__ __forceinline__ uint32_t quantb(float x, float lo, float scale, int b
     const float top = (float)((1u << bits) - 1u);
     return q <= 0.0f ? 0u : (q >= top ? (uint32_t)top : (uint32_t)q);  // NaN -> 0
 }
+// The coherence key of one alive path (< 2^30): direction octant | origin code | direction.
+__device__ __forceinline__ uint32_t path_key(const float4 o, const float4 d, const float3 lo, const float3 sc,
+                                             const MortonPlan& mp) {
+    const uint32_t m = ((uint32_t)(d.z < 0.0f) << 2) | ((uint32_t)(d.x < 0.0f) << 1) | (uint32_t)(d.y < 0.0f);
+#if ORT_SORT_KEY >= 2
+    // direction (2 bits per axis of |d|/max|d|)
+    const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
+    const float inv = 3.999f / fmaxf(fmaxf(ax, ay), fmaxf(az, 1e-30f));
+    const uint32_t dq = ((uint32_t)(ax * inv) << 4) | ((uint32_t)(ay * inv) << 2) | (uint32_t)(az * inv);
+#endif
+#if ORT_SORT_KEY == 3
+    // octant | anisotropic origin code (21 bits) | direction
+    uint32_t q[3] = {quantb(o.x, mp.lo[0], mp.scale[0], mp.bits[0]), quantb(o.y, mp.lo[1], mp.scale[1], mp.bits[1]),
+                     quantb(o.z, mp.lo[2], mp.scale[2], mp.bits[2])};
+    int rem[3] = {mp.bits[0], mp.bits[1], mp.bits[2]};
+    uint32_t code = 0;
+#pragma unroll
+    for (int i = 0; i < kMortonBits; ++i) {
+        const int a = (int)(((i < 16 ? mp.axis_lo >> (2 * i) : mp.axis_hi >> (2 * (i - 16)))) & 3u);
+        const int r = a == 0 ? --rem[0] : (a == 1 ? --rem[1] : --rem[2]);
+        const uint32_t qa = a == 0 ? q[0] : (a == 1 ? q[1] : q[2]);
+        code = (code << 1) | ((qa >> r) & 1u);
+    }
+    return (m << 27) | (code << 6) | dq;
+#elif ORT_SORT_KEY == 2
+    // octant | origin Morton (7 bits per axis) | direction
+    return (m << 27) | ((spread3(quant9(o.x, lo.x, sc.x) >> 2) << 2 | spread3(quant9(o.y, lo.y, sc.y) >> 2) << 1 |
+                        spread3(quant9(o.z, lo.z, sc.z) >> 2)) << 6) | dq;
+#else
+    return (m << 27) | (spread3(quant9(o.x, lo.x, sc.x)) << 2) | (spread3(quant9(o.y, lo.y, sc.y)) << 1) |
+           spread3(quant9(o.z, lo.z, sc.z));
+#endif
+}
+
 // Grid-stride, one atomic per block: an atomic per wave on the one counter serialised
 // (~0.5 M atomics at C5 took 3.8 ms per bounce).
 __global__ void k_path_keys(const float4* po, const float4* pd, int n, float3 lo, float3 sc, MortonPlan mp,
@@ -701,38 +735,7 @@ __global__ void k_path_keys(const float4* po, const float4* pd, int n, float3 lo
         const float4 d = pd[k];
         const bool alive = d.w != 0.0f;
         uint32_t key = 0xffffffffu;
-        if (alive) {
-            const float4 o = po[k];
-            const uint32_t m = ((uint32_t)(d.z < 0.0f) << 2) | ((uint32_t)(d.x < 0.0f) << 1) | (uint32_t)(d.y < 0.0f);
-#if ORT_SORT_KEY >= 2
-            // direction (2 bits per axis of |d|/max|d|)
-            const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
-            const float inv = 3.999f / fmaxf(fmaxf(ax, ay), fmaxf(az, 1e-30f));
-            const uint32_t dq = ((uint32_t)(ax * inv) << 4) | ((uint32_t)(ay * inv) << 2) | (uint32_t)(az * inv);
-#endif
-#if ORT_SORT_KEY == 3
-            // octant | anisotropic origin code (21 bits) | direction
-            uint32_t q[3] = {quantb(o.x, mp.lo[0], mp.scale[0], mp.bits[0]), quantb(o.y, mp.lo[1], mp.scale[1], mp.bits[1]),
-                             quantb(o.z, mp.lo[2], mp.scale[2], mp.bits[2])};
-            int rem[3] = {mp.bits[0], mp.bits[1], mp.bits[2]};
-            uint32_t code = 0;
-#pragma unroll
-            for (int i = 0; i < kMortonBits; ++i) {
-                const int a = (int)(((i < 16 ? mp.axis_lo >> (2 * i) : mp.axis_hi >> (2 * (i - 16)))) & 3u);
-                const int r = a == 0 ? --rem[0] : (a == 1 ? --rem[1] : --rem[2]);
-                const uint32_t qa = a == 0 ? q[0] : (a == 1 ? q[1] : q[2]);
-                code = (code << 1) | ((qa >> r) & 1u);
-            }
-            key = (m << 27) | (code << 6) | dq;
-#elif ORT_SORT_KEY == 2
-            // octant | origin Morton (7 bits per axis) | direction
-            key = (m << 27) | ((spread3(quant9(o.x, lo.x, sc.x) >> 2) << 2 | spread3(quant9(o.y, lo.y, sc.y) >> 2) << 1 |
-                               spread3(quant9(o.z, lo.z, sc.z) >> 2)) << 6) | dq;
-#else
-            key = (m << 27) | (spread3(quant9(o.x, lo.x, sc.x)) << 2) | (spread3(quant9(o.y, lo.y, sc.y)) << 1) |
-                  spread3(quant9(o.z, lo.z, sc.z));
-#endif
-        }
+        if (alive) key = path_key(po[k], d, lo, sc, mp);
         keys[k] = key;
         vals[k] = k;
         alive_n += alive ? 1 : 0;
@@ -748,7 +751,68 @@ __global__ void k_path_keys(const float4* po, const float4* pd, int n, float3 lo
         if (t) atomicAdd(count, t);
     }
 }
+
+// Keys of the alive list (sort_paths 2): key i = the coherence key of path list[i], >> drop.
+__global__ void k_list_keys(const float4* po, const float4* pd, const int* list, int n, float3 lo, float3 sc,
+                            MortonPlan mp, int drop, uint32_t* keys, int* vals) {
+    for (int i = blockIdx.x * kB + threadIdx.x; i < n; i += gridDim.x * kB) {
+        const int k = list[i];
+        keys[i] = path_key(po[k], pd[k], lo, sc, mp) >> drop;
+        vals[i] = k;
+    }
+}
+
+void plan_for(const float* root_lo, const float* root_hi, float3& lo, float3& sc, MortonPlan& mp) {
+    float l[3], c[3];
+    for (int a = 0; a < 3; ++a) {
+        const float ext = root_hi[a] - root_lo[a];
+        l[a] = root_lo[a];
+        c[a] = (ext > 0.0f && ext < 3.0e38f) ? 512.0f / ext : 0.0f;
+    }
+    lo = make_float3(l[0], l[1], l[2]);
+    sc = make_float3(c[0], c[1], c[2]);
+    mp = MortonPlan{};
+    // deal kMortonBits splits to the longest current cell
+    float cell[3];
+    for (int a = 0; a < 3; ++a) {
+        const float ext = root_hi[a] - root_lo[a];
+        cell[a] = (ext > 0.0f && ext < 3.0e38f) ? ext : 0.0f;
+        mp.lo[a] = root_lo[a];
+    }
+    for (int i = 0; i < kMortonBits; ++i) {
+        int a = 0;
+        for (int j = 1; j < 3; ++j)
+            if (cell[j] > cell[a]) a = j;
+        cell[a] *= 0.5f;
+        mp.bits[a] += 1;
+        if (i < 16) mp.axis_lo |= (uint32_t)a << (2 * i);
+        else mp.axis_hi |= (uint32_t)a << (2 * (i - 16));
+    }
+    for (int a = 0; a < 3; ++a) {
+        const float ext = root_hi[a] - root_lo[a];
+        mp.scale[a] = (ext > 0.0f && ext < 3.0e38f) ? (float)(1u << mp.bits[a]) / ext : 0.0f;
+    }
+}
 }  // namespace
+
+#ifndef ORT_LIST_SORT_BITS
+#define ORT_LIST_SORT_BITS 30  // key bits sorted by sortList (the lowest 30 - bits are dropped)
+#endif
+
+hipError_t sortList(void* temp, size_t temp_bytes, const float4* po, const float4* pd, const float* root_lo,
+                    const float* root_hi, const int* list, int n, const SortBuffers& b, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    float3 lo, sc;
+    MortonPlan mp;
+    plan_for(root_lo, root_hi, lo, sc, mp);
+    const int grid = std::max(1, std::min((n + kB - 1) / kB, 2048));
+    hipLaunchKernelGGL(k_list_keys, dim3(grid), dim3(kB), 0, s, po, pd, list, n, lo, sc, mp, 30 - ORT_LIST_SORT_BITS,
+                       b.keys_in, b.vals_in);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return rocprim::radix_sort_pairs(temp, temp_bytes, b.keys_in, b.keys_out, b.vals_in, b.vals_out, (size_t)n, 0,
+                                     ORT_LIST_SORT_BITS, s);
+}
 
 size_t sortAliveTempBytes(int n) {
     size_t tb = 0;
@@ -762,36 +826,8 @@ hipError_t sortAlive(void* temp, size_t temp_bytes, const float4* po, const floa
     hipError_t e = hipMemsetAsync(count, 0, sizeof(int), s);
     if (e != hipSuccess) return e;
     float3 lo, sc;
-    float l[3], c[3];
-    for (int a = 0; a < 3; ++a) {
-        const float ext = root_hi[a] - root_lo[a];
-        l[a] = root_lo[a];
-        c[a] = (ext > 0.0f && ext < 3.0e38f) ? 512.0f / ext : 0.0f;
-    }
-    lo = make_float3(l[0], l[1], l[2]);
-    sc = make_float3(c[0], c[1], c[2]);
-    MortonPlan mp{};
-    {   // deal kMortonBits splits to the longest current cell
-        float cell[3];
-        for (int a = 0; a < 3; ++a) {
-            const float ext = root_hi[a] - root_lo[a];
-            cell[a] = (ext > 0.0f && ext < 3.0e38f) ? ext : 0.0f;
-            mp.lo[a] = root_lo[a];
-        }
-        for (int i = 0; i < kMortonBits; ++i) {
-            int a = 0;
-            for (int j = 1; j < 3; ++j)
-                if (cell[j] > cell[a]) a = j;
-            cell[a] *= 0.5f;
-            mp.bits[a] += 1;
-            if (i < 16) mp.axis_lo |= (uint32_t)a << (2 * i);
-            else mp.axis_hi |= (uint32_t)a << (2 * (i - 16));
-        }
-        for (int a = 0; a < 3; ++a) {
-            const float ext = root_hi[a] - root_lo[a];
-            mp.scale[a] = (ext > 0.0f && ext < 3.0e38f) ? (float)(1u << mp.bits[a]) / ext : 0.0f;
-        }
-    }
+    MortonPlan mp;
+    plan_for(root_lo, root_hi, lo, sc, mp);
     hipLaunchKernelGGL(k_path_keys, dim3(std::min((n + kB - 1) / kB, 2048)), dim3(kB), 0, s, po, pd, n, lo, sc, mp,
                        b.keys_in, b.vals_in, count);
     if ((e = hipGetLastError()) != hipSuccess) return e;

@@ -921,10 +921,13 @@ struct ort_ctx {
     int kid_skip = 1;     // ORT_OPT_KID_SKIP: rejected-sphere skip of one-sphere leaf children
     int wave_queue = 0;  // ORT_OPT_WAVE_QUEUE: per-lane walk from a wave-level block queue (opt-in)
     int packet = 0;     // ORT_OPT_PACKET: wave-level walk for camera rays (SALU-bound so far: off)
-    // ORT_OPT_SORT_PATHS: coherence-sort the alive paths between bounces.  Off by default: with the
-    // shade kernels in slot order the bounce traces gain ~0.7 ms per C5 frame from the sort but
-    // the keys + radix sort of every slot cost ~3 ms (frame 62.6 sorted vs 60.7 ms, A/B)
-    int sort_paths = 0;
+    // ORT_OPT_SORT_PATHS: order of the alive paths between bounces.  2 (default): the list the
+    // shade kernel appended, radix-sorted by the coherence key after reading its length back --
+    // C5 bounce traces 33.8 -> 31.2 ms, frame 55.5 -> 54.9 ms (A/B).  1 (every slot's key sorted,
+    // dead ones last) costs as much as it saves; coarser orders lose: octant only or 12-18 key
+    // bits ~ slot order, octant + direction bits and 16-bit atomic buckets slower than slot
+    // order, a block-local sort of 4096-entry runs (rocprim block_radix_sort) 55.4 ms.
+    int sort_paths = 2;
     float root_lo[3] = {0, 0, 0}, root_hi[3] = {0, 0, 0};  // root box (coherence-sort key)
     DevBuf lut;         // rank LUT (global copy, for the packet kernel)
     ort::GpuTree tree;  // reference-layout tree of the last ort_build_scene(keep_tree)
@@ -943,7 +946,7 @@ struct ort_ctx {
     // wavefront pipeline state, sized for the largest tile rendered so far
     DevBuf hit, defer_list, defer_count, po, pd, pc, prng, pcol;
     DevBuf qlist, qcount, qtemp;  // bounce >= 1 path compaction
-    DevBuf skeys, skeys2, svals;  // coherence sort
+    DevBuf skeys, skeys2, svals, shist;  // coherence sort (shist: the list sort's value input)
 };
 
 namespace {
@@ -1351,15 +1354,19 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     const bool compact = !direct && !pers_all && p->max_depth > 1;
     // primary-ray mode (1 sample, 1 bounce) on the compact layout: the trace kernels shade
     const bool fuse = direct && mode == 0 && !pers_all && !ctx->packet;
-    const bool sorted = compact && ctx->sort_paths;
+    const bool sorted = compact && ctx->sort_paths == 1;   // radix sort of every slot's key
+    const bool listsort = compact && ctx->sort_paths == 2; // sort of the appended list (its length read back)
     size_t qtemp_bytes = 0;
     if (compact) {
-        qtemp_bytes = sorted ? ort::sortAliveTempBytes((int)slots) : 0;
+        qtemp_bytes = (sorted || listsort) ? ort::sortAliveTempBytes((int)slots) : 0;
         if ((rc = ensure(ctx, ctx->qlist, 4 * slots)) || (rc = ensure(ctx, ctx->qcount, 64)) ||
             (rc = ensure(ctx, ctx->qtemp, std::max<size_t>(qtemp_bytes, 16))))
             return rc;
         if (sorted && ((rc = ensure(ctx, ctx->skeys, 4 * slots)) || (rc = ensure(ctx, ctx->skeys2, 4 * slots)) ||
                        (rc = ensure(ctx, ctx->svals, 4 * slots))))
+            return rc;
+        if (listsort && ((rc = ensure(ctx, ctx->skeys, 4 * slots)) || (rc = ensure(ctx, ctx->skeys2, 4 * slots)) ||
+                         (rc = ensure(ctx, ctx->shist, 4 * slots)) || (rc = ensure(ctx, ctx->svals, 4 * slots))))
             return rc;
     }
     PipeArgs a;
@@ -1467,7 +1474,19 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                                        (int)slots, ctx->root_lo, ctx->root_hi, sb, (int*)ctx->qcount.p, s);
                     if (e != hipSuccess) return hip_fail(ctx, e, "path compaction");
                 }  // else the shade kernel appended them
-                a.qlist = (const int*)ctx->qlist.p;
+                if (listsort) {
+                    // the list's length, read back (one host wait per bounce): the sort then
+                    // costs the alive paths only, not every slot (C5: 36.6 M keys, not 99.6 M)
+                    int n_alive = 0;
+                    HIPCHK(ctx, hipMemcpyAsync(&n_alive, ctx->qcount.p, sizeof(int), hipMemcpyDeviceToHost, s));
+                    HIPCHK(ctx, hipStreamSynchronize(s));
+                    const ort::SortBuffers sb{(uint32_t*)ctx->skeys.p, (uint32_t*)ctx->skeys2.p, (int*)ctx->shist.p,
+                                              (int*)ctx->svals.p};
+                    e = ort::sortList(ctx->qtemp.p, qtemp_bytes, (const float4*)ctx->po.p, (const float4*)ctx->pd.p,
+                                      ctx->root_lo, ctx->root_hi, (const int*)ctx->qlist.p, n_alive, sb, s);
+                    if (e != hipSuccess) return hip_fail(ctx, e, "path list sort");
+                }
+                a.qlist = (const int*)(listsort ? ctx->svals.p : ctx->qlist.p);
                 a.qcount = (const int*)ctx->qcount.p;
             }
         }
@@ -1542,7 +1561,7 @@ int ort_destroy(ort_ctx* ctx) {
     free_buf(ctx->counters);
     free_buf(ctx->lut);
     DevBuf* pipe[] = {&ctx->hit, &ctx->defer_list, &ctx->defer_count, &ctx->po, &ctx->pd, &ctx->pc, &ctx->prng, &ctx->pcol,
-                      &ctx->qlist, &ctx->qcount, &ctx->qtemp, &ctx->skeys, &ctx->skeys2, &ctx->svals};
+                      &ctx->qlist, &ctx->qcount, &ctx->qtemp, &ctx->skeys, &ctx->skeys2, &ctx->svals, &ctx->shist};
     for (DevBuf* b : pipe) free_buf(*b);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
@@ -1588,7 +1607,8 @@ int ort_set_option(ort_ctx* ctx, int option, int value) {
         return ORT_OK;
     }
     if (option == ORT_OPT_SORT_PATHS) {
-        ctx->sort_paths = value ? 1 : 0;
+        if (value < 0 || value > 2) return fail(ctx, ORT_ERR_INVALID_ARG, "sort_paths must be 0, 1 or 2");
+        ctx->sort_paths = value;
         return ORT_OK;
     }
     if (option == ORT_OPT_REFILL) {

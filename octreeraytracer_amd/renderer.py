@@ -127,9 +127,10 @@ class Renderer:
         XCD, 1 128x128-pixel super-tiles per XCD, 0 raster; same pixels."""
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_XCD_SWIZZLE, int(mode)))
 
-    def set_sort_paths(self, on: bool):
-        """Coherence-sort the alive paths between bounces (default on); same pixels."""
-        self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_SORT_PATHS, int(bool(on))))
+    def set_sort_paths(self, mode: int):
+        """Order of the alive paths between bounces (same pixels): 0 slot order, 1 radix sort of
+        every slot by coherence key, 2 bucket order of the alive list (key's top 16 bits)."""
+        self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_SORT_PATHS, int(mode)))
 
     def set_persistent(self, on):
         """Persistent trace kernel with lane refill: False/0 off, True/1 every trace, 2 bounce >= 1

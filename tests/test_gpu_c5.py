@@ -50,8 +50,9 @@ def test_c5_tree_is_the_reference_tree(c5):
 
 @pytest.mark.parametrize("name,tile", _tiles())
 def test_c5_bounce_depth_4_bit_exact(ort, oracle, c5, name, tile):
-    """The C5 workload (1 spp, 4 bounces: camera-ray deep kernel, path compaction in slot
-    order, persistent refill kernel for bounces >= 1) against the oracle on the same tree."""
+    """The C5 workload (1 spp, 4 bounces: camera-ray deep kernel, path compaction and
+    coherence sort of the list, persistent refill kernel with the rejected-sphere skip for
+    bounces >= 1) against the oracle on the same tree."""
     s, t, r, _ = c5
     p = ort.FrameParams.default_camera(C5["width"], C5["height"], num_samples=1, max_depth=C5["bounces"])
     tl = ort.Tile(*tile)

@@ -241,8 +241,8 @@ def test_bounce_compaction_after_larger_frames(ort, oracle, renderer, scene_c2):
 @pytest.mark.parametrize("depth,mspn", [(9, 0), (10, 1)])
 def test_deep_tree_kernel_bit_exact(ort, oracle, renderer, depth, mspn):
     """Depth 9-10 trees take ort_trace_compact_deep (96-bit level masks): primary frame and
-    multi-bounce tiles (path compaction in slot order and with the coherence sort) against the
-    oracle."""
+    multi-bounce tiles (path compaction in slot order, with the coherence sort of every slot and
+    of the compacted list) against the oracle."""
     s = ort.random_spheres(20_000, 7)
     t = ort.build_octree(s, depth, mspn)
     renderer.build_scene(s, depth, mspn)
@@ -251,7 +251,7 @@ def test_deep_tree_kernel_bit_exact(ort, oracle, renderer, depth, mspn):
     assert_same(renderer.render(p), oracle.render(s, t, p), f"deep d{depth} primary")
     pb = ort.FrameParams.default_camera(1280, 720, num_samples=2, max_depth=4)
     try:
-        for sort in (0, 1):
+        for sort in (0, 1, 2):
             renderer.set_sort_paths(sort)
             for tile in (ort.Tile(300, 160, 200, 96), ort.Tile(0, 1280, 5, 48, 8, 90)):
                 got = renderer.render(pb, tile)
@@ -259,7 +259,7 @@ def test_deep_tree_kernel_bit_exact(ort, oracle, renderer, depth, mspn):
                                     band_stride=tile.band_stride)
                 assert_same(got, ref, f"deep d{depth} bounces {tile} sort={sort}")
     finally:
-        renderer.set_sort_paths(0)  # the default
+        renderer.set_sort_paths(2)  # the default
 
 
 @pytest.mark.parametrize("mode", [0, 1, 2])
