@@ -390,23 +390,95 @@ __device__ inline void shade_direct_padding(const PipeArgs& A, int k) {
     o[2] = 0.0f;
 }
 
+// The shading proper of path slot k, given its ray and RNG state and the walk's result
+// (entry < 0: no hit); shared by ort_shade_kernel and the trace kernels that shade bounce 0
+// themselves.  Returns true when the path goes on to the next bounce.
+template <int MODE, bool FIRST, bool DIRECT>
+__device__ __forceinline__ bool shade_state(const PipeArgs& A, int k, size_t p, ort::Ray ray, ort_rng st, int entry,
+                                            float t) {
+    ort::V3 c = ort::mk(1.0f, 1.0f, 1.0f);
+    float importance = 1.0f;
+    if (!FIRST) {
+        const float4 cc = A.pc[k];
+        c = ort::mk(cc.x, cc.y, cc.z);
+        importance = A.po[k].w;
+    }
+    bool done = true;
+    if (!A.nobounce) {
+        ort::HitRec rec;
+        if (entry >= 0) rec = ort::hit_record<MODE>(A.S, ray, t, entry);
+        if (A.last && A.sample == A.pp.ns - 1)  // nothing reads the ray or RNG state after this bounce
+            done = ort::shade_bounce<true>(entry >= 0, rec, ray, c, importance, st);
+        else
+            done = ort::shade_bounce(entry >= 0, rec, ray, c, importance, st);
+        if (!done && (A.last || importance < 0.01f)) done = true;  // loop bound / glsl:605
+    }
+    if constexpr (DIRECT) {
+        const ort::V3 v = ort::finish_pixel(ort::add(ort::mk(0.0f, 0.0f, 0.0f), c), 1);
+        float* o = A.out + 3 * p;
+        o[0] = v.x; o[1] = v.y; o[2] = v.z;
+    } else {
+        if (done) {
+            ort::V3 acc = ort::mk(0.0f, 0.0f, 0.0f);
+            if (A.sample > 0) {
+                const float4 a = A.pcol[k];
+                acc = ort::mk(a.x, a.y, a.z);
+            }
+            acc = ort::add(acc, c);
+            A.pcol[k] = make_float4(acc.x, acc.y, acc.z, 0.0f);
+            A.pd[k] = make_float4(ray.d.x, ray.d.y, ray.d.z, 0.0f);
+        } else {
+            A.po[k] = make_float4(ray.o.x, ray.o.y, ray.o.z, importance);
+            A.pd[k] = make_float4(ray.d.x, ray.d.y, ray.d.z, 1.0f);
+            A.pc[k] = make_float4(c.x, c.y, c.z, 0.0f);
+        }
+        A.prng[k] = make_float2(st.x, st.y);
+    }
+    return !DIRECT && !done;
+}
+
+// Appends slot k (where go) to list / count: one atomic per workgroup, the workgroup's slots
+// kept in increasing order.  Every thread of the workgroup must call it.
+__device__ inline void append_slots(bool go, int k, int* list, int* count) {
+    __shared__ int wcnt[kBlock / 64];
+    __shared__ int wbase;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const unsigned long long m = __ballot(go);
+    if (lane == 0) wcnt[w] = __popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int t = 0;
+        for (int i = 0; i < kBlock / 64; ++i) t += wcnt[i];
+        wbase = t ? atomicAdd(count, t) : 0;
+    }
+    __syncthreads();
+    int off = wbase;
+    for (int i = 0; i < w; ++i) off += wcnt[i];
+    const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    if (go) list[off + __popcll(m & below)] = k;
+}
+
 // One ray per lane over the compact layout (default): the tile-block order of the path
 // slots keeps each wave on an 8x8 pixel block, whose rays walk nearly the same nodes.
 // DEEP: trees deeper than 8 levels need the 96-bit level masks (ort_trace_compact_deep).
 // One path slot k of the compact-layout trace (the per-lane walk); counts accumulate in cnt.
-template <bool COUNT, bool PRIMARY, bool DEEP, bool FUSE>
-__device__ __forceinline__ void trace_slot(PipeArgs& A, LdsView& L, int k, ort::Counters& cnt) {
+// FUSE: 0 the walk's hit record is stored (shaded by ort_shade_kernel); 1 (1 sample, 1 bounce)
+// the kernel shades its ray into the final pixel; 2 (bounce 0 of a multi-bounce frame) the
+// kernel shades its ray into the path state and returns whether the path goes on.
+template <bool COUNT, bool PRIMARY, bool DEEP, int FUSE>
+__device__ __forceinline__ bool trace_slot(PipeArgs& A, LdsView& L, int k, ort::Counters& cnt) {
     bool alive;
     ort_rng rng0;  // FUSE: the camera ray's RNG state, kept for the shading after the walk
     const ort::Ray ray = slot_ray<PRIMARY>(A, k, alive, FUSE ? &rng0 : nullptr);
     if (!alive) {
-        if (FUSE) shade_direct_padding(A, k);
-        return;
+        if (FUSE == 1) shade_direct_padding(A, k);
+        if (FUSE == 2) A.pd[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // never alive (ort_shade_kernel's hole)
+        return false;
     }
     const ort::V3 inv = ort::mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
     if (A.exact_only || !ort::fast_path_ok(ray, inv, 0.001f, ORT_MAXFLOAT)) {
         A.defer_list[atomicAdd(A.sync, 1)] = k;  // ort_trace_exact walks (and, FUSE, shades) it
-        return;
+        return false;
     }
     if (COUNT) cnt.v[5] += 1;
     float t = 0.0f;
@@ -430,13 +502,18 @@ __device__ __forceinline__ void trace_slot(PipeArgs& A, LdsView& L, int k, ort::
 #else
         const PipeArgs& A2 = A;
 #endif
-        shade_direct(A2, k2, walked, rng0, hit, entry, t);
+        if constexpr (FUSE == 1) {
+            shade_direct(A2, k2, walked, rng0, hit, entry, t);
+        } else {
+            return shade_state<0, true, false>(A2, k2, 0, walked, rng0, hit ? entry : -1, t);
+        }
     } else {
         A.hit[k] = make_int2(hit ? entry : -1, __float_as_int(t));
     }
+    return false;
 }
 
-template <bool COUNT, bool PRIMARY, bool DEEP, bool FUSE>
+template <bool COUNT, bool PRIMARY, bool DEEP, int FUSE>
 __device__ __forceinline__ void trace_compact_body(PipeArgs& A, unsigned char* smem) {
     if (!PRIMARY && A.qlist && (int)(blockIdx.x * kBlock) >= *A.qcount) return;  // whole block past the list
     LdsView L = setup_lds<true>(smem, A.S);
@@ -444,7 +521,14 @@ __device__ __forceinline__ void trace_compact_body(PipeArgs& A, unsigned char* s
     if (!PRIMARY && !list_slot(A, k)) return;
     ort::Counters cnt;
     for (int q = 0; q < 6; ++q) cnt.v[q] = 0;
-    trace_slot<COUNT, PRIMARY, DEEP, FUSE>(A, L, k, cnt);
+    const bool go = trace_slot<COUNT, PRIMARY, DEEP, FUSE>(A, L, k, cnt);
+    if constexpr (FUSE == 2) {  // the paths that go on join the next bounce's list
+#if defined(__HIP_DEVICE_COMPILE__)
+        typedef __attribute__((address_space(4))) const PipeArgs KernArgs;
+        KernArgs* kp = (KernArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+        append_slots(go, k, kp->qnext, kp->qnext_count);
+#endif
+    }
     flush_counts<COUNT>(cnt, A.counters);
 }
 
@@ -452,7 +536,7 @@ __device__ __forceinline__ void trace_compact_body(PipeArgs& A, unsigned char* s
 // block (an 8x8 pixel block, or 64 entries of a bounce list) with one atomic, as soon as
 // their previous block is done -- no workgroup-level wait and one LDS setup per resident
 // group.  Balances the tail when a GPU has few blocks (a 1/8 band tile of an 8-GPU frame).
-template <bool COUNT, bool PRIMARY, bool DEEP, bool FUSE>
+template <bool COUNT, bool PRIMARY, bool DEEP, int FUSE>
 __device__ __forceinline__ void trace_queue_body(PipeArgs& A, unsigned char* smem) {
     (void)setup_lds<true>(smem, A.S);
     const int lane = threadIdx.x & 63;
@@ -490,12 +574,12 @@ __device__ __forceinline__ void trace_queue_body(PipeArgs& A, unsigned char* sme
 }
 
 // FUSE: 1 sample, 1 bounce -- the kernel also shades (shade_direct), no hit records.
-template <bool COUNT, bool PRIMARY, bool FUSE>
+template <bool COUNT, bool PRIMARY, int FUSE>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ORT_TRACE_WAVES))) ort_trace_compact(PipeArgs A) {
     extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];  // plane tables: 1 KiB-aligned
     trace_compact_body<COUNT, PRIMARY, false, FUSE>(A, smem);
 }
-template <bool COUNT, bool PRIMARY, bool FUSE>
+template <bool COUNT, bool PRIMARY, int FUSE>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ORT_TRACE_WAVES_DEEP)))
 ort_trace_compact_deep(PipeArgs A) {
     extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];  // plane tables: 1 KiB-aligned
@@ -742,7 +826,7 @@ __global__ void __launch_bounds__(kBlock) ort_trace_kernel(PipeArgs A) {
 }
 
 // Exact compact walk (traverse_compact) for the deferred rays; grid-stride loop.
-template <bool COUNT, bool PRIMARY, bool FUSE>
+template <bool COUNT, bool PRIMARY, int FUSE>
 __global__ void __launch_bounds__(kBlock) ort_trace_exact(PipeArgs A) {
     extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];  // plane tables: 1 KiB-aligned
     const int n = *A.sync;
@@ -758,8 +842,14 @@ __global__ void __launch_bounds__(kBlock) ort_trace_exact(PipeArgs A) {
         float t;
         int entry;
         const int st = ort::trace_ray<0, COUNT>(A.S, L.planes, nullptr, ray, false, t, entry, L.fr, nullptr, nullptr, cnt);
-        if (FUSE) shade_direct(A, k, ray, rng, st == ORT_TRACE_HIT, entry, t);
-        else A.hit[k] = make_int2(st == ORT_TRACE_HIT ? entry : -1, __float_as_int(t));
+        if (FUSE == 1) {
+            shade_direct(A, k, ray, rng, st == ORT_TRACE_HIT, entry, t);
+        } else if (FUSE == 2) {  // bounce 0 shaded here; the rare deferred path joins the list alone
+            if (shade_state<0, true, false>(A, k, 0, ray, rng, st == ORT_TRACE_HIT ? entry : -1, t))
+                A.qnext[atomicAdd(A.qnext_count, 1)] = k;
+        } else {
+            A.hit[k] = make_int2(st == ORT_TRACE_HIT ? entry : -1, __float_as_int(t));
+        }
     }
     flush_counts<COUNT>(cnt, A.counters);
 }
@@ -801,68 +891,11 @@ __device__ __forceinline__ bool shade_slot(const PipeArgs& A, int k) {
         st.x = r2.x;
         st.y = r2.y;
     }
-    ort::V3 c = ort::mk(1.0f, 1.0f, 1.0f);
-    float importance = 1.0f;
-    if (!FIRST) {
-        const float4 cc = A.pc[k];
-        c = ort::mk(cc.x, cc.y, cc.z);
-        importance = A.po[k].w;
-    }
-    bool done = true;
-    if (!A.nobounce) {
-        const int2 h = A.hit[k];
-        ort::HitRec rec;
-        if (h.x >= 0) rec = ort::hit_record<MODE>(A.S, ray, __int_as_float(h.y), h.x);
-        if (A.last && A.sample == A.pp.ns - 1)  // nothing reads the ray or RNG state after this bounce
-            done = ort::shade_bounce<true>(h.x >= 0, rec, ray, c, importance, st);
-        else
-            done = ort::shade_bounce(h.x >= 0, rec, ray, c, importance, st);
-        if (!done && (A.last || importance < 0.01f)) done = true;  // loop bound / glsl:605
-    }
-    if constexpr (DIRECT) {
-        const ort::V3 v = ort::finish_pixel(ort::add(ort::mk(0.0f, 0.0f, 0.0f), c), 1);
-        float* o = A.out + 3 * p;
-        o[0] = v.x; o[1] = v.y; o[2] = v.z;
-    } else {
-        if (done) {
-            ort::V3 acc = ort::mk(0.0f, 0.0f, 0.0f);
-            if (A.sample > 0) {
-                const float4 a = A.pcol[k];
-                acc = ort::mk(a.x, a.y, a.z);
-            }
-            acc = ort::add(acc, c);
-            A.pcol[k] = make_float4(acc.x, acc.y, acc.z, 0.0f);
-            A.pd[k] = make_float4(ray.d.x, ray.d.y, ray.d.z, 0.0f);
-        } else {
-            A.po[k] = make_float4(ray.o.x, ray.o.y, ray.o.z, importance);
-            A.pd[k] = make_float4(ray.d.x, ray.d.y, ray.d.z, 1.0f);
-            A.pc[k] = make_float4(c.x, c.y, c.z, 0.0f);
-        }
-        A.prng[k] = make_float2(st.x, st.y);
-    }
-    return !DIRECT && !done;
+    int2 h = make_int2(-1, 0);
+    if (!A.nobounce) h = A.hit[k];
+    return shade_state<MODE, FIRST, DIRECT>(A, k, p, ray, st, h.x, __int_as_float(h.y));
 }
 
-// Appends slot k (where go) to list / count: one atomic per workgroup, the workgroup's slots
-// kept in increasing order.  Every thread of the workgroup must call it.
-__device__ inline void append_slots(bool go, int k, int* list, int* count) {
-    __shared__ int wcnt[kBlock / 64];
-    __shared__ int wbase;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const unsigned long long m = __ballot(go);
-    if (lane == 0) wcnt[w] = __popcll(m);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int t = 0;
-        for (int i = 0; i < kBlock / 64; ++i) t += wcnt[i];
-        wbase = t ? atomicAdd(count, t) : 0;
-    }
-    __syncthreads();
-    int off = wbase;
-    for (int i = 0; i < w; ++i) off += wcnt[i];
-    const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    if (go) list[off + __popcll(m & below)] = k;
-}
 
 // Shades every path slot of its workgroup (slot order); with A.qnext, the paths that go on
 // are appended to the next bounce's list (the compaction, without a separate select pass).
@@ -1233,7 +1266,7 @@ int ensure(ort_ctx* ctx, DevBuf& b, size_t bytes) {
 
 template <bool COUNT, bool PRIMARY>
 hipError_t launch_trace_p(int mode, const PipeArgs& a, int blocks, int pblocks, size_t lds, hipStream_t s, bool packet,
-                          bool fuse, int qblocks) {
+                          int fuse, int qblocks) {
     if (mode == 0 && pblocks > 0) {
         if (a.S.depth > 8) hipLaunchKernelGGL((ort_trace_persistent<COUNT, true>), dim3(pblocks), dim3(kBlock), lds, s, a);
         else hipLaunchKernelGGL((ort_trace_persistent<COUNT, false>), dim3(pblocks), dim3(kBlock), lds, s, a);
@@ -1241,10 +1274,10 @@ hipError_t launch_trace_p(int mode, const PipeArgs& a, int blocks, int pblocks, 
     else if (mode == 0 && qblocks > 0 && !(PRIMARY && packet)) {
         const dim3 g(qblocks), t(kBlock);
         if (a.S.depth > 8) {
-            if (fuse) hipLaunchKernelGGL((ort_trace_compact_deep_q<COUNT, PRIMARY, true>), g, t, lds, s, a);
+            if (fuse == 1) hipLaunchKernelGGL((ort_trace_compact_deep_q<COUNT, PRIMARY, true>), g, t, lds, s, a);
             else hipLaunchKernelGGL((ort_trace_compact_deep_q<COUNT, PRIMARY, false>), g, t, lds, s, a);
         } else {
-            if (fuse) hipLaunchKernelGGL((ort_trace_compact_q<COUNT, PRIMARY, true>), g, t, lds, s, a);
+            if (fuse == 1) hipLaunchKernelGGL((ort_trace_compact_q<COUNT, PRIMARY, true>), g, t, lds, s, a);
             else hipLaunchKernelGGL((ort_trace_compact_q<COUNT, PRIMARY, false>), g, t, lds, s, a);
         }
     }
@@ -1254,12 +1287,15 @@ hipError_t launch_trace_p(int mode, const PipeArgs& a, int blocks, int pblocks, 
     }
     else if (mode == 0 && a.S.depth > 8)
     {
-        if (fuse) hipLaunchKernelGGL((ort_trace_compact_deep<COUNT, PRIMARY, true>), dim3(blocks), dim3(kBlock), lds, s, a);
-        else hipLaunchKernelGGL((ort_trace_compact_deep<COUNT, PRIMARY, false>), dim3(blocks), dim3(kBlock), lds, s, a);
+        if (fuse == 1) hipLaunchKernelGGL((ort_trace_compact_deep<COUNT, PRIMARY, 1>), dim3(blocks), dim3(kBlock), lds, s, a);
+        else if (fuse == 2) hipLaunchKernelGGL((ort_trace_compact_deep<COUNT, PRIMARY, 2>), dim3(blocks), dim3(kBlock), lds, s, a);
+        else hipLaunchKernelGGL((ort_trace_compact_deep<COUNT, PRIMARY, 0>), dim3(blocks), dim3(kBlock), lds, s, a);
     }
-    else if (mode == 0 && fuse)
-        hipLaunchKernelGGL((ort_trace_compact<COUNT, PRIMARY, true>), dim3(blocks), dim3(kBlock), lds, s, a);
-    else if (mode == 0) hipLaunchKernelGGL((ort_trace_compact<COUNT, PRIMARY, false>), dim3(blocks), dim3(kBlock), lds, s, a);
+    else if (mode == 0 && fuse == 1)
+        hipLaunchKernelGGL((ort_trace_compact<COUNT, PRIMARY, 1>), dim3(blocks), dim3(kBlock), lds, s, a);
+    else if (mode == 0 && fuse == 2)
+        hipLaunchKernelGGL((ort_trace_compact<COUNT, PRIMARY, 2>), dim3(blocks), dim3(kBlock), lds, s, a);
+    else if (mode == 0) hipLaunchKernelGGL((ort_trace_compact<COUNT, PRIMARY, 0>), dim3(blocks), dim3(kBlock), lds, s, a);
     else if (mode == 1) hipLaunchKernelGGL((ort_trace_kernel<1, COUNT, PRIMARY>), dim3(blocks), dim3(kBlock), 0, s, a);
     else hipLaunchKernelGGL((ort_trace_kernel<2, COUNT, PRIMARY>), dim3(blocks), dim3(kBlock), 0, s, a);
     return hipGetLastError();
@@ -1267,9 +1303,9 @@ hipError_t launch_trace_p(int mode, const PipeArgs& a, int blocks, int pblocks, 
 
 template <bool COUNT>
 hipError_t launch_trace(int mode, bool primary, const PipeArgs& a, int blocks, int pblocks, size_t lds, hipStream_t s,
-                        bool packet, bool fuse, int qblocks) {
+                        bool packet, int fuse, int qblocks) {
     return primary ? launch_trace_p<COUNT, true>(mode, a, blocks, pblocks, lds, s, packet, fuse, qblocks)
-                   : launch_trace_p<COUNT, false>(mode, a, blocks, pblocks, lds, s, packet, false, qblocks);
+                   : launch_trace_p<COUNT, false>(mode, a, blocks, pblocks, lds, s, packet, 0, qblocks);
 }
 
 template <int MODE>
@@ -1356,6 +1392,9 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     const bool fuse = direct && mode == 0 && !pers_all && !ctx->packet;
     const bool sorted = compact && ctx->sort_paths == 1;   // radix sort of every slot's key
     const bool listsort = compact && ctx->sort_paths == 2; // sort of the appended list (its length read back)
+    // bounce 0 of a multi-bounce frame: the trace kernels shade their camera rays into the path
+    // state and append the paths that go on (no hit records, no shade launch: C5 -0.7 ms)
+    const bool fuse_first = compact && !sorted && mode == 0 && !ctx->packet && !ctx->wave_queue && !dcounters;
     size_t qtemp_bytes = 0;
     if (compact) {
         qtemp_bytes = (sorted || listsort) ? ort::sortAliveTempBytes((int)slots) : 0;
@@ -1417,6 +1456,7 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
         a.nobounce = maxd <= 0;
         for (int b = 0; b < bounces; ++b) {
             a.last = (b == bounces - 1);
+            const int fmode = fuse ? 1 : ((b == 0 && fuse_first && !a.rays_stored) ? 2 : 0);
             if (!a.nobounce) {
                 HIPCHK(ctx, hipMemsetAsync(ctx->defer_count.p, 0, 64, s));
                 const int slot = fslot;
@@ -1429,8 +1469,14 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                 if (timed) HIPCHK(ctx, hipEventRecord(ctx->tr0[slot][seg], s));
                 const bool prim = (b == 0) && !a.rays_stored;
                 const int pb = (pers_all || (pers_bounce && b > 0)) ? pblocks : 0;
-                e = dcounters ? launch_trace<true>(mode, prim, a, (int)blocks, pb, lds, s, ctx->packet != 0, fuse, qblocks)
-                              : launch_trace<false>(mode, prim, a, (int)blocks, pb, lds, s, ctx->packet != 0, fuse, qblocks);
+                PipeArgs at = a;
+                if (fmode == 2) {  // the trace kernels append bounce 1's list (as ort_shade_kernel would)
+                    HIPCHK(ctx, hipMemsetAsync(ctx->qcount.p, 0, sizeof(int), s));
+                    at.qnext = (int*)ctx->qlist.p;
+                    at.qnext_count = (int*)ctx->qcount.p;
+                }
+                e = dcounters ? launch_trace<true>(mode, prim, at, (int)blocks, pb, lds, s, ctx->packet != 0, fmode, qblocks)
+                              : launch_trace<false>(mode, prim, at, (int)blocks, pb, lds, s, ctx->packet != 0, fmode, qblocks);
                 if (e != hipSuccess) return hip_fail(ctx, e, "trace kernel launch");
                 if (timed) {
                     HIPCHK(ctx, hipEventRecord(ctx->tr1[slot][seg], s));
@@ -1439,16 +1485,17 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                 if (mode == 0) {
                     const bool prim = (b == 0) && !a.rays_stored;
                     const dim3 g(exact_blocks), t(kBlock);
-                    if (dcounters && fuse) hipLaunchKernelGGL((ort_trace_exact<true, true, true>), g, t, lds_exact, s, a);
-                    else if (dcounters && prim) hipLaunchKernelGGL((ort_trace_exact<true, true, false>), g, t, lds_exact, s, a);
-                    else if (dcounters) hipLaunchKernelGGL((ort_trace_exact<true, false, false>), g, t, lds_exact, s, a);
-                    else if (fuse) hipLaunchKernelGGL((ort_trace_exact<false, true, true>), g, t, lds_exact, s, a);
-                    else if (prim) hipLaunchKernelGGL((ort_trace_exact<false, true, false>), g, t, lds_exact, s, a);
-                    else hipLaunchKernelGGL((ort_trace_exact<false, false, false>), g, t, lds_exact, s, a);
+                    if (dcounters && fuse) hipLaunchKernelGGL((ort_trace_exact<true, true, 1>), g, t, lds_exact, s, at);
+                    else if (dcounters && prim) hipLaunchKernelGGL((ort_trace_exact<true, true, 0>), g, t, lds_exact, s, at);
+                    else if (dcounters) hipLaunchKernelGGL((ort_trace_exact<true, false, 0>), g, t, lds_exact, s, at);
+                    else if (fuse) hipLaunchKernelGGL((ort_trace_exact<false, true, 1>), g, t, lds_exact, s, at);
+                    else if (fmode == 2) hipLaunchKernelGGL((ort_trace_exact<false, true, 2>), g, t, lds_exact, s, at);
+                    else if (prim) hipLaunchKernelGGL((ort_trace_exact<false, true, 0>), g, t, lds_exact, s, at);
+                    else hipLaunchKernelGGL((ort_trace_exact<false, false, 0>), g, t, lds_exact, s, at);
                     if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "ort_trace_exact launch");
                 }
             }
-            if (!fuse) {
+            if (!fuse && fmode != 2) {
                 // every slot in slot order (a dead path returns after reading its pd.w), not the
                 // trace's compacted list: the sorted list scatters the path-state reads and
                 // writes; in slot order they coalesce (C5 frame 65.4 -> 63.0 ms, A/B)
