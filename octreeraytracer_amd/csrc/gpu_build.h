@@ -68,11 +68,10 @@ struct SortBuffers {
     int* vals_in;
     int* vals_out;  // = the list the next bounce walks
 };
-// Coherence sort of the alive list itself (ORT_OPT_SORT_PATHS 2): list[0, n) -> b.vals_out,
-// ordered by the path key; n (the list's length) known on the host.  Temp storage as for
-// sortAlive with the same n bound.
-hipError_t sortList(void* temp, size_t temp_bytes, const float4* po, const float4* pd, const float* root_lo,
-                    const float* root_hi, const int* list, int n, const SortBuffers& b, hipStream_t s);
+// Coherence sort of the alive list itself (ORT_OPT_SORT_PATHS 2): n (key, path) pairs, keys
+// written by the kernels that appended the list (path_key.h) -> b.vals_out in key order.
+// Temp storage as for sortAlive with the same n bound.
+hipError_t sortList(void* temp, size_t temp_bytes, int n, const SortBuffers& b, hipStream_t s);
 size_t sortAliveTempBytes(int n);
 hipError_t sortAlive(void* temp, size_t temp_bytes, const float4* po, const float4* pd, int n, const float* root_lo,
                      const float* root_hi, const SortBuffers& b, int* count, hipStream_t s);

@@ -30,6 +30,7 @@
 
 #include "gpu_build.h"
 #include "kid_table.h"
+#include "path_key.h"
 
 namespace ort {
 namespace {
@@ -660,82 +661,18 @@ std::string gpuExplicitLayout(const GpuTree& t, hipStream_t s, ExplicitDev& out)
     return "";
 }
 
-#ifndef ORT_SORT_KEY
-#define ORT_SORT_KEY 3  // 1: octant | origin Morton (9 bits/axis); 2: + direction bits (C5: 2% faster);
-                        // 3: the Morton bits dealt to the axes by extent (anisotropic root boxes)
-#endif
 namespace {
-[[maybe_unused]] __device__ __forceinline__ uint32_t spread3(uint32_t v) {  // 9 bits -> every third bit
-    v &= 0x1ffu;
-    v = (v | (v << 16)) & 0x030000ffu;
-    v = (v | (v << 8)) & 0x0300f00fu;
-    v = (v | (v << 4)) & 0x030c30c3u;
-    v = (v | (v << 2)) & 0x09249249u;
-    return v;
-}
-[[maybe_unused]] __device__ __forceinline__ uint32_t quant9(float x, float lo, float scale) {
-    const float q = (x - lo) * scale;
-    return q <= 0.0f ? 0u : (q >= 511.0f ? 511u : (uint32_t)q);  // NaN -> 0
-}
-// Origin code of ORT_SORT_KEY 3: kMortonBits bits, dealt one at a time to the axis whose cell
-// is currently the longest (a k-d split order: a root box of 500 x 4.8 x 500, as at C5, gets
-// its bits in x and z, not a third of them in y), most significant first.
-constexpr int kMortonBits = 21;  // alive keys stay below 2^30 (dead = 0xffffffff sorts last)
-struct MortonPlan {
-    float lo[3], scale[3];  // q_a = (x - lo) * scale in [0, 2^bits_a)
-    int bits[3];
-    uint32_t axis_lo, axis_hi;  // 2 bits per split: axis of split i (i < 16 in lo)
-};
-__device__ __forceinline__ uint32_t quantb(float x, float lo, float scale, int bits) {
-    const float q = (x - lo) * scale;
-    const float top = (float)((1u << bits) - 1u);
-    return q <= 0.0f ? 0u : (q >= top ? (uint32_t)top : (uint32_t)q);  // NaN -> 0
-}
-// The coherence key of one alive path (< 2^30): direction octant | origin code | direction.
-__device__ __forceinline__ uint32_t path_key(const float4 o, const float4 d, const float3 lo, const float3 sc,
-                                             const MortonPlan& mp) {
-    const uint32_t m = ((uint32_t)(d.z < 0.0f) << 2) | ((uint32_t)(d.x < 0.0f) << 1) | (uint32_t)(d.y < 0.0f);
-#if ORT_SORT_KEY >= 2
-    // direction (2 bits per axis of |d|/max|d|)
-    const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
-    const float inv = 3.999f / fmaxf(fmaxf(ax, ay), fmaxf(az, 1e-30f));
-    const uint32_t dq = ((uint32_t)(ax * inv) << 4) | ((uint32_t)(ay * inv) << 2) | (uint32_t)(az * inv);
-#endif
-#if ORT_SORT_KEY == 3
-    // octant | anisotropic origin code (21 bits) | direction
-    uint32_t q[3] = {quantb(o.x, mp.lo[0], mp.scale[0], mp.bits[0]), quantb(o.y, mp.lo[1], mp.scale[1], mp.bits[1]),
-                     quantb(o.z, mp.lo[2], mp.scale[2], mp.bits[2])};
-    int rem[3] = {mp.bits[0], mp.bits[1], mp.bits[2]};
-    uint32_t code = 0;
-#pragma unroll
-    for (int i = 0; i < kMortonBits; ++i) {
-        const int a = (int)(((i < 16 ? mp.axis_lo >> (2 * i) : mp.axis_hi >> (2 * (i - 16)))) & 3u);
-        const int r = a == 0 ? --rem[0] : (a == 1 ? --rem[1] : --rem[2]);
-        const uint32_t qa = a == 0 ? q[0] : (a == 1 ? q[1] : q[2]);
-        code = (code << 1) | ((qa >> r) & 1u);
-    }
-    return (m << 27) | (code << 6) | dq;
-#elif ORT_SORT_KEY == 2
-    // octant | origin Morton (7 bits per axis) | direction
-    return (m << 27) | ((spread3(quant9(o.x, lo.x, sc.x) >> 2) << 2 | spread3(quant9(o.y, lo.y, sc.y) >> 2) << 1 |
-                        spread3(quant9(o.z, lo.z, sc.z) >> 2)) << 6) | dq;
-#else
-    return (m << 27) | (spread3(quant9(o.x, lo.x, sc.x)) << 2) | (spread3(quant9(o.y, lo.y, sc.y)) << 1) |
-           spread3(quant9(o.z, lo.z, sc.z));
-#endif
-}
-
 // Grid-stride, one atomic per block: an atomic per wave on the one counter serialised
 // (~0.5 M atomics at C5 took 3.8 ms per bounce).
-__global__ void k_path_keys(const float4* po, const float4* pd, int n, float3 lo, float3 sc, MortonPlan mp,
-                            uint32_t* keys, int* vals, int* count) {
+__global__ void k_path_keys(const float4* po, const float4* pd, int n, MortonPlan mp, uint32_t* keys, int* vals,
+                            int* count) {
     __shared__ int wave_alive[kB / 64];
     int alive_n = 0;
     for (int k = blockIdx.x * kB + threadIdx.x; k < n; k += gridDim.x * kB) {
         const float4 d = pd[k];
         const bool alive = d.w != 0.0f;
         uint32_t key = 0xffffffffu;
-        if (alive) key = path_key(po[k], d, lo, sc, mp);
+        if (alive) key = path_key(po[k], d, mp);
         keys[k] = key;
         vals[k] = k;
         alive_n += alive ? 1 : 0;
@@ -752,66 +689,12 @@ __global__ void k_path_keys(const float4* po, const float4* pd, int n, float3 lo
     }
 }
 
-// Keys of the alive list (sort_paths 2): key i = the coherence key of path list[i], >> drop.
-__global__ void k_list_keys(const float4* po, const float4* pd, const int* list, int n, float3 lo, float3 sc,
-                            MortonPlan mp, int drop, uint32_t* keys, int* vals) {
-    for (int i = blockIdx.x * kB + threadIdx.x; i < n; i += gridDim.x * kB) {
-        const int k = list[i];
-        keys[i] = path_key(po[k], pd[k], lo, sc, mp) >> drop;
-        vals[i] = k;
-    }
-}
-
-void plan_for(const float* root_lo, const float* root_hi, float3& lo, float3& sc, MortonPlan& mp) {
-    float l[3], c[3];
-    for (int a = 0; a < 3; ++a) {
-        const float ext = root_hi[a] - root_lo[a];
-        l[a] = root_lo[a];
-        c[a] = (ext > 0.0f && ext < 3.0e38f) ? 512.0f / ext : 0.0f;
-    }
-    lo = make_float3(l[0], l[1], l[2]);
-    sc = make_float3(c[0], c[1], c[2]);
-    mp = MortonPlan{};
-    // deal kMortonBits splits to the longest current cell
-    float cell[3];
-    for (int a = 0; a < 3; ++a) {
-        const float ext = root_hi[a] - root_lo[a];
-        cell[a] = (ext > 0.0f && ext < 3.0e38f) ? ext : 0.0f;
-        mp.lo[a] = root_lo[a];
-    }
-    for (int i = 0; i < kMortonBits; ++i) {
-        int a = 0;
-        for (int j = 1; j < 3; ++j)
-            if (cell[j] > cell[a]) a = j;
-        cell[a] *= 0.5f;
-        mp.bits[a] += 1;
-        if (i < 16) mp.axis_lo |= (uint32_t)a << (2 * i);
-        else mp.axis_hi |= (uint32_t)a << (2 * (i - 16));
-    }
-    for (int a = 0; a < 3; ++a) {
-        const float ext = root_hi[a] - root_lo[a];
-        mp.scale[a] = (ext > 0.0f && ext < 3.0e38f) ? (float)(1u << mp.bits[a]) / ext : 0.0f;
-    }
-}
 }  // namespace
 
-#ifndef ORT_LIST_SORT_BITS
-#define ORT_LIST_SORT_BITS 30  // key bits sorted by sortList (the lowest 30 - bits are dropped)
-#endif
-
-hipError_t sortList(void* temp, size_t temp_bytes, const float4* po, const float4* pd, const float* root_lo,
-                    const float* root_hi, const int* list, int n, const SortBuffers& b, hipStream_t s) {
+hipError_t sortList(void* temp, size_t temp_bytes, int n, const SortBuffers& b, hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    float3 lo, sc;
-    MortonPlan mp;
-    plan_for(root_lo, root_hi, lo, sc, mp);
-    const int grid = std::max(1, std::min((n + kB - 1) / kB, 2048));
-    hipLaunchKernelGGL(k_list_keys, dim3(grid), dim3(kB), 0, s, po, pd, list, n, lo, sc, mp, 30 - ORT_LIST_SORT_BITS,
-                       b.keys_in, b.vals_in);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
     return rocprim::radix_sort_pairs(temp, temp_bytes, b.keys_in, b.keys_out, b.vals_in, b.vals_out, (size_t)n, 0,
-                                     ORT_LIST_SORT_BITS, s);
+                                     kPathKeyBits, s);
 }
 
 size_t sortAliveTempBytes(int n) {
@@ -825,11 +708,9 @@ hipError_t sortAlive(void* temp, size_t temp_bytes, const float4* po, const floa
                      const float* root_hi, const SortBuffers& b, int* count, hipStream_t s) {
     hipError_t e = hipMemsetAsync(count, 0, sizeof(int), s);
     if (e != hipSuccess) return e;
-    float3 lo, sc;
-    MortonPlan mp;
-    plan_for(root_lo, root_hi, lo, sc, mp);
-    hipLaunchKernelGGL(k_path_keys, dim3(std::min((n + kB - 1) / kB, 2048)), dim3(kB), 0, s, po, pd, n, lo, sc, mp,
-                       b.keys_in, b.vals_in, count);
+    const MortonPlan mp = mortonPlan(root_lo, root_hi);
+    hipLaunchKernelGGL(k_path_keys, dim3(std::min((n + kB - 1) / kB, 2048)), dim3(kB), 0, s, po, pd, n, mp, b.keys_in,
+                       b.vals_in, count);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     // alive keys are < 2^30, dead keys 0xffffffff: on bits [0, 31) every dead key sorts after
     // every alive one

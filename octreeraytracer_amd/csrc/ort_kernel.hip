@@ -26,6 +26,7 @@
 #include "camera.h"
 #include "gpu_build.h"
 #include "layout.h"
+#include "path_key.h"
 #include "ort_internal.h"
 #include "render_core.h"
 
@@ -58,6 +59,8 @@ struct PipeArgs {
     const int* qcount;   // their number (device)
     int* qnext;          // shade kernels: append the paths that go on here (next bounce's list), or null
     int* qnext_count;
+    uint32_t* qnext_keys;  // ... and their coherence keys beside them (ORT_OPT_SORT_PATHS 2), or null
+    ort::MortonPlan mp;    // the keys' origin code (path_key.h)
     int2* hit;        // per path: {entry (-1 miss), t bits}
     int* defer_list;
     int* sync;        // [0] deferred count, [1] work cursor of the persistent trace
@@ -439,7 +442,7 @@ __device__ __forceinline__ bool shade_state(const PipeArgs& A, int k, size_t p, 
 
 // Appends slot k (where go) to list / count: one atomic per workgroup, the workgroup's slots
 // kept in increasing order.  Every thread of the workgroup must call it.
-__device__ inline void append_slots(bool go, int k, int* list, int* count) {
+__device__ inline void append_slots(bool go, int k, uint32_t key, int* list, uint32_t* keys, int* count) {
     __shared__ int wcnt[kBlock / 64];
     __shared__ int wbase;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -455,7 +458,11 @@ __device__ inline void append_slots(bool go, int k, int* list, int* count) {
     int off = wbase;
     for (int i = 0; i < w; ++i) off += wcnt[i];
     const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    if (go) list[off + __popcll(m & below)] = k;
+    if (go) {
+        const int pos = off + __popcll(m & below);
+        list[pos] = k;
+        if (keys) keys[pos] = key;
+    }
 }
 
 // One ray per lane over the compact layout (default): the tile-block order of the path
@@ -526,7 +533,9 @@ __device__ __forceinline__ void trace_compact_body(PipeArgs& A, unsigned char* s
 #if defined(__HIP_DEVICE_COMPILE__)
         typedef __attribute__((address_space(4))) const PipeArgs KernArgs;
         KernArgs* kp = (KernArgs*)__builtin_amdgcn_kernarg_segment_ptr();
-        append_slots(go, k, kp->qnext, kp->qnext_count);
+        uint32_t key = 0;
+        if (go && kp->qnext_keys) key = ort::path_key(kp->po[k], kp->pd[k], kp->mp);  // the state just stored
+        append_slots(go, k, key, kp->qnext, kp->qnext_keys, kp->qnext_count);
 #endif
     }
     flush_counts<COUNT>(cnt, A.counters);
@@ -845,8 +854,11 @@ __global__ void __launch_bounds__(kBlock) ort_trace_exact(PipeArgs A) {
         if (FUSE == 1) {
             shade_direct(A, k, ray, rng, st == ORT_TRACE_HIT, entry, t);
         } else if (FUSE == 2) {  // bounce 0 shaded here; the rare deferred path joins the list alone
-            if (shade_state<0, true, false>(A, k, 0, ray, rng, st == ORT_TRACE_HIT ? entry : -1, t))
-                A.qnext[atomicAdd(A.qnext_count, 1)] = k;
+            if (shade_state<0, true, false>(A, k, 0, ray, rng, st == ORT_TRACE_HIT ? entry : -1, t)) {
+                const int pos = atomicAdd(A.qnext_count, 1);
+                A.qnext[pos] = k;
+                if (A.qnext_keys) A.qnext_keys[pos] = ort::path_key(A.po[k], A.pd[k], A.mp);
+            }
         } else {
             A.hit[k] = make_int2(st == ORT_TRACE_HIT ? entry : -1, __float_as_int(t));
         }
@@ -903,7 +915,11 @@ template <int MODE, bool FIRST, bool DIRECT>
 __global__ void __launch_bounds__(kBlock) ort_shade_kernel(PipeArgs A) {
     const int k = blockIdx.x * kBlock + threadIdx.x;
     const bool go = shade_slot<MODE, FIRST, DIRECT>(A, k);
-    if (!DIRECT && A.qnext) append_slots(go, k, A.qnext, A.qnext_count);
+    if (!DIRECT && A.qnext) {
+        uint32_t key = 0;
+        if (go && A.qnext_keys) key = ort::path_key(A.po[k], A.pd[k], A.mp);  // the state just stored
+        append_slots(go, k, key, A.qnext, A.qnext_keys, A.qnext_count);
+    }
 }
 
 // col / ns, gamma (glsl:659-661) for the multi-sample / multi-bounce case.
@@ -979,7 +995,7 @@ struct ort_ctx {
     // wavefront pipeline state, sized for the largest tile rendered so far
     DevBuf hit, defer_list, defer_count, po, pd, pc, prng, pcol;
     DevBuf qlist, qcount, qtemp;  // bounce >= 1 path compaction
-    DevBuf skeys, skeys2, svals, shist;  // coherence sort (shist: the list sort's value input)
+    DevBuf skeys, skeys2, svals;  // coherence sort
 };
 
 namespace {
@@ -1405,7 +1421,7 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                        (rc = ensure(ctx, ctx->svals, 4 * slots))))
             return rc;
         if (listsort && ((rc = ensure(ctx, ctx->skeys, 4 * slots)) || (rc = ensure(ctx, ctx->skeys2, 4 * slots)) ||
-                         (rc = ensure(ctx, ctx->shist, 4 * slots)) || (rc = ensure(ctx, ctx->svals, 4 * slots))))
+                         (rc = ensure(ctx, ctx->svals, 4 * slots))))
             return rc;
     }
     PipeArgs a;
@@ -1433,6 +1449,7 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     a.counters = dcounters;
     a.wclock = (ulonglong4*)ctx->wclock;
     a.wclock_n = (int)ctx->wclock_n;
+    a.mp = ort::mortonPlan(ctx->root_lo, ctx->root_hi);
     const size_t lds = lds_bytes(mode, ctx->depth, false);
     const size_t lds_exact = lds_bytes(mode, ctx->depth, true);
     const int pblocks = (mode == 0 && ctx->persistent) ? persistent_blocks(ctx->device, dcounters != nullptr, ctx->depth > 8, lds, blocks) : 0;
@@ -1474,6 +1491,7 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                     HIPCHK(ctx, hipMemsetAsync(ctx->qcount.p, 0, sizeof(int), s));
                     at.qnext = (int*)ctx->qlist.p;
                     at.qnext_count = (int*)ctx->qcount.p;
+                    at.qnext_keys = listsort ? (uint32_t*)ctx->skeys.p : nullptr;
                 }
                 e = dcounters ? launch_trace<true>(mode, prim, at, (int)blocks, pb, lds, s, ctx->packet != 0, fmode, qblocks)
                               : launch_trace<false>(mode, prim, at, (int)blocks, pb, lds, s, ctx->packet != 0, fmode, qblocks);
@@ -1509,6 +1527,7 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                     HIPCHK(ctx, hipMemsetAsync(ctx->qcount.p, 0, sizeof(int), s));
                     a2.qnext = (int*)ctx->qlist.p;
                     a2.qnext_count = (int*)ctx->qcount.p;
+                    a2.qnext_keys = listsort ? (uint32_t*)ctx->skeys.p : nullptr;
                 }
                 e = launch_shade(mode, b == 0, direct, a2, (int)blocks, s);
                 if (e != hipSuccess) return hip_fail(ctx, e, "ort_shade_kernel launch");
@@ -1527,10 +1546,10 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                     int n_alive = 0;
                     HIPCHK(ctx, hipMemcpyAsync(&n_alive, ctx->qcount.p, sizeof(int), hipMemcpyDeviceToHost, s));
                     HIPCHK(ctx, hipStreamSynchronize(s));
-                    const ort::SortBuffers sb{(uint32_t*)ctx->skeys.p, (uint32_t*)ctx->skeys2.p, (int*)ctx->shist.p,
+                    // (key, path) pairs as the shade / trace kernels appended them
+                    const ort::SortBuffers sb{(uint32_t*)ctx->skeys.p, (uint32_t*)ctx->skeys2.p, (int*)ctx->qlist.p,
                                               (int*)ctx->svals.p};
-                    e = ort::sortList(ctx->qtemp.p, qtemp_bytes, (const float4*)ctx->po.p, (const float4*)ctx->pd.p,
-                                      ctx->root_lo, ctx->root_hi, (const int*)ctx->qlist.p, n_alive, sb, s);
+                    e = ort::sortList(ctx->qtemp.p, qtemp_bytes, n_alive, sb, s);
                     if (e != hipSuccess) return hip_fail(ctx, e, "path list sort");
                 }
                 a.qlist = (const int*)(listsort ? ctx->svals.p : ctx->qlist.p);
@@ -1608,7 +1627,7 @@ int ort_destroy(ort_ctx* ctx) {
     free_buf(ctx->counters);
     free_buf(ctx->lut);
     DevBuf* pipe[] = {&ctx->hit, &ctx->defer_list, &ctx->defer_count, &ctx->po, &ctx->pd, &ctx->pc, &ctx->prng, &ctx->pcol,
-                      &ctx->qlist, &ctx->qcount, &ctx->qtemp, &ctx->skeys, &ctx->skeys2, &ctx->svals, &ctx->shist};
+                      &ctx->qlist, &ctx->qcount, &ctx->qtemp, &ctx->skeys, &ctx->skeys2, &ctx->svals};
     for (DevBuf* b : pipe) free_buf(*b);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);

@@ -1,0 +1,78 @@
+// path_key.h -- the coherence key of an alive path between bounces (ORT_OPT_SORT_PATHS):
+// computed where a path is appended to the next bounce's list (ort_kernel.hip shade/trace
+// kernels) and by the every-slot sort (gpu_build.hip sortAlive).  Only orders work: pixels
+// never depend on it.
+//
+// key = direction octant (3 bits) | origin code (kMortonBits) | direction (2 bits per axis of
+// |d| / max|d|), < 2^30.  The origin code quantises the origin in the tree's root box and deals
+// its bits one at a time to the axis whose cell is currently the longest (a k-d split order: a
+// root box of 500 x 4.8 x 500, as at C5, gets its bits in x and z, not a third of them in y),
+// most significant first.  Measured on C5 (tools/ab_stream.py): every one of these bits counts
+// -- 24-bit keys (fewer origin bits), octant-only and octant + direction orders were all slower.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ort {
+
+constexpr int kMortonBits = 21;
+constexpr int kPathKeyBits = 3 + kMortonBits + 6;  // 30: alive keys < 2^30, dead = 0xffffffff
+
+struct MortonPlan {
+    float lo[3], scale[3];      // q_a = (x - lo) * scale in [0, 2^bits_a)
+    int bits[3];
+    uint32_t axis_lo, axis_hi;  // 2 bits per split: axis of split i (i < 16 in lo)
+};
+
+// Host: the split plan of a root box.
+inline MortonPlan mortonPlan(const float* root_lo, const float* root_hi) {
+    MortonPlan mp{};
+    float cell[3];
+    for (int a = 0; a < 3; ++a) {
+        const float ext = root_hi[a] - root_lo[a];
+        cell[a] = (ext > 0.0f && ext < 3.0e38f) ? ext : 0.0f;
+        mp.lo[a] = root_lo[a];
+    }
+    for (int i = 0; i < kMortonBits; ++i) {  // deal the splits to the longest current cell
+        int a = 0;
+        for (int j = 1; j < 3; ++j)
+            if (cell[j] > cell[a]) a = j;
+        cell[a] *= 0.5f;
+        mp.bits[a] += 1;
+        if (i < 16) mp.axis_lo |= (uint32_t)a << (2 * i);
+        else mp.axis_hi |= (uint32_t)a << (2 * (i - 16));
+    }
+    for (int a = 0; a < 3; ++a) {
+        const float ext = root_hi[a] - root_lo[a];
+        mp.scale[a] = (ext > 0.0f && ext < 3.0e38f) ? (float)(1u << mp.bits[a]) / ext : 0.0f;
+    }
+    return mp;
+}
+
+__device__ __forceinline__ uint32_t key_quant(float x, float lo, float scale, int bits) {
+    const float q = (x - lo) * scale;
+    const float top = (float)((1u << bits) - 1u);
+    return q <= 0.0f ? 0u : (q >= top ? (uint32_t)top : (uint32_t)q);  // NaN -> 0
+}
+
+__device__ __forceinline__ uint32_t path_key(const float4 o, const float4 d, const MortonPlan& mp) {
+    const uint32_t m = ((uint32_t)(d.z < 0.0f) << 2) | ((uint32_t)(d.x < 0.0f) << 1) | (uint32_t)(d.y < 0.0f);
+    const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
+    const float inv = 3.999f / fmaxf(fmaxf(ax, ay), fmaxf(az, 1e-30f));
+    const uint32_t dq = ((uint32_t)(ax * inv) << 4) | ((uint32_t)(ay * inv) << 2) | (uint32_t)(az * inv);
+    const uint32_t q[3] = {key_quant(o.x, mp.lo[0], mp.scale[0], mp.bits[0]),
+                           key_quant(o.y, mp.lo[1], mp.scale[1], mp.bits[1]),
+                           key_quant(o.z, mp.lo[2], mp.scale[2], mp.bits[2])};
+    int rem[3] = {mp.bits[0], mp.bits[1], mp.bits[2]};
+    uint32_t code = 0;
+#pragma unroll
+    for (int i = 0; i < kMortonBits; ++i) {
+        const int a = (int)(((i < 16 ? mp.axis_lo >> (2 * i) : mp.axis_hi >> (2 * (i - 16)))) & 3u);
+        const int r = a == 0 ? --rem[0] : (a == 1 ? --rem[1] : --rem[2]);
+        const uint32_t qa = a == 0 ? q[0] : (a == 1 ? q[1] : q[2]);
+        code = (code << 1) | ((qa >> r) & 1u);
+    }
+    return (m << (6 + kMortonBits)) | (code << 6) | dq;
+}
+
+}  // namespace ort
