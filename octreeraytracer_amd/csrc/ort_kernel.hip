@@ -247,8 +247,11 @@ __global__ void __launch_bounds__(kBlock) ort_raygen_kernel(PipeArgs A) {
 #ifndef ORT_TRACE_WAVES
 #define ORT_TRACE_WAVES 8
 #endif
-#ifndef ORT_TRACE_WAVES_DEEP  // 96-bit masks, no inline leaf children: 64 VGPRs, spill-free
-#define ORT_TRACE_WAVES_DEEP 8
+// Deep (depth > 8) per-lane kernel: its LDS image (24.6 KB per 256-thread workgroup at depth 10)
+// caps a CU at 6 workgroups = 6 waves/SIMD, so it may use the registers of 6 waves: 64-69
+// VGPRs without spills (at 8 the bounce-0 shading variant spilled 3; C5 +0.4 % in A/B).
+#ifndef ORT_TRACE_WAVES_DEEP
+#define ORT_TRACE_WAVES_DEEP 6
 #endif
 // Items a wave takes from the global cursor at a time.  The resident waves then work on a
 // window of about (waves x kChunk) consecutive list items -- neighbouring paths, overlapping
