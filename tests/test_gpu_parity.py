@@ -186,6 +186,30 @@ def test_kernel_variants_identical(ort, oracle, renderer, scene_c2, persistent, 
         renderer.set_wave_queue(False)
 
 
+@pytest.mark.parametrize("kid_skip", [1, 0])
+@pytest.mark.parametrize("sort", [2, 1, 0])
+@pytest.mark.parametrize("depth,mspn", [(6, 1), (10, 1)])
+def test_bounce_orders_and_skip_identical(ort, oracle, renderer, depth, mspn, sort, kid_skip):
+    """Every order of the alive paths between bounces (ORT_OPT_SORT_PATHS: list sort with the
+    length read back, every-slot sort, slot order) and the rejected-sphere skip on and off give
+    the oracle's pixels, on maxSpheresPerNode-1 trees (where the skip fires) of depth 6 (64-bit
+    bounce walk) and 10 (96-bit), with several samples (path state carried across samples)."""
+    s = ort.random_spheres(8000, 3)
+    t = ort.build_octree(s, depth, mspn)
+    renderer.upload(s, t)
+    renderer.set_sort_paths(sort)
+    renderer.set_kid_skip(kid_skip)
+    try:
+        p = ort.FrameParams.default_camera(960, 540, num_samples=2, max_depth=5)
+        tile = ort.Tile(100, 400, 200, 96)
+        got = renderer.render(p, tile)
+        ref = oracle.render(s, t, p, tile.x0, tile.y0, tile.width, tile.rows)
+        assert_same(got, ref, f"sort={sort} kid_skip={kid_skip} d{depth}")
+    finally:
+        renderer.set_sort_paths(2)  # the defaults
+        renderer.set_kid_skip(1)
+
+
 @pytest.fixture(scope="module")
 def scene_c3(ort):
     s = ort.random_spheres(100_000, 42)
