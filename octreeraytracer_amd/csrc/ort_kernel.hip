@@ -181,9 +181,17 @@ __host__ __device__ inline void block_tile(const PipeArgs& A, int blk, int& bx, 
 }
 
 // Path slot k (tile-block order: 256 slots = one 16x16 tile, 64 = one 8x8 wave block)
-// -> tile column/row.  Returns false for slots outside the tile.
+// -> tile column/row.  Returns false for slots outside the tile.  UNI: every lane of the wave
+// holds a slot of the same 256-slot block (the per-tile kernels), so the tile lookup -- two
+// integer divisions by the tile-grid width -- runs once per wave on the scalar unit.
+template <bool UNI = false>
 __host__ __device__ inline bool slot_coords(const PipeArgs& A, int k, int& col, int& row) {
-    const int blk = k >> 8, tid = k & 255, wave = tid >> 6, lane = tid & 63;
+#if defined(__HIP_DEVICE_COMPILE__)
+    const int blk = UNI ? __builtin_amdgcn_readfirstlane(k >> 8) : k >> 8;
+#else
+    const int blk = k >> 8;
+#endif
+    const int tid = k & 255, wave = tid >> 6, lane = tid & 63;
     int bx, by;
     block_tile(A, blk, bx, by);
     col = bx * 16 + (wave & 1) * 8 + (lane & 7);
@@ -211,7 +219,7 @@ __device__ inline ort::Ray load_ray(const PipeArgs& A, int k, bool& alive) {
 __global__ void __launch_bounds__(kBlock) ort_raygen_kernel(PipeArgs A) {
     const int k = blockIdx.x * kBlock + threadIdx.x;
     int col, row;
-    const bool in = slot_coords(A, k, col, row);
+    const bool in = slot_coords<true>(A, k, col, row);
     const int y = in ? tile_row_to_y(A.tm, row) : 0;
     if (!in || y >= A.pp.H) {
         A.pd[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // hole
@@ -341,11 +349,11 @@ __device__ inline bool list_slot(const PipeArgs& A, int& k) {
 // Path-slot ray for the trace kernels: bounce 0 generates the sample's camera ray here
 // (main() up to radiance()'s first line; the shade kernel regenerates it identically),
 // later bounces read the ray the previous shade kernel stored.
-template <bool PRIMARY>
+template <bool PRIMARY, bool UNI = false>
 __device__ inline ort::Ray slot_ray(const PipeArgs& A, int k, bool& alive, ort_rng* st_out = nullptr) {
     if constexpr (PRIMARY) {
         int col, row;
-        alive = slot_coords(A, k, col, row);
+        alive = slot_coords<UNI>(A, k, col, row);
         const int y = alive ? tile_row_to_y(A.tm, row) : 0;
         alive = alive && y < A.pp.H;
         ort::Ray ray;
@@ -370,9 +378,10 @@ __device__ inline ort::Ray slot_ray(const PipeArgs& A, int k, bool& alive, ort_r
 
 // 1 sample, 1 bounce (the primary-ray benchmark mode): the trace kernels shade their own
 // rays -- exactly ort_shade_kernel<0, true, true> -- instead of writing hit records for it.
+template <bool UNI = false>
 __device__ inline void shade_direct(const PipeArgs& A, int k, ort::Ray ray, ort_rng st, bool hit, int entry, float t) {
     int col, row;
-    (void)slot_coords(A, k, col, row);
+    (void)slot_coords<UNI>(A, k, col, row);
     ort::V3 c = ort::mk(1.0f, 1.0f, 1.0f);
     float importance = 1.0f;
     ort::HitRec rec;
@@ -389,7 +398,7 @@ __device__ inline void shade_direct(const PipeArgs& A, int k, ort::Ray ray, ort_
 // Tile rows past the frame (band padding) are written as zeros, as the shade kernel does.
 __device__ inline void shade_direct_padding(const PipeArgs& A, int k) {
     int col, row;
-    if (!slot_coords(A, k, col, row) || tile_row_to_y(A.tm, row) < A.pp.H) return;
+    if (!slot_coords<true>(A, k, col, row) || tile_row_to_y(A.tm, row) < A.pp.H) return;
     float* o = A.out + 3 * ((size_t)row * A.tm.tw + col);
     o[0] = 0.0f;
     o[1] = 0.0f;
@@ -479,7 +488,7 @@ template <bool COUNT, bool PRIMARY, bool DEEP, int FUSE>
 __device__ __forceinline__ bool trace_slot(PipeArgs& A, LdsView& L, int k, ort::Counters& cnt) {
     bool alive;
     ort_rng rng0;  // FUSE: the camera ray's RNG state, kept for the shading after the walk
-    const ort::Ray ray = slot_ray<PRIMARY>(A, k, alive, FUSE ? &rng0 : nullptr);
+    const ort::Ray ray = slot_ray<PRIMARY, true>(A, k, alive, FUSE ? &rng0 : nullptr);
     if (!alive) {
         if (FUSE == 1) shade_direct_padding(A, k);
         if (FUSE == 2) A.pd[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // never alive (ort_shade_kernel's hole)
@@ -513,7 +522,7 @@ __device__ __forceinline__ bool trace_slot(PipeArgs& A, LdsView& L, int k, ort::
         const PipeArgs& A2 = A;
 #endif
         if constexpr (FUSE == 1) {
-            shade_direct(A2, k2, walked, rng0, hit, entry, t);
+            shade_direct<true>(A2, k2, walked, rng0, hit, entry, t);
         } else {
             return shade_state<0, true, false>(A2, k2, 0, walked, rng0, hit ? entry : -1, t);
         }
@@ -876,7 +885,7 @@ template <int MODE, bool FIRST, bool DIRECT>
 __device__ __forceinline__ bool shade_slot(const PipeArgs& A, int k) {
     if (!FIRST && !list_slot(A, k)) return false;
     int col, row;
-    const bool in_tile = slot_coords(A, k, col, row);
+    const bool in_tile = FIRST ? slot_coords<true>(A, k, col, row) : slot_coords(A, k, col, row);
     const int y = in_tile ? tile_row_to_y(A.tm, row) : 0;
     const size_t p = (size_t)row * A.tm.tw + col;
     if (!in_tile || y >= A.pp.H) {
@@ -929,7 +938,7 @@ __global__ void __launch_bounds__(kBlock) ort_shade_kernel(PipeArgs A) {
 __global__ void __launch_bounds__(kBlock) ort_finalize_kernel(PipeArgs A) {
     const int k = blockIdx.x * kBlock + threadIdx.x;
     int col, row;
-    if (!slot_coords(A, k, col, row)) return;
+    if (!slot_coords<true>(A, k, col, row)) return;
     const int y = tile_row_to_y(A.tm, row);
     float* o = A.out + 3 * ((size_t)row * A.tm.tw + col);
     if (y >= A.pp.H) {

@@ -1328,8 +1328,11 @@ ORT_FN Ray primary_ray(const PixelParams& P, int px, int py, int s, ort_rng& st)
     const int sqrt_ns = (int)sqrtf((float)P.ns);
     const int i = s % sqrt_ns;
     const int j = s / sqrt_ns;
-    const float u = (fx + ((float)i + ort_rand2D(&st)) / (float)sqrt_ns) / W;
-    const float v = (fy + ((float)j + ort_rand2D(&st)) / (float)sqrt_ns) / H;
+    // x / 1.0f == x exactly: one sample per pixel (the benchmark) skips both divisions
+    const float ru = (float)i + ort_rand2D(&st);
+    const float u = (fx + (sqrt_ns == 1 ? ru : ru / (float)sqrt_ns)) / W;
+    const float rv = (float)j + ort_rand2D(&st);
+    const float v = (fy + (sqrt_ns == 1 ? rv : rv / (float)sqrt_ns)) / H;
     Ray ray = camera_ray(P.cam, u, v, W, H, st);
     ray.d = normalize(ray.d);
     return ray;
