@@ -1434,7 +1434,7 @@ ORT_FN bool shade_bounce(bool hit, const HitRec& h, Ray& ray, V3& c, float& impo
 // col /= float(numSamples); pow(col, 1/2.2) (glsl:659-661)
 ORT_FN V3 finish_pixel(V3 col, int ns) {
     const float fns = (float)ns;
-    col = mk(col.x / fns, col.y / fns, col.z / fns);
+    if (ns != 1) col = mk(col.x / fns, col.y / fns, col.z / fns);  // x / 1.0f == x exactly
     const float g = 1.0f / 2.2f;
     return mk(ort_powf(col.x, g), ort_powf(col.y, g), ort_powf(col.z, g));
 }
