@@ -74,5 +74,5 @@ struct SortBuffers {
 hipError_t sortList(void* temp, size_t temp_bytes, int n, const SortBuffers& b, hipStream_t s);
 size_t sortAliveTempBytes(int n);
 hipError_t sortAlive(void* temp, size_t temp_bytes, const float4* po, const float4* pd, int n, const float* root_lo,
-                     const float* root_hi, const SortBuffers& b, int* count, hipStream_t s);
+                     const float* root_hi, const uint32_t* spread, const SortBuffers& b, int* count, hipStream_t s);
 }  // namespace ort

@@ -664,15 +664,15 @@ std::string gpuExplicitLayout(const GpuTree& t, hipStream_t s, ExplicitDev& out)
 namespace {
 // Grid-stride, one atomic per block: an atomic per wave on the one counter serialised
 // (~0.5 M atomics at C5 took 3.8 ms per bounce).
-__global__ void k_path_keys(const float4* po, const float4* pd, int n, MortonPlan mp, uint32_t* keys, int* vals,
-                            int* count) {
+__global__ void k_path_keys(const float4* po, const float4* pd, int n, MortonPlan mp, const uint32_t* spread,
+                            uint32_t* keys, int* vals, int* count) {
     __shared__ int wave_alive[kB / 64];
     int alive_n = 0;
     for (int k = blockIdx.x * kB + threadIdx.x; k < n; k += gridDim.x * kB) {
         const float4 d = pd[k];
         const bool alive = d.w != 0.0f;
         uint32_t key = 0xffffffffu;
-        if (alive) key = path_key(po[k], d, mp);
+        if (alive) key = path_key(po[k], d, mp, spread);
         keys[k] = key;
         vals[k] = k;
         alive_n += alive ? 1 : 0;
@@ -705,12 +705,12 @@ size_t sortAliveTempBytes(int n) {
 }
 
 hipError_t sortAlive(void* temp, size_t temp_bytes, const float4* po, const float4* pd, int n, const float* root_lo,
-                     const float* root_hi, const SortBuffers& b, int* count, hipStream_t s) {
+                     const float* root_hi, const uint32_t* spread, const SortBuffers& b, int* count, hipStream_t s) {
     hipError_t e = hipMemsetAsync(count, 0, sizeof(int), s);
     if (e != hipSuccess) return e;
     const MortonPlan mp = mortonPlan(root_lo, root_hi);
-    hipLaunchKernelGGL(k_path_keys, dim3(std::min((n + kB - 1) / kB, 2048)), dim3(kB), 0, s, po, pd, n, mp, b.keys_in,
-                       b.vals_in, count);
+    hipLaunchKernelGGL(k_path_keys, dim3(std::min((n + kB - 1) / kB, 2048)), dim3(kB), 0, s, po, pd, n, mp, spread,
+                       b.keys_in, b.vals_in, count);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     // alive keys are < 2^30, dead keys 0xffffffff: on bits [0, 31) every dead key sorts after
     // every alive one

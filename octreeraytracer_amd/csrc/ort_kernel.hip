@@ -61,6 +61,7 @@ struct PipeArgs {
     int* qnext_count;
     uint32_t* qnext_keys;  // ... and their coherence keys beside them (ORT_OPT_SORT_PATHS 2), or null
     ort::MortonPlan mp;    // the keys' origin code (path_key.h)
+    const uint32_t* key_spread;  // ... as table lookups (mortonSpread)
     int2* hit;        // per path: {entry (-1 miss), t bits}
     int* defer_list;
     int* sync;        // [0] deferred count, [1] work cursor of the persistent trace
@@ -546,7 +547,7 @@ __device__ __forceinline__ void trace_compact_body(PipeArgs& A, unsigned char* s
         typedef __attribute__((address_space(4))) const PipeArgs KernArgs;
         KernArgs* kp = (KernArgs*)__builtin_amdgcn_kernarg_segment_ptr();
         uint32_t key = 0;
-        if (go && kp->qnext_keys) key = ort::path_key(kp->po[k], kp->pd[k], kp->mp);  // the state just stored
+        if (go && kp->qnext_keys) key = ort::path_key(kp->po[k], kp->pd[k], kp->mp, kp->key_spread);  // the state just stored
         append_slots(go, k, key, kp->qnext, kp->qnext_keys, kp->qnext_count);
 #endif
     }
@@ -869,7 +870,7 @@ __global__ void __launch_bounds__(kBlock) ort_trace_exact(PipeArgs A) {
             if (shade_state<0, true, false>(A, k, 0, ray, rng, st == ORT_TRACE_HIT ? entry : -1, t)) {
                 const int pos = atomicAdd(A.qnext_count, 1);
                 A.qnext[pos] = k;
-                if (A.qnext_keys) A.qnext_keys[pos] = ort::path_key(A.po[k], A.pd[k], A.mp);
+                if (A.qnext_keys) A.qnext_keys[pos] = ort::path_key(A.po[k], A.pd[k], A.mp, A.key_spread);
             }
         } else {
             A.hit[k] = make_int2(st == ORT_TRACE_HIT ? entry : -1, __float_as_int(t));
@@ -929,7 +930,7 @@ __global__ void __launch_bounds__(kBlock) ort_shade_kernel(PipeArgs A) {
     const bool go = shade_slot<MODE, FIRST, DIRECT>(A, k);
     if (!DIRECT && A.qnext) {
         uint32_t key = 0;
-        if (go && A.qnext_keys) key = ort::path_key(A.po[k], A.pd[k], A.mp);  // the state just stored
+        if (go && A.qnext_keys) key = ort::path_key(A.po[k], A.pd[k], A.mp, A.key_spread);  // the state just stored
         append_slots(go, k, key, A.qnext, A.qnext_keys, A.qnext_count);
     }
 }
@@ -1008,6 +1009,8 @@ struct ort_ctx {
     DevBuf hit, defer_list, defer_count, po, pd, pc, prng, pcol;
     DevBuf qlist, qcount, qtemp;  // bounce >= 1 path compaction
     DevBuf skeys, skeys2, svals;  // coherence sort
+    DevBuf key_spread;            // its origin-code tables for the scene's root box (path_key.h)
+    float spread_box[6] = {0, 0, 0, 0, 0, 0};  // the root box key_spread was built for
 };
 
 namespace {
@@ -1435,6 +1438,17 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
         if (listsort && ((rc = ensure(ctx, ctx->skeys, 4 * slots)) || (rc = ensure(ctx, ctx->skeys2, 4 * slots)) ||
                          (rc = ensure(ctx, ctx->svals, 4 * slots))))
             return rc;
+        if (sorted || listsort) {  // the key tables of the current root box (built once per scene)
+            const float box[6] = {ctx->root_lo[0], ctx->root_lo[1], ctx->root_lo[2],
+                                  ctx->root_hi[0], ctx->root_hi[1], ctx->root_hi[2]};
+            if (!ctx->key_spread.p || std::memcmp(box, ctx->spread_box, sizeof box) != 0) {
+                if ((rc = ensure(ctx, ctx->key_spread, 4 * (size_t)ort::kSpreadWords))) return rc;
+                std::vector<uint32_t> tab((size_t)ort::kSpreadWords);
+                ort::mortonSpread(ort::mortonPlan(ctx->root_lo, ctx->root_hi), tab.data());
+                HIPCHK(ctx, hipMemcpy(ctx->key_spread.p, tab.data(), 4 * tab.size(), hipMemcpyHostToDevice));
+                std::memcpy(ctx->spread_box, box, sizeof box);
+            }
+        }
     }
     PipeArgs a;
     std::memset(&a, 0, sizeof(a));
@@ -1462,6 +1476,7 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     a.wclock = (ulonglong4*)ctx->wclock;
     a.wclock_n = (int)ctx->wclock_n;
     a.mp = ort::mortonPlan(ctx->root_lo, ctx->root_hi);
+    a.key_spread = (const uint32_t*)ctx->key_spread.p;
     const size_t lds = lds_bytes(mode, ctx->depth, false);
     const size_t lds_exact = lds_bytes(mode, ctx->depth, true);
     const int pblocks = (mode == 0 && ctx->persistent) ? persistent_blocks(ctx->device, dcounters != nullptr, ctx->depth > 8, lds, blocks) : 0;
@@ -1549,7 +1564,8 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                     const ort::SortBuffers sb{(uint32_t*)ctx->skeys.p, (uint32_t*)ctx->skeys2.p, (int*)ctx->svals.p,
                                               (int*)ctx->qlist.p};
                     e = ort::sortAlive(ctx->qtemp.p, qtemp_bytes, (const float4*)ctx->po.p, (const float4*)ctx->pd.p,
-                                       (int)slots, ctx->root_lo, ctx->root_hi, sb, (int*)ctx->qcount.p, s);
+                                       (int)slots, ctx->root_lo, ctx->root_hi, (const uint32_t*)ctx->key_spread.p, sb,
+                                       (int*)ctx->qcount.p, s);
                     if (e != hipSuccess) return hip_fail(ctx, e, "path compaction");
                 }  // else the shade kernel appended them
                 if (listsort) {
@@ -1639,7 +1655,7 @@ int ort_destroy(ort_ctx* ctx) {
     free_buf(ctx->counters);
     free_buf(ctx->lut);
     DevBuf* pipe[] = {&ctx->hit, &ctx->defer_list, &ctx->defer_count, &ctx->po, &ctx->pd, &ctx->pc, &ctx->prng, &ctx->pcol,
-                      &ctx->qlist, &ctx->qcount, &ctx->qtemp, &ctx->skeys, &ctx->skeys2, &ctx->svals};
+                      &ctx->qlist, &ctx->qcount, &ctx->qtemp, &ctx->skeys, &ctx->skeys2, &ctx->svals, &ctx->key_spread};
     for (DevBuf* b : pipe) free_buf(*b);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);

@@ -49,28 +49,44 @@ inline MortonPlan mortonPlan(const float* root_lo, const float* root_hi) {
     return mp;
 }
 
+// Host: the origin code as three table lookups per axis (spread[a][byte][v] = the code bits
+// that byte `byte` of axis a's quantised coordinate contributes, v its value) -- the same
+// code as dealing the kMortonBits bits one at a time, most significant first; ~9 loads
+// instead of ~130 VALU per key.  kSpreadWords entries.
+constexpr int kSpreadWords = 3 * 3 * 256;
+inline void mortonSpread(const MortonPlan& mp, uint32_t* spread) {
+    for (int i = 0; i < kSpreadWords; ++i) spread[i] = 0u;
+    int rem[3] = {mp.bits[0], mp.bits[1], mp.bits[2]};
+    for (int i = 0; i < kMortonBits; ++i) {  // split i puts bit r of axis a at code bit kMortonBits-1-i
+        const int a = (int)(((i < 16 ? mp.axis_lo >> (2 * i) : mp.axis_hi >> (2 * (i - 16)))) & 3u);
+        const int r = --rem[a];
+        const uint32_t pos = 1u << (kMortonBits - 1 - i);
+        const int byte = r >> 3, bit = r & 7;
+        for (int v = 0; v < 256; ++v)
+            if ((v >> bit) & 1) spread[(a * 3 + byte) * 256 + v] |= pos;
+    }
+}
+
 __device__ __forceinline__ uint32_t key_quant(float x, float lo, float scale, int bits) {
     const float q = (x - lo) * scale;
     const float top = (float)((1u << bits) - 1u);
     return q <= 0.0f ? 0u : (q >= top ? (uint32_t)top : (uint32_t)q);  // NaN -> 0
 }
 
-__device__ __forceinline__ uint32_t path_key(const float4 o, const float4 d, const MortonPlan& mp) {
+// spread: mortonSpread's table (device memory).
+__device__ __forceinline__ uint32_t path_key(const float4 o, const float4 d, const MortonPlan& mp,
+                                             const uint32_t* spread) {
     const uint32_t m = ((uint32_t)(d.z < 0.0f) << 2) | ((uint32_t)(d.x < 0.0f) << 1) | (uint32_t)(d.y < 0.0f);
     const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
     const float inv = 3.999f / fmaxf(fmaxf(ax, ay), fmaxf(az, 1e-30f));
     const uint32_t dq = ((uint32_t)(ax * inv) << 4) | ((uint32_t)(ay * inv) << 2) | (uint32_t)(az * inv);
-    const uint32_t q[3] = {key_quant(o.x, mp.lo[0], mp.scale[0], mp.bits[0]),
-                           key_quant(o.y, mp.lo[1], mp.scale[1], mp.bits[1]),
-                           key_quant(o.z, mp.lo[2], mp.scale[2], mp.bits[2])};
-    int rem[3] = {mp.bits[0], mp.bits[1], mp.bits[2]};
+    const float oa[3] = {o.x, o.y, o.z};
     uint32_t code = 0;
 #pragma unroll
-    for (int i = 0; i < kMortonBits; ++i) {
-        const int a = (int)(((i < 16 ? mp.axis_lo >> (2 * i) : mp.axis_hi >> (2 * (i - 16)))) & 3u);
-        const int r = a == 0 ? --rem[0] : (a == 1 ? --rem[1] : --rem[2]);
-        const uint32_t qa = a == 0 ? q[0] : (a == 1 ? q[1] : q[2]);
-        code = (code << 1) | ((qa >> r) & 1u);
+    for (int a = 0; a < 3; ++a) {
+        const uint32_t q = key_quant(oa[a], mp.lo[a], mp.scale[a], mp.bits[a]);  // < 2^21
+        const uint32_t* t = spread + a * 768;
+        code |= t[q & 255u] | t[256 + ((q >> 8) & 255u)] | t[512 + (q >> 16)];
     }
     return (m << (6 + kMortonBits)) | (code << 6) | dq;
 }
