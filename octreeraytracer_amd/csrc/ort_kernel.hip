@@ -54,6 +54,7 @@ struct PipeArgs {
     int exact_only;   // ORT_OPT_EXACT_TRAVERSAL: every compact ray takes the exact walk
     int refill;       // persistent trace: refill a wave when at least this many lanes idle
     int rays_stored;  // bounce-0 rays were written by ort_raygen_kernel (persistent pipeline)
+    int final_out;    // a path that ends in the last sample writes its final pixel (no finalize pass)
     const uint8_t* lut;  // global copy of the rank LUT (ort::rank_lut_entry), 8 x 256 bytes
     const int* qlist;    // bounce >= 1: the alive path slots (compacted, increasing), or null = all
     const int* qcount;   // their number (device)
@@ -441,7 +442,13 @@ __device__ __forceinline__ bool shade_state(const PipeArgs& A, int k, size_t p, 
                 acc = ort::mk(a.x, a.y, a.z);
             }
             acc = ort::add(acc, c);
-            A.pcol[k] = make_float4(acc.x, acc.y, acc.z, 0.0f);
+            if (A.final_out && A.sample == A.pp.ns - 1) {  // ort_finalize_kernel's work for this pixel
+                const ort::V3 v = ort::finish_pixel(acc, A.pp.ns);
+                float* o = A.out + 3 * p;
+                o[0] = v.x; o[1] = v.y; o[2] = v.z;
+            } else {
+                A.pcol[k] = make_float4(acc.x, acc.y, acc.z, 0.0f);
+            }
             A.pd[k] = make_float4(ray.d.x, ray.d.y, ray.d.z, 0.0f);
         } else {
             A.po[k] = make_float4(ray.o.x, ray.o.y, ray.o.z, importance);
@@ -492,7 +499,10 @@ __device__ __forceinline__ bool trace_slot(PipeArgs& A, LdsView& L, int k, ort::
     const ort::Ray ray = slot_ray<PRIMARY, true>(A, k, alive, FUSE ? &rng0 : nullptr);
     if (!alive) {
         if (FUSE == 1) shade_direct_padding(A, k);
-        if (FUSE == 2) A.pd[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // never alive (ort_shade_kernel's hole)
+        if (FUSE == 2) {
+            A.pd[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // never alive (ort_shade_kernel's hole)
+            if (A.final_out && A.sample == A.pp.ns - 1) shade_direct_padding(A, k);  // band padding rows
+        }
         return false;
     }
     const ort::V3 inv = ort::mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
@@ -525,7 +535,9 @@ __device__ __forceinline__ bool trace_slot(PipeArgs& A, LdsView& L, int k, ort::
         if constexpr (FUSE == 1) {
             shade_direct<true>(A2, k2, walked, rng0, hit, entry, t);
         } else {
-            return shade_state<0, true, false>(A2, k2, 0, walked, rng0, hit ? entry : -1, t);
+            int col, row;
+            (void)slot_coords<true>(A2, k2, col, row);
+            return shade_state<0, true, false>(A2, k2, (size_t)row * A2.tm.tw + col, walked, rng0, hit ? entry : -1, t);
         }
     } else {
         A.hit[k] = make_int2(hit ? entry : -1, __float_as_int(t));
@@ -867,7 +879,9 @@ __global__ void __launch_bounds__(kBlock) ort_trace_exact(PipeArgs A) {
         if (FUSE == 1) {
             shade_direct(A, k, ray, rng, st == ORT_TRACE_HIT, entry, t);
         } else if (FUSE == 2) {  // bounce 0 shaded here; the rare deferred path joins the list alone
-            if (shade_state<0, true, false>(A, k, 0, ray, rng, st == ORT_TRACE_HIT ? entry : -1, t)) {
+            int col, row;
+            (void)slot_coords(A, k, col, row);
+            if (shade_state<0, true, false>(A, k, (size_t)row * A.tm.tw + col, ray, rng, st == ORT_TRACE_HIT ? entry : -1, t)) {
                 const int pos = atomicAdd(A.qnext_count, 1);
                 A.qnext[pos] = k;
                 if (A.qnext_keys) A.qnext_keys[pos] = ort::path_key(A.po[k], A.pd[k], A.mp, A.key_spread);
@@ -1476,6 +1490,9 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     a.wclock = (ulonglong4*)ctx->wclock;
     a.wclock_n = (int)ctx->wclock_n;
     a.mp = ort::mortonPlan(ctx->root_lo, ctx->root_hi);
+    // with bounce 0 shaded in the trace kernels every pixel's path ends in a kernel that knows
+    // its pixel, so the last sample writes the final pixels itself (no finalize pass)
+    a.final_out = fuse_first ? 1 : 0;
     a.key_spread = (const uint32_t*)ctx->key_spread.p;
     const size_t lds = lds_bytes(mode, ctx->depth, false);
     const size_t lds_exact = lds_bytes(mode, ctx->depth, true);
@@ -1586,7 +1603,7 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
         }
     }
     if (ctx->tseg[fslot] > 0) ctx->frames += 1;
-    if (!direct) {
+    if (!direct && !a.final_out) {
         hipLaunchKernelGGL(ort_finalize_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, s, a);
         if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "ort_finalize_kernel launch");
     }

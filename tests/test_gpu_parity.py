@@ -210,6 +210,21 @@ def test_bounce_orders_and_skip_identical(ort, oracle, renderer, depth, mspn, so
         renderer.set_kid_skip(1)
 
 
+@pytest.mark.parametrize("ns", [1, 2])
+def test_band_padding_rows_with_bounces(ort, oracle, renderer, scene_c2, ns):
+    """Band tiles whose rows run past the frame (the multi-GPU partition's padding) in the
+    multi-bounce pipeline, where the last shading writes the final pixels itself: the padding
+    rows come back as zeros and every other pixel as the oracle's."""
+    s, t = scene_c2
+    renderer.upload(s, t)
+    p = ort.FrameParams.default_camera(320, 180, num_samples=ns, max_depth=4)
+    tile = ort.Tile(0, 320, 150, 64, 16, 64)  # rows y = 150 + 64 (j / 16) + j % 16: most past 180
+    got = renderer.render(p, tile)
+    ref = oracle.render(s, t, p, 0, 150, 320, 64, band_height=16, band_stride=64)
+    assert_same(got, ref, f"band padding ns={ns}")
+    assert float(np.abs(got[16:]).max()) == 0.0  # rows past the frame
+
+
 @pytest.fixture(scope="module")
 def scene_c3(ort):
     s = ort.random_spheres(100_000, 42)
