@@ -898,7 +898,6 @@ __global__ void __launch_bounds__(kBlock) ort_trace_exact(PipeArgs A) {
 // to the next bounce.
 template <int MODE, bool FIRST, bool DIRECT>
 __device__ __forceinline__ bool shade_slot(const PipeArgs& A, int k) {
-    if (!FIRST && !list_slot(A, k)) return false;
     int col, row;
     const bool in_tile = FIRST ? slot_coords<true>(A, k, col, row) : slot_coords(A, k, col, row);
     const int y = in_tile ? tile_row_to_y(A.tm, row) : 0;
@@ -940,8 +939,15 @@ __device__ __forceinline__ bool shade_slot(const PipeArgs& A, int k) {
 // are appended to the next bounce's list (the compaction, without a separate select pass).
 template <int MODE, bool FIRST, bool DIRECT>
 __global__ void __launch_bounds__(kBlock) ort_shade_kernel(PipeArgs A) {
-    const int k = blockIdx.x * kBlock + threadIdx.x;
-    const bool go = shade_slot<MODE, FIRST, DIRECT>(A, k);
+    int k = blockIdx.x * kBlock + threadIdx.x;
+    bool in = true;
+    if (!FIRST && A.qlist) {  // the bounce's alive paths in append order (not the sorted trace list)
+        const int n = *A.qcount;
+        if ((int)(blockIdx.x * kBlock) >= n) return;  // whole workgroup past the list
+        in = k < n;
+        if (in) k = A.qlist[k];
+    }
+    const bool go = in && shade_slot<MODE, FIRST, DIRECT>(A, k);
     if (!DIRECT && A.qnext) {
         uint32_t key = 0;
         if (go && A.qnext_keys) key = ort::path_key(A.po[k], A.pd[k], A.mp, A.key_spread);  // the state just stored
@@ -1021,7 +1027,7 @@ struct ort_ctx {
     DevBuf scratch_out, counters;
     // wavefront pipeline state, sized for the largest tile rendered so far
     DevBuf hit, defer_list, defer_count, po, pd, pc, prng, pcol;
-    DevBuf qlist, qcount, qtemp;  // bounce >= 1 path compaction
+    DevBuf qlist, qlist2, qcount, qtemp;  // bounce >= 1 path compaction (two lists: read one, append the other)
     DevBuf skeys, skeys2, svals;  // coherence sort
     DevBuf key_spread;            // its origin-code tables for the scene's root box (path_key.h)
     float spread_box[6] = {0, 0, 0, 0, 0, 0};  // the root box key_spread was built for
@@ -1443,7 +1449,8 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     size_t qtemp_bytes = 0;
     if (compact) {
         qtemp_bytes = (sorted || listsort) ? ort::sortAliveTempBytes((int)slots) : 0;
-        if ((rc = ensure(ctx, ctx->qlist, 4 * slots)) || (rc = ensure(ctx, ctx->qcount, 64)) ||
+        if ((rc = ensure(ctx, ctx->qlist, 4 * slots)) || (rc = ensure(ctx, ctx->qlist2, 4 * slots)) ||
+            (rc = ensure(ctx, ctx->qcount, 64)) ||
             (rc = ensure(ctx, ctx->qtemp, std::max<size_t>(qtemp_bytes, 16))))
             return rc;
         if (sorted && ((rc = ensure(ctx, ctx->skeys, 4 * slots)) || (rc = ensure(ctx, ctx->skeys2, 4 * slots)) ||
@@ -1509,6 +1516,11 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
         a.rays_stored = pers_all && pblocks > 0;
         a.qlist = nullptr;  // bounce 0: every slot
         a.qcount = nullptr;
+        // the alive paths of the current bounce in append order, and the buffer the next
+        // bounce's are appended to: qbuf[cur] / qcnt[cur] and qbuf[cur ^ 1] / qcnt[cur ^ 1]
+        int* qbuf[2] = {(int*)ctx->qlist.p, (int*)ctx->qlist2.p};
+        int* qcnt[2] = {(int*)ctx->qcount.p, (int*)ctx->qcount.p + 4};
+        int cur = 1;  // bounce 0 appends to qbuf[0]
         if (a.rays_stored) {  // the persistent kernel refills lanes from stored rays
             hipLaunchKernelGGL(ort_raygen_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, s, a);
             if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "ort_raygen_kernel launch");
@@ -1532,9 +1544,9 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                 const int pb = (pers_all || (pers_bounce && b > 0)) ? pblocks : 0;
                 PipeArgs at = a;
                 if (fmode == 2) {  // the trace kernels append bounce 1's list (as ort_shade_kernel would)
-                    HIPCHK(ctx, hipMemsetAsync(ctx->qcount.p, 0, sizeof(int), s));
-                    at.qnext = (int*)ctx->qlist.p;
-                    at.qnext_count = (int*)ctx->qcount.p;
+                    HIPCHK(ctx, hipMemsetAsync(qcnt[cur ^ 1], 0, sizeof(int), s));
+                    at.qnext = qbuf[cur ^ 1];
+                    at.qnext_count = qcnt[cur ^ 1];
                     at.qnext_keys = listsort ? (uint32_t*)ctx->skeys.p : nullptr;
                 }
                 e = dcounters ? launch_trace<true>(mode, prim, at, (int)blocks, pb, lds, s, ctx->packet != 0, fmode, qblocks)
@@ -1558,19 +1570,23 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                 }
             }
             if (!fuse && fmode != 2) {
-                // every slot in slot order (a dead path returns after reading its pd.w), not the
-                // trace's compacted list: the sorted list scatters the path-state reads and
-                // writes; in slot order they coalesce (C5 frame 65.4 -> 63.0 ms, A/B)
+                // bounce >= 1: the bounce's alive paths in APPEND order (about slot order: the
+                // path-state reads and writes coalesce; the sorted trace list scattered them, C5
+                // 65.4 -> 63.0 ms) -- or, with the every-slot sort (sort_paths 1), every slot
                 PipeArgs a2 = a;
                 a2.qlist = nullptr;
                 a2.qcount = nullptr;
+                if (compact && !sorted && b > 0) {
+                    a2.qlist = qbuf[cur];
+                    a2.qcount = qcnt[cur];
+                }
                 if (compact && !sorted && !a.nobounce && b + 1 < bounces) {
                     // the compaction: the shade kernel appends the paths that go on, one atomic
                     // per workgroup (a separate rocprim::select pass over the slots cost 0.55 ms
-                    // per C5 bounce); this bounce's list has been read by now
-                    HIPCHK(ctx, hipMemsetAsync(ctx->qcount.p, 0, sizeof(int), s));
-                    a2.qnext = (int*)ctx->qlist.p;
-                    a2.qnext_count = (int*)ctx->qcount.p;
+                    // per C5 bounce), into the other list buffer
+                    HIPCHK(ctx, hipMemsetAsync(qcnt[cur ^ 1], 0, sizeof(int), s));
+                    a2.qnext = qbuf[cur ^ 1];
+                    a2.qnext_count = qcnt[cur ^ 1];
                     a2.qnext_keys = listsort ? (uint32_t*)ctx->skeys.p : nullptr;
                 }
                 e = launch_shade(mode, b == 0, direct, a2, (int)blocks, s);
@@ -1585,20 +1601,26 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                                        (int*)ctx->qcount.p, s);
                     if (e != hipSuccess) return hip_fail(ctx, e, "path compaction");
                 }  // else the shade kernel appended them
-                if (listsort) {
-                    // the list's length, read back (one host wait per bounce): the sort then
-                    // costs the alive paths only, not every slot (C5: 36.6 M keys, not 99.6 M)
-                    int n_alive = 0;
-                    HIPCHK(ctx, hipMemcpyAsync(&n_alive, ctx->qcount.p, sizeof(int), hipMemcpyDeviceToHost, s));
-                    HIPCHK(ctx, hipStreamSynchronize(s));
-                    // (key, path) pairs as the shade / trace kernels appended them
-                    const ort::SortBuffers sb{(uint32_t*)ctx->skeys.p, (uint32_t*)ctx->skeys2.p, (int*)ctx->qlist.p,
-                                              (int*)ctx->svals.p};
-                    e = ort::sortList(ctx->qtemp.p, qtemp_bytes, n_alive, sb, s);
-                    if (e != hipSuccess) return hip_fail(ctx, e, "path list sort");
+                if (sorted) {
+                    a.qlist = (const int*)ctx->qlist.p;
+                    a.qcount = (const int*)ctx->qcount.p;
+                } else {
+                    cur ^= 1;  // the list just appended is the next bounce's
+                    if (listsort) {
+                        // the list's length, read back (one host wait per bounce): the sort then
+                        // costs the alive paths only, not every slot (C5: 36.6 M keys, not 99.6 M)
+                        int n_alive = 0;
+                        HIPCHK(ctx, hipMemcpyAsync(&n_alive, qcnt[cur], sizeof(int), hipMemcpyDeviceToHost, s));
+                        HIPCHK(ctx, hipStreamSynchronize(s));
+                        // (key, path) pairs as the shade / trace kernels appended them
+                        const ort::SortBuffers sb{(uint32_t*)ctx->skeys.p, (uint32_t*)ctx->skeys2.p, qbuf[cur],
+                                                  (int*)ctx->svals.p};
+                        e = ort::sortList(ctx->qtemp.p, qtemp_bytes, n_alive, sb, s);
+                        if (e != hipSuccess) return hip_fail(ctx, e, "path list sort");
+                    }
+                    a.qlist = listsort ? (const int*)ctx->svals.p : qbuf[cur];
+                    a.qcount = qcnt[cur];
                 }
-                a.qlist = (const int*)(listsort ? ctx->svals.p : ctx->qlist.p);
-                a.qcount = (const int*)ctx->qcount.p;
             }
         }
     }
@@ -1672,7 +1694,7 @@ int ort_destroy(ort_ctx* ctx) {
     free_buf(ctx->counters);
     free_buf(ctx->lut);
     DevBuf* pipe[] = {&ctx->hit, &ctx->defer_list, &ctx->defer_count, &ctx->po, &ctx->pd, &ctx->pc, &ctx->prng, &ctx->pcol,
-                      &ctx->qlist, &ctx->qcount, &ctx->qtemp, &ctx->skeys, &ctx->skeys2, &ctx->svals, &ctx->key_spread};
+                      &ctx->qlist, &ctx->qlist2, &ctx->qcount, &ctx->qtemp, &ctx->skeys, &ctx->skeys2, &ctx->svals, &ctx->key_spread};
     for (DevBuf* b : pipe) free_buf(*b);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
