@@ -85,12 +85,19 @@ __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t
 
 constexpr size_t kRankLutBytes = 8 * 256;  // ort::rank_lut_entry table
 
+// The persistent bounce kernel at depth 9-10 (Masks96Lean with ORT_REV_BOUNCE): 512-thread
+// workgroups over the reversed-table image (fast_rev_planes: 32.8 KB at depth 10, the rank
+// LUT in its gap), 53.3 KB of LDS with 512 lanes' frames -- 3 workgroups = 6 waves/SIMD.
+constexpr bool kRevBounce = ORT_REV_BOUNCE;
+constexpr int kPersistDeepBlock = kRevBounce ? 512 : kBlock;
+
 // with_tm: the exact walk also keeps a per-level tmin column; the fast walk needs none.
-size_t lds_bytes(int mode, int depth, bool with_tm) {
+// rev / nb: the image layout and workgroup size (the deep persistent kernel's: true, 512).
+size_t lds_bytes(int mode, int depth, bool with_tm, bool rev = false, int nb = kBlock) {
     if (mode != 0) return 0;
-    const size_t planes = align16(sizeof(float) * (size_t)ort::fast_plane_floats(depth));  // + reversed copies
+    const ort::LdsLayout l = ort::lds_layout(depth, rev || ort::fast_rev_planes(depth));
     const size_t levels = (size_t)std::max(depth, 1);
-    return planes + kRankLutBytes + (with_tm ? 2 : 1) * levels * kBlock * sizeof(int);
+    return (size_t)l.frames + (with_tm ? 2 : 1) * levels * (size_t)nb * sizeof(int);
 }
 
 // LDS image of one workgroup: split planes | rank LUT | frame columns (co[, tmin]).
@@ -99,37 +106,40 @@ struct LdsView {
     const uint8_t* lut;
     ort::LdsFrames fr;
 };
-template <bool WITH_LUT>
-__device__ inline LdsView lds_view(unsigned char* smem, int D) {
-    const int np = ort::fast_plane_floats(D);
-    const size_t poff = align16(sizeof(float) * (size_t)np);
-    const size_t foff = poff + kRankLutBytes;
+template <bool WITH_LUT, int NB = kBlock>
+__device__ inline LdsView lds_view(unsigned char* smem, int D, bool rev = false) {
+    const ort::LdsLayout l = ort::lds_layout(D, rev || ort::fast_rev_planes(D));
     LdsView v;
     v.planes = reinterpret_cast<float*>(smem);
-    v.lut = WITH_LUT ? smem + poff : nullptr;
-    v.fr.co = reinterpret_cast<int*>(smem + foff);
-    v.fr.tm = reinterpret_cast<float*>(smem + foff + (size_t)(D > 0 ? D : 1) * kBlock * sizeof(int));
-    v.fr.stride = kBlock;
+    v.lut = WITH_LUT ? smem + l.lut : nullptr;
+    v.fr.co = reinterpret_cast<int*>(smem + l.frames);
+    v.fr.tm = reinterpret_cast<float*>(smem + l.frames + (size_t)(D > 0 ? D : 1) * NB * sizeof(int));
+    v.fr.stride = NB;
     v.fr.lane = threadIdx.x;
     return v;
 }
 // The plane tables and rank LUT are the same for every workgroup of a scene: k_lds_image
-// builds them once per scene (ort_ctx::lds_img) and each workgroup copies the image in
-// 16-byte pieces -- building them per workgroup (an integer division per plane entry, ~80
-// VALU per LUT byte) cost as much VALU as several walk steps of every wave.
-__global__ void __launch_bounds__(kBlock) k_lds_image(const float* planes, int D, unsigned char* img) {
+// builds them once per scene (ort_ctx::lds_img; at depth 9-10 also the reversed-table image
+// ort_ctx::lds_rev) and each workgroup copies the image in 16-byte pieces -- building them
+// per workgroup (an integer division per plane entry, ~80 VALU per LUT byte) cost as much
+// VALU as several walk steps of every wave.
+__global__ void __launch_bounds__(kBlock) k_lds_image(const float* planes, int D, bool rev, unsigned char* img) {
     const int tid = threadIdx.x;
-    ort::fill_fast_planes(planes, reinterpret_cast<float*>(img), D, tid, kBlock);  // forward, then reversed
-    uint8_t* lut = img + align16(sizeof(float) * (size_t)ort::fast_plane_floats(D));
+    rev = rev || ort::fast_rev_planes(D);
+    ort::fill_fast_planes(planes, reinterpret_cast<float*>(img), D, rev, tid, kBlock);  // forward, then reversed
+    __syncthreads();  // the LUT may sit in a gap of the tables (lds_layout)
+    uint8_t* lut = img + ort::lds_layout(D, rev).lut;
     for (int i = tid; i < (int)kRankLutBytes; i += kBlock) lut[i] = ort::rank_lut_entry((uint32_t)i >> 8, (uint32_t)i & 255u);
 }
-template <bool WITH_LUT>
+// REV: the reversed-table image of a depth 9-10 tree (S.lds_rev), for NB-thread workgroups.
+template <bool WITH_LUT, int NB = kBlock, bool REV = false>
 __device__ inline LdsView setup_lds(unsigned char* smem, const ort::KScene& S) {
-    const int n16 = WITH_LUT ? S.lds_img_n16 : S.lds_img_p16;
+    const int n16 = REV ? S.lds_rev_n16 : (WITH_LUT ? S.lds_img_n16 : S.lds_img_p16);
+    const uint4* src = REV ? S.lds_rev : S.lds_img;
     uint4* dst = reinterpret_cast<uint4*>(smem);
-    for (int i = threadIdx.x; i < n16; i += kBlock) dst[i] = S.lds_img[i];
+    for (int i = threadIdx.x; i < n16; i += NB) dst[i] = src[i];
     __syncthreads();
-    return lds_view<WITH_LUT>(smem, S.depth);
+    return lds_view<WITH_LUT, NB>(smem, S.depth, REV);
 }
 
 // Tile (bx, by) of 16x16 pixels rendered by workgroup blk.  The dispatcher deals workgroup b
@@ -275,9 +285,12 @@ constexpr int kChunk = ORT_CHUNK;
 // DEEP: trees deeper than 8 levels (96-bit masks, lean state); depth <= 8 takes the
 // primary-ray walk's 64-bit masks and reversed plane tables (71 VGPRs, 7 waves/SIMD).
 template <bool COUNT, bool DEEP>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ORT_PERSISTENT_WAVES))) ort_trace_persistent(PipeArgs A) {
-    extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];  // plane tables: 1 KiB-aligned
-    LdsView L = setup_lds<true>(smem, A.S);
+__global__ void __launch_bounds__(DEEP ? kPersistDeepBlock : kBlock) __attribute__((amdgpu_waves_per_eu(ORT_PERSISTENT_WAVES)))
+ort_trace_persistent(PipeArgs A) {
+    // plane tables at 4T-byte-aligned absolute LDS addresses (fast_rev_planes; no static LDS here)
+    extern __shared__ __attribute__((aligned(4096))) unsigned char smem[];
+    constexpr bool REV = DEEP && kRevBounce;
+    LdsView L = setup_lds<true, DEEP ? kPersistDeepBlock : kBlock, REV>(smem, A.S);
     const uint8_t* lut = L.lut;
     const int lane = threadIdx.x & 63;
     const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -1023,6 +1036,7 @@ struct ort_ctx {
     DevBuf sph_cr, sph_ma, sph_fr;
     DevBuf node, leaf_sph, leaf_idx, planes, kid;  // compact
     DevBuf lds_img;                              // compact: the workgroup LDS image (k_lds_image)
+    DevBuf lds_rev;                              // ... depth 9-10: the reversed-table image (persistent kernel)
     DevBuf nodeA, nodeB, cnt, indices;           // explicit
     DevBuf scratch_out, counters;
     // wavefront pipeline state, sized for the largest tile rendered so far
@@ -1060,7 +1074,7 @@ void free_buf(DevBuf& b) {
 
 void free_scene(ort_ctx* c) {
     DevBuf* all[] = {&c->sph_cr, &c->sph_ma, &c->sph_fr, &c->node, &c->kid, &c->leaf_sph, &c->leaf_idx,
-                     &c->planes, &c->lds_img, &c->nodeA, &c->nodeB, &c->cnt, &c->indices};
+                     &c->planes, &c->lds_img, &c->lds_rev, &c->nodeA, &c->nodeB, &c->cnt, &c->indices};
     for (DevBuf* b : all) free_buf(*b);
     ort::freeGpuTree(c->tree);
     c->has_scene = false;
@@ -1077,12 +1091,16 @@ int upload(ort_ctx* ctx, DevBuf& b, const void* src, size_t bytes) {
 
 // The compact layout's workgroup LDS image (plane tables | rank LUT) from ctx->planes.
 int build_lds_image(ort_ctx* ctx) {
-    const size_t bytes = align16(sizeof(float) * (size_t)ort::fast_plane_floats(ctx->depth)) + kRankLutBytes;
-    int rc;
-    if ((rc = upload(ctx, ctx->lds_img, nullptr, bytes))) return rc;
-    hipLaunchKernelGGL(k_lds_image, dim3(1), dim3(kBlock), 0, ctx->stream, (const float*)ctx->planes.p, ctx->depth,
-                       (unsigned char*)ctx->lds_img.p);
-    HIPCHK(ctx, hipGetLastError());
+    for (int rev = 0; rev < 2; ++rev) {
+        if (rev && !(kRevBounce && ctx->depth > 8)) break;
+        DevBuf& img = rev ? ctx->lds_rev : ctx->lds_img;
+        const size_t bytes = (size_t)ort::lds_layout(ctx->depth, rev || ort::fast_rev_planes(ctx->depth)).frames;
+        int rc;
+        if ((rc = upload(ctx, img, nullptr, bytes))) return rc;
+        hipLaunchKernelGGL(k_lds_image, dim3(1), dim3(kBlock), 0, ctx->stream, (const float*)ctx->planes.p, ctx->depth,
+                           rev != 0, (unsigned char*)img.p);
+        HIPCHK(ctx, hipGetLastError());
+    }
     return ORT_OK;
 }
 
@@ -1263,7 +1281,9 @@ ort::KScene device_scene(const ort_ctx* c) {
     S.planes = (const float*)c->planes.p;
     S.lds_img = (const uint4*)c->lds_img.p;
     S.lds_img_p16 = (int)(align16(sizeof(float) * (size_t)ort::fast_plane_floats(c->depth)) / 16);
-    S.lds_img_n16 = S.lds_img_p16 + (int)(kRankLutBytes / 16);
+    S.lds_img_n16 = ort::lds_layout(c->depth, ort::fast_rev_planes(c->depth)).frames / 16;
+    S.lds_rev = (const uint4*)c->lds_rev.p;
+    S.lds_rev_n16 = ort::lds_layout(c->depth, true).frames / 16;
     S.depth = c->depth;
     S.nodeA = (const float4*)c->nodeA.p;
     S.nodeB = (const float4*)c->nodeB.p;
@@ -1319,7 +1339,9 @@ template <bool COUNT, bool PRIMARY>
 hipError_t launch_trace_p(int mode, const PipeArgs& a, int blocks, int pblocks, size_t lds, hipStream_t s, bool packet,
                           int fuse, int qblocks) {
     if (mode == 0 && pblocks > 0) {
-        if (a.S.depth > 8) hipLaunchKernelGGL((ort_trace_persistent<COUNT, true>), dim3(pblocks), dim3(kBlock), lds, s, a);
+        if (a.S.depth > 8)
+            hipLaunchKernelGGL((ort_trace_persistent<COUNT, true>), dim3(pblocks), dim3(kPersistDeepBlock),
+                               lds_bytes(0, a.S.depth, false, kRevBounce, kPersistDeepBlock), s, a);
         else hipLaunchKernelGGL((ort_trace_persistent<COUNT, false>), dim3(pblocks), dim3(kBlock), lds, s, a);
     }
     else if (mode == 0 && qblocks > 0 && !(PRIMARY && packet)) {
@@ -1390,14 +1412,15 @@ int queue_blocks(ort_ctx* ctx, bool count, size_t lds, long long needed) {
 
 // Resident workgroups of the persistent trace kernel (a plain launch: extra groups just
 // start when others finish; no grid-wide synchronisation depends on residency).
-int persistent_blocks(int device, bool count, bool deep, size_t lds, long long needed) {
+int persistent_blocks(int device, bool count, bool deep, int depth, size_t lds, long long needed) {
     int per_cu = 0, cus = 0;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+    const size_t dlds = lds_bytes(0, depth, false, kRevBounce, kPersistDeepBlock);
     if (count)
-        (void)(deep ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ort_trace_persistent<true, true>, kBlock, lds)
+        (void)(deep ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ort_trace_persistent<true, true>, kPersistDeepBlock, dlds)
                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ort_trace_persistent<true, false>, kBlock, lds));
     else
-        (void)(deep ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ort_trace_persistent<false, true>, kBlock, lds)
+        (void)(deep ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ort_trace_persistent<false, true>, kPersistDeepBlock, dlds)
                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ort_trace_persistent<false, false>, kBlock, lds));
     long long b = (long long)std::max(per_cu, 1) * std::max(cus, 1);
     return (int)std::max(1LL, std::min(b, needed));
@@ -1503,7 +1526,7 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     a.key_spread = (const uint32_t*)ctx->key_spread.p;
     const size_t lds = lds_bytes(mode, ctx->depth, false);
     const size_t lds_exact = lds_bytes(mode, ctx->depth, true);
-    const int pblocks = (mode == 0 && ctx->persistent) ? persistent_blocks(ctx->device, dcounters != nullptr, ctx->depth > 8, lds, blocks) : 0;
+    const int pblocks = (mode == 0 && ctx->persistent) ? persistent_blocks(ctx->device, dcounters != nullptr, ctx->depth > 8, ctx->depth, lds, blocks) : 0;
     const int exact_blocks = 1024;
     // wave queue: as many workgroups as are resident (never more than the frame has)
     const int qblocks = (mode == 0 && ctx->wave_queue) ? queue_blocks(ctx, dcounters != nullptr, lds, blocks) : 0;
@@ -1805,7 +1828,7 @@ int ort_scene_get_info(const ort_ctx* ctx, ort_scene_info* info) {
     info->layout = ctx->layout;
     info->tree_depth = ctx->depth;
     const DevBuf* all[] = {&ctx->sph_cr, &ctx->sph_ma, &ctx->sph_fr, &ctx->node, &ctx->kid, &ctx->leaf_sph, &ctx->leaf_idx,
-                           &ctx->planes, &ctx->lds_img, &ctx->nodeA, &ctx->nodeB, &ctx->cnt, &ctx->indices};
+                           &ctx->planes, &ctx->lds_img, &ctx->lds_rev, &ctx->nodeA, &ctx->nodeB, &ctx->cnt, &ctx->indices};
     int64_t b = 0;
     for (const DevBuf* d : all) b += (int64_t)d->bytes;
     info->device_bytes = b;
@@ -1960,6 +1983,7 @@ int ort_debug_emulate_render(const float* cr, const float* ma, const float* fr, 
         S.n_nodes = n_nodes;
         ort::CompactLayout cl;
         std::vector<float> fplanes;  // fast-walk plane tables (forward + reversed)
+        std::vector<float> fplanes_b;  // ... of the bounce walk (Masks96Lean's reversed tables at depth 9-10)
         std::vector<float> A, B;
         int mode = 2;
         if (p->use_octree == 1) {
@@ -1978,6 +2002,9 @@ int ort_debug_emulate_render(const float* cr, const float* ma, const float* fr, 
                 S.depth = cl.depth;
                 fplanes.resize(ort::fast_plane_floats(cl.depth));
                 ort::fill_fast_planes(cl.planes.data(), fplanes.data(), cl.depth);
+                const bool rev_b = ort::Masks96Lean::kRevPlanes || ort::fast_rev_planes(cl.depth);
+                fplanes_b.resize(ort::fast_plane_floats(cl.depth, rev_b));
+                ort::fill_fast_planes(cl.planes.data(), fplanes_b.data(), cl.depth, rev_b);
             } else {
                 mode = 1;
                 A.resize(4 * (size_t)n_nodes);
@@ -2018,14 +2045,16 @@ int ort_debug_emulate_render(const float* cr, const float* ma, const float* fr, 
                 // counters from the counting walk (the reference's work, no skip) -- and the two
                 // pixels must agree bit for bit
                 if (mode == 0) {
-                    v = ort::shade_pixel<0, false>(pp, S, fplanes.data(), rank_lut, lf, nullptr, nullptr, t->x0 + c, y, cc);
-                    vc = ort::shade_pixel<0, true>(pp, S, fplanes.data(), rank_lut, lf, nullptr, nullptr, t->x0 + c, y, cc);
+                    v = ort::shade_pixel<0, false>(pp, S, fplanes.data(), fplanes_b.data(), rank_lut, lf, nullptr, nullptr,
+                                                   t->x0 + c, y, cc);
+                    vc = ort::shade_pixel<0, true>(pp, S, fplanes.data(), fplanes_b.data(), rank_lut, lf, nullptr, nullptr,
+                                                   t->x0 + c, y, cc);
                 } else if (mode == 1) {
-                    v = ort::shade_pixel<1, false>(pp, S, nullptr, nullptr, lf, snode.data(), stmin.data(), t->x0 + c, y, cc);
-                    vc = ort::shade_pixel<1, true>(pp, S, nullptr, nullptr, lf, snode.data(), stmin.data(), t->x0 + c, y, cc);
+                    v = ort::shade_pixel<1, false>(pp, S, nullptr, nullptr, nullptr, lf, snode.data(), stmin.data(), t->x0 + c, y, cc);
+                    vc = ort::shade_pixel<1, true>(pp, S, nullptr, nullptr, nullptr, lf, snode.data(), stmin.data(), t->x0 + c, y, cc);
                 } else {
-                    v = ort::shade_pixel<2, false>(pp, S, nullptr, nullptr, lf, nullptr, nullptr, t->x0 + c, y, cc);
-                    vc = ort::shade_pixel<2, true>(pp, S, nullptr, nullptr, lf, nullptr, nullptr, t->x0 + c, y, cc);
+                    v = ort::shade_pixel<2, false>(pp, S, nullptr, nullptr, nullptr, lf, nullptr, nullptr, t->x0 + c, y, cc);
+                    vc = ort::shade_pixel<2, true>(pp, S, nullptr, nullptr, nullptr, lf, nullptr, nullptr, t->x0 + c, y, cc);
                 }
                 if (ort::f2u(v.x) != ort::f2u(vc.x) || ort::f2u(v.y) != ort::f2u(vc.y) || ort::f2u(v.z) != ort::f2u(vc.z))
                     return fail(nullptr, ORT_ERR_INTERNAL, "emulation: production and counting walks differ at pixel (" +

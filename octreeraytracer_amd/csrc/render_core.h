@@ -99,6 +99,8 @@ struct KScene {
     const uint4* lds_img;    // the workgroup LDS image (fast plane tables | rank LUT), built once
     int lds_img_n16;         // per scene; its size in 16-byte chunks (planes part: lds_img_p16)
     int lds_img_p16;
+    const uint4* lds_rev;    // depth 9-10: the reversed-table image (fast_rev_planes), lds_rev_n16 chunks
+    int lds_rev_n16;
     int depth;               // tree depth D (root = 0)
     uint32_t node_bytes;     // buffer sizes for the range-checked buffer loads (< 2^32)
     uint32_t leaf_bytes;
@@ -241,30 +243,60 @@ struct LevelMasks {
     }
 };
 
-// The fast walk's split-plane tables.  Trees of depth <= 8: per axis a a 3 KiB block at
-// byte 3072 a -- the layout's forward table (entry i = plane i) at its start and the same
-// table reversed (entry i = plane 2^D - i) 1 KiB further -- so that a ray walking an axis
-// downwards indexes its planes upwards like every other ray (no per-ray stride), and every
-// table starts at a multiple of 1024 bytes: a node's near plane (index < 256) is then a byte
-// offset whose low 10 bits are the index, and the pop moves it to a child's with one
-// and/or (fast_step).  At depth 8 the forward table's last entry is the reversed one's first
-// (the same plane), and the reversed table's last sits at byte 2048 of the block.  Deeper
-// trees keep the forward tables only, back to back (the reversed copies would cost LDS
-// occupancy), and a +-4 byte stride per axis.
-ORT_FN bool fast_rev_planes(int depth) { return depth <= 8; }
-ORT_FN int fast_axis_floats(int depth) { return fast_rev_planes(depth) ? 768 : (1 << depth) + 1; }
-ORT_FN int fast_plane_floats(int depth) { return 3 * fast_axis_floats(depth); }
-ORT_FN void fill_fast_planes(const float* fwd, float* out, int depth, int i0 = 0, int step = 1) {
+// The fast walk's split-plane tables.  Reversed layout (every kernel at depth <= 8; the
+// persistent bounce kernel at depth 9-10): with T = max(256, 2^D) floats, per axis a block
+// of 3T floats at float 3T a -- the layout's forward table (entry i = plane i) at its start
+// and the same table reversed (entry i = plane 2^D - i) T floats further -- so that a ray
+// walking an axis downwards indexes its planes upwards like every other ray (no per-ray
+// stride), and every table starts at a multiple of 4T bytes: a node's near plane (index < T)
+// is then a byte offset whose low bits are 4 x the index, and the pop moves it to a child's
+// with one and/or (fast_step).  The forward table's last entry is the reversed one's first
+// (the same plane); the last axis block ends with its reversed table (7T + 2^D + 1 floats in
+// all).  Forward layout (the other kernels at depth 9-10, whose LDS holds 256 lanes'
+// frames): the forward tables back to back, 2^D + 1 floats each, and a +-4 byte stride per
+// axis.  The image a workgroup copies into LDS (lds_layout) is the tables, the rank LUT
+// (8 x 256 bytes: in the gap after axis 0's reversed table where it fits, at depth 10) and
+// then the frame columns.
+ORT_FN bool fast_rev_planes(int depth) { return depth <= 8; }  // the default image's layout
+ORT_FN int fast_rev_T(int depth) { return depth <= 8 ? 256 : 1 << depth; }
+ORT_FN int fast_axis_floats(int depth, bool rev) { return rev ? 3 * fast_rev_T(depth) : (1 << depth) + 1; }
+ORT_FN int fast_axis_floats(int depth) { return fast_axis_floats(depth, fast_rev_planes(depth)); }
+ORT_FN int fast_plane_floats(int depth, bool rev) {
+    return rev ? 7 * fast_rev_T(depth) + (1 << depth) + 1 : 3 * fast_axis_floats(depth, false);
+}
+ORT_FN int fast_plane_floats(int depth) { return fast_plane_floats(depth, fast_rev_planes(depth)); }
+struct LdsLayout {
+    int lut;     // byte offset of the rank LUT
+    int frames;  // byte offset of the frame columns (= the image's size; a multiple of 16)
+};
+ORT_FN LdsLayout lds_layout(int depth, bool rev) {
+    const int pb = (4 * fast_plane_floats(depth, rev) + 15) & ~15;
+    const int T = fast_rev_T(depth);
+    LdsLayout l;
+    if (rev && 4 * (2 * T - (1 << depth) - 1) >= 2048) {  // the gap after axis 0's reversed table
+        l.lut = 12 * T - 2048;
+        l.frames = pb;
+    } else {
+        l.lut = pb;
+        l.frames = pb + 2048;
+    }
+    return l;
+}
+ORT_FN void fill_fast_planes(const float* fwd, float* out, int depth, bool rev, int i0 = 0, int step = 1) {
     const int P1 = (1 << depth) + 1;
-    const int S = fast_axis_floats(depth);
-    const bool rev = fast_rev_planes(depth);
-    for (int o = i0; o < 3 * S; o += step) {  // gather form: one writer per entry
+    const int S = fast_axis_floats(depth, rev);
+    const int T = fast_rev_T(depth);
+    const int n = fast_plane_floats(depth, rev);
+    for (int o = i0; o < n; o += step) {  // gather form: one writer per entry
         const int a = o / S, r = o - a * S;
-        float v = 0.0f;  // the gaps: never read
+        float v = 0.0f;  // the gaps: never read as planes
         if (r < P1) v = fwd[a * P1 + r];
-        else if (rev && r >= 256 && r - 256 < P1) v = fwd[a * P1 + (P1 - 1 - (r - 256))];
+        else if (rev && r >= T && r - T < P1) v = fwd[a * P1 + (P1 - 1 - (r - T))];
         out[o] = v;
     }
+}
+ORT_FN void fill_fast_planes(const float* fwd, float* out, int depth) {
+    fill_fast_planes(fwd, out, depth, fast_rev_planes(depth));
 }
 
 // Child-box entry t of octant `oct` for a node at depth `dep` with cell (cx,cy,cz):
@@ -664,8 +696,8 @@ struct FastStateT {
     V3 d;            // original-axis direction (Sphere_hit)
     float ya;        // RN(1 / dot(d, d))
     float oA, oB, oC, iA, iB, iC;  // role-axis origin / 1/d
-    // kRevPlanes (depth <= 8): byte offsets from pl0 of the current node's near plane per role
-    // axis (table start, a multiple of 1024, + 4 * index; see fast_axis_floats)
+    // kRevPlanes: byte offsets from pl0 of the current node's near plane per role axis (table
+    // start, a multiple of 4T bytes, + 4 * index; see fast_rev_planes)
     const float* pl0;
     uint32_t aA, aB, aC;
     uint32_t h4;      // half the current node's width, in bytes of plane table (4 * 2^(D-1-depth))
@@ -735,6 +767,12 @@ struct Masks96Lean : Masks96 {
 #endif
     static constexpr bool kLeadLeaves = ORT_LEAD_LEAVES_PERSISTENT;
     static constexpr bool kKidSkip = true;
+    // the reversed plane tables (fast_rev_planes) at depth 9-10 too: the persistent kernel
+    // runs 512-thread workgroups, whose LDS holds them at 6 waves/SIMD
+#ifndef ORT_REV_BOUNCE
+#define ORT_REV_BOUNCE 1
+#endif
+    static constexpr bool kRevPlanes = ORT_REV_BOUNCE;
 };
 // Depth <= 8 walk without the inline leaf children: the persistent bounce kernel's walk
 // (inline leaves pay off on coherent camera rays, not on scattered bounce rays).
@@ -764,12 +802,13 @@ ORT_FN bool fast_begin(const KScene& S, const float* planes, const uint8_t* rank
     // nibble k = rank_perm(k, m): the identity (or, swap, bits 0/1 exchanged) XOR m per nibble
     st.otab = (swap ? 0x75643120u : 0x76543210u) ^ (m * 0x11111111u);
     // planes: fast_plane_floats(D) floats (fill_fast_planes)
-    if (Masks::kRevPlanes) {  // per axis: forward table, reversed one 1 KiB further
+    if (Masks::kRevPlanes) {  // per axis: forward table, reversed one T floats further
         st.pl0 = planes;
-        const uint32_t b0 = FastStateT<Masks>::table_base(planes);  // 1 KiB-aligned (ort_kernel.hip)
-        st.aA = b0 + 4u * ((swap ? 768u : 0u) + (gA ? 256u : 0u));
-        st.aB = b0 + 4u * ((swap ? 0u : 768u) + (gB ? 256u : 0u));
-        st.aC = b0 + 4u * (1536u + (gC ? 256u : 0u));
+        const uint32_t b0 = FastStateT<Masks>::table_base(planes);  // 4T-byte-aligned (ort_kernel.hip)
+        const uint32_t T = (uint32_t)fast_rev_T(D), S3 = 3u * T;
+        st.aA = b0 + 4u * ((swap ? S3 : 0u) + (gA ? T : 0u));
+        st.aB = b0 + 4u * ((swap ? 0u : S3) + (gB ? T : 0u));
+        st.aC = b0 + 4u * (2u * S3 + (gC ? T : 0u));
         st.h4 = 2u * (uint32_t)top;
         const uint32_t t4 = 4u * (uint32_t)top;
         st.tNA = st.iA * (st.plane(st.aA) - st.oA);
@@ -1010,7 +1049,7 @@ ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks
     st.rec = fetch_node(S, st.node);
     if (Masks::kRevPlanes) {
         // near plane of the level-(L+1) child: the level-L ancestor's (offset bits below 8w
-        // cleared; the table start is a multiple of 1024 > 8w) plus w planes on the axes
+        // cleared; the table start is a multiple of 4T >= 8w bytes) plus w planes on the axes
         // where the child is the far half
         const uint32_t w4 = 4u << (D - 1 - L);
         st.h4 = w4 >> 1;
@@ -1347,10 +1386,12 @@ ORT_FN Ray primary_ray(const PixelParams& P, int px, int py, int s, ort_rng& st)
 // cannot take (some 1/d component not finite) is reported as DEFER instead of walking
 // it exactly here, so the exact walk's registers stay out of the hot kernel.
 // bounce: the ray of a bounce >= 1 -- walked like the GPU's bounce kernel does (Masks64Plain /
-// Masks96Lean: no inline leaf children, the rejected-sphere skip), same result.
+// Masks96Lean: no inline leaf children, the rejected-sphere skip; at depth 9-10 over the plane
+// tables planes_b in the Masks96Lean layout), same result.
 template <int MODE, bool COUNT, class Frames>
 ORT_FN int trace_ray(const KScene& S, const float* planes, const uint8_t* rank_lut, const Ray& r, bool allow_defer,
-                     float& t, int& entry, Frames& fr, int* snode, float* stmin, Counters& cnt, bool bounce = false) {
+                     float& t, int& entry, Frames& fr, int* snode, float* stmin, Counters& cnt, bool bounce = false,
+                     const float* planes_b = nullptr) {
     bool hit;
     entry = -1;
     t = 0.0f;
@@ -1363,7 +1404,7 @@ ORT_FN int trace_ray(const KScene& S, const float* planes, const uint8_t* rank_l
             else if (S.depth <= 8)
                 hit = traverse_fast_t<COUNT, Masks64Plain>(S, planes, rank_lut, r, inv, 0.001f, ORT_MAXFLOAT, entry, t, fr, cnt);
             else
-                hit = traverse_fast_t<COUNT, Masks96Lean>(S, planes, rank_lut, r, inv, 0.001f, ORT_MAXFLOAT, entry, t, fr, cnt);
+                hit = traverse_fast_t<COUNT, Masks96Lean>(S, planes_b, rank_lut, r, inv, 0.001f, ORT_MAXFLOAT, entry, t, fr, cnt);
         } else if (allow_defer) {
             return ORT_TRACE_DEFER;
         } else {
@@ -1441,9 +1482,10 @@ ORT_FN V3 finish_pixel(V3 col, int ns) {
 
 // main() of the fragment shader (glsl:636-664) for pixel (px, py), py = 0 the bottom row,
 // as one sequential chain of the steps above (host emulation).
+// planes_b: the bounce walk's plane tables (trace_ray).
 template <int MODE, bool COUNT, class Frames>
-ORT_FN V3 shade_pixel(const PixelParams& P, const KScene& S, const float* planes, const uint8_t* rank_lut, Frames& fr,
-                      int* snode, float* stmin, int px, int py, Counters& cnt) {
+ORT_FN V3 shade_pixel(const PixelParams& P, const KScene& S, const float* planes, const float* planes_b,
+                      const uint8_t* rank_lut, Frames& fr, int* snode, float* stmin, int px, int py, Counters& cnt) {
     ort_rng st;
     pixel_rng_init(P, px, py, st);
     V3 col = mk(0.0f, 0.0f, 0.0f);
@@ -1455,7 +1497,7 @@ ORT_FN V3 shade_pixel(const PixelParams& P, const KScene& S, const float* planes
             if (importance < 0.01f) break;
             float t;
             int entry;
-            const int tr = trace_ray<MODE, COUNT>(S, planes, rank_lut, ray, false, t, entry, fr, snode, stmin, cnt, b > 0);
+            const int tr = trace_ray<MODE, COUNT>(S, planes, rank_lut, ray, false, t, entry, fr, snode, stmin, cnt, b > 0, planes_b);
             HitRec h;
             if (tr == ORT_TRACE_HIT) h = hit_record<MODE>(S, ray, t, entry);
             const bool hit = tr == ORT_TRACE_HIT;
