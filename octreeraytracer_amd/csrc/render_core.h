@@ -639,7 +639,7 @@ struct Masks64 {  // levels 0..7: trees of depth <= 8
 #endif
     }
 };
-struct Masks96 {  // levels 0..11
+struct Masks96 {  // levels 0..9 (ORT_COMPACT_MAX_DEPTH 10)
     static constexpr bool kInlineLeaves = false;
 #ifndef ORT_LEAD_LEAVES_DEEP
 #define ORT_LEAD_LEAVES_DEEP 1
@@ -648,34 +648,41 @@ struct Masks96 {  // levels 0..11
     static constexpr bool kRevPlanes = false;
     static constexpr bool kKeepNear = true;
     static constexpr bool kKidSkip = false;
+    // levels 2..9 in lo (bits 8(L-2)..), levels 0..1 in hi: the deep levels a walk spends
+    // nearly all its steps at share one word, so the put/pop branches below are taken alike
+    // by almost every lane of a wave (with levels 8.. in hi, lanes split over them often)
+#ifndef ORT_MASKS_SPLIT_AT
+#define ORT_MASKS_SPLIT_AT 2
+#endif
+    static constexpr int kSplit = ORT_MASKS_SPLIT_AT;  // first level held in lo
     uint64_t lo;
     uint32_t hi;
     ORT_FN void clear() { lo = 0; hi = 0; }
     ORT_FN bool empty() const { return (lo | hi) == 0; }
     ORT_FN void put(int L, uint32_t rev) {
-        if (L < 8) lo |= (uint64_t)rev << (8 * L);
-        else hi |= rev << (8 * (L - 8));
+        if (L >= kSplit) lo |= (uint64_t)rev << (8 * (L - kSplit));
+        else hi |= rev << (8 * L);
     }
     ORT_FN int pop() {
-        if (hi) {
-            const int hb = 31 - __builtin_clz(hi);
-            hi ^= 1u << hb;
-            return 64 + hb;
+        if (lo) {
+            const int hb = 63 - __builtin_clzll(lo);
+            lo ^= (uint64_t)1 << hb;
+            return 8 * kSplit + hb;
         }
-        const int hb = 63 - __builtin_clzll(lo);
-        lo ^= (uint64_t)1 << hb;
+        const int hb = 31 - __builtin_clz(hi);
+        hi ^= 1u << hb;
         return hb;
     }
     ORT_FN bool take(int hb) {
-        if (hb >= 64) {
-            const uint32_t b = 1u << (hb - 64);
-            const bool t = (hi & b) != 0;
-            hi &= ~b;
+        if (hb >= 8 * kSplit) {
+            const uint64_t b = (uint64_t)1 << (hb - 8 * kSplit);
+            const bool t = (lo & b) != 0;
+            lo &= ~b;
             return t;
         }
-        const uint64_t b = (uint64_t)1 << hb;
-        const bool t = (lo & b) != 0;
-        lo &= ~b;
+        const uint32_t b = 1u << hb;
+        const bool t = (hi & b) != 0;
+        hi &= ~b;
         return t;
     }    ORT_FN void uniform() {
 #if defined(__HIP_DEVICE_COMPILE__)
