@@ -601,6 +601,13 @@ ORT_FN float4 fetch_sphere(const KScene& S, int e) {
 #endif
 }
 
+// The rejected-sphere skip's kid entry of a popped node loaded in the pop beside its record
+// (its latency hidden behind the pop's plane reads) instead of in the node's step.
+#ifndef ORT_KID_PREFETCH
+#define ORT_KID_PREFETCH 1
+#endif
+constexpr bool kKidPrefetch = ORT_KID_PREFETCH;
+
 // Plane idx of a ray-order table (base[idx]; see fast_begin for the reversed copies).
 ORT_FN float plane_at(const float* base, int idx) { return base[idx]; }
 
@@ -729,6 +736,7 @@ struct FastStateT {
     uint32_t cP;     // (not kRevPlanes) ray-order index of the current node's near plane, 10 bits per axis
     uint32_t otab;   // nibble r = octant of rank r; nibble 0 = m
     int node, depth;
+    uint2 kd;        // (kKidSkip, ORT_KID_PREFETCH) kid entry of `node`, loaded with rec
     uint2 rec;       // node record of `node`, loaded as soon as the pop knows it (its latency
                      // overlaps the pop's plane reads instead of opening the next step)
     float closest;   // (t_min is kFastTMin)
@@ -847,6 +855,7 @@ ORT_FN bool fast_begin(const KScene& S, const float* planes, const uint8_t* rank
     }
     st.node = 0;
     st.rec = fetch_node(S, 0);
+    if (kKidPrefetch && Masks::kKidSkip && S.kid) st.kd = fetch_kid(S, 0);
     st.depth = 0;
     st.closest = t_max;
     st.hitEntry = -1;
@@ -1002,7 +1011,7 @@ ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks
         // in the counting kernels, which count the reference walk's work
         uint32_t skip = 0;
         if (!COUNT && Masks::kKidSkip && S.kid) {
-            const uint2 kd = fetch_kid(S, st.node);
+            const uint2 kd = kKidPrefetch ? st.kd : fetch_kid(S, st.node);
             const uint32_t m = (((kd.x & 0xffffffu) == st.kc_id) ? (kd.x >> 24) : 0u) |
                                (((kd.y & 0xffffffu) == st.kc_id) ? (kd.y >> 24) : 0u);
             const float ptmin = fmax_tmin(fmax3(tNA, tNB, tNC));
@@ -1054,6 +1063,7 @@ ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks
     st.depth = L + 1;
     st.node = fr.getCo(L) + (int)((st.otab >> (4 * rk)) & 15u);
     st.rec = fetch_node(S, st.node);
+    if (kKidPrefetch && !COUNT && Masks::kKidSkip && S.kid) st.kd = fetch_kid(S, st.node);
     if (Masks::kRevPlanes) {
         // near plane of the level-(L+1) child: the level-L ancestor's (offset bits below 8w
         // cleared; the table start is a multiple of 4T >= 8w bytes) plus w planes on the axes
