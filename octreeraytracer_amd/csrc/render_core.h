@@ -620,8 +620,9 @@ struct Masks64 {  // levels 0..7: trees of depth <= 8
     static constexpr bool kLeadLeaves = false;
     static constexpr bool kRevPlanes = true;  // depth <= 8: reversed plane tables (fast_rev_planes)
     static constexpr bool kKeepNear = true;   // keep the node's near-plane pointers (FastStateT::nA..)
-    // rejected-sphere skip (kid_table.h): off in the camera-ray walks, whose inline leaf
-    // children already avoid most leaf pops (C3 5 % slower with it), on in the bounce walks
+    // rejected-sphere skip (kid_table.h): off in the depth <= 8 camera-ray walk, whose inline
+    // leaf children already avoid most leaf pops (C3 5 % slower with it); on in the bounce
+    // walks and the deep camera walk (Masks96)
     static constexpr bool kKidSkip = false;
     uint64_t m;
     ORT_FN void clear() { m = 0; }
@@ -654,7 +655,12 @@ struct Masks96 {  // levels 0..9 (ORT_COMPACT_MAX_DEPTH 10)
     static constexpr bool kLeadLeaves = ORT_LEAD_LEAVES_DEEP;
     static constexpr bool kRevPlanes = false;
     static constexpr bool kKeepNear = true;
-    static constexpr bool kKidSkip = false;
+    // the rejected-sphere skip here too: with the kid entry loaded in the pop, C5's camera
+    // walk 17.52 -> 16.41 ms in A/B (no gain while the entry was loaded in the node's step)
+#ifndef ORT_KID_SKIP_DEEP_CAMERA
+#define ORT_KID_SKIP_DEEP_CAMERA 1
+#endif
+    static constexpr bool kKidSkip = ORT_KID_SKIP_DEEP_CAMERA;
     // levels 2..9 in lo (bits 8(L-2)..), levels 0..1 in hi: the deep levels a walk spends
     // nearly all its steps at share one word, so the put/pop branches below are taken alike
     // by almost every lane of a wave (with levels 8.. in hi, lanes split over them often)
