@@ -623,7 +623,10 @@ struct Masks64 {  // levels 0..7: trees of depth <= 8
     // rejected-sphere skip (kid_table.h): off in the depth <= 8 camera-ray walk, whose inline
     // leaf children already avoid most leaf pops (C3 5 % slower with it); on in the bounce
     // walks and the deep camera walk (Masks96)
-    static constexpr bool kKidSkip = false;
+#ifndef ORT_KID_SKIP_CAMERA8
+#define ORT_KID_SKIP_CAMERA8 0
+#endif
+    static constexpr bool kKidSkip = ORT_KID_SKIP_CAMERA8;
     uint64_t m;
     ORT_FN void clear() { m = 0; }
     ORT_FN bool empty() const { return m == 0; }
@@ -649,8 +652,11 @@ struct Masks64 {  // levels 0..7: trees of depth <= 8
 };
 struct Masks96 {  // levels 0..9 (ORT_COMPACT_MAX_DEPTH 10)
     static constexpr bool kInlineLeaves = false;
+    // leading leaf children tested inline: C5 camera walk 19.45 -> 17.62 ms when added, but
+    // with the rejected-sphere skip on (which drops most of those leaves before they are
+    // pushed) 16.60 -> 15.37 ms without them (tools/ab_stream.py): off
 #ifndef ORT_LEAD_LEAVES_DEEP
-#define ORT_LEAD_LEAVES_DEEP 1
+#define ORT_LEAD_LEAVES_DEEP 0
 #endif
     static constexpr bool kLeadLeaves = ORT_LEAD_LEAVES_DEEP;
     static constexpr bool kRevPlanes = false;
