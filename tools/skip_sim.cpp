@@ -193,6 +193,16 @@ void skip_sim_run(const float* nmin, const float* nmax, const int32_t* co, const
 // per_ray (2 per ray): pops reference, pops with skips
 static int kids_k_parent = 0;
 void skip_sim_push_parent(int v) { kids_k_parent = v; }
+// Subtree mode: a child also qualifies when its whole subtree holds one distinct sphere
+// (skip_sim_summaries with K >= 1); null = leaf children only.
+static const int32_t* g_sum_ids = nullptr;
+static const int8_t* g_sum_n = nullptr;
+static int g_sum_k = 1;
+void skip_sim_push_subtree(const int32_t* sum_ids, const int8_t* sum_n, int K) {
+    g_sum_ids = sum_ids;
+    g_sum_n = sum_n;
+    g_sum_k = K;
+}
 void skip_sim_push(const float* nmin, const float* nmax, const int32_t* co, const int32_t* oo, const int32_t* cnt,
                    const int32_t* idx, int32_t n, const float* sph, int cache, int kids_k, const float* rays,
                    int64_t nrays, int64_t* stats, int32_t* per_ray) {
@@ -244,10 +254,15 @@ void skip_sim_push(const float* nmin, const float* nmax, const int32_t* co, cons
                     // distinct one-sphere-leaf spheres among the children (the parent's budget)
                     int32_t ks[8];
                     int kn = 0;
+                    auto one = [&](int64_t c, int32_t& s) {
+                        if (co[c] == -1 && cnt[c] == 1) { s = idx[oo[c]]; return true; }
+                        if (g_sum_n && co[c] != -1 && g_sum_n[c] == 1) { s = g_sum_ids[c * g_sum_k]; return true; }
+                        return false;
+                    };
                     for (int i = 0; i < 8; ++i) {
                         const int64_t c = (int64_t)co[ni] + i;
-                        if (c >= n || co[c] != -1 || cnt[c] != 1) continue;
-                        const int32_t s = idx[oo[c]];
+                        int32_t s;
+                        if (c >= n || !one(c, s)) continue;
                         bool seen = false;
                         for (int q = 0; q < kn; ++q) seen = seen || ks[q] == s;
                         if (!seen) ks[kn++] = s;
@@ -260,8 +275,9 @@ void skip_sim_push(const float* nmin, const float* nmax, const int32_t* co, cons
                             (co[c] == -1 && oo[c] == -1))
                             continue;
                         const float ct = fmaxr(cmin, ntmin);
-                        if (skip && co[c] == -1 && cnt[c] == 1) {
-                            const int32_t s = idx[oo[c]];
+                        int32_t s1;
+                        if (skip && one(c, s1)) {
+                            const int32_t s = s1;
                             int pos = -1;
                             for (int q = 0; q < kn; ++q) if (ks[q] == s) pos = q;
                             const int qc = cache_find(s);
