@@ -258,9 +258,9 @@ __global__ void __launch_bounds__(kBlock) ort_raygen_kernel(PipeArgs A) {
 // cannot take are appended to the defer list for ort_trace_exact.
 // Waves per SIMD (minimum, amdgpu_waves_per_eu): the per-lane trace kernels run at 8 (59-64
 // VGPRs, spill-free; tools/kernel_resources.py).  The persistent bounce kernel is asked for 6:
-// with the rejected-sphere skip its 96-bit walk needs 87 VGPRs unconstrained (5 waves), at 6
-// waves it fits 80 with 5 spilled (C5 frame -2.4 % vs 5 waves, tools/ab_stream.py); the LDS
-// image (24.6 KB per workgroup at depth 10) caps it at 6 anyway.
+// its depth 9-10 walk over the reversed plane tables fits 79 VGPRs there without spills (the
+// forward-table walk needed 87 unconstrained and spilled 5 at 6 waves), and its LDS (53.3 KB
+// per 512-thread workgroup at depth 10) caps it at 6 anyway; the depth <= 8 instance 78.
 #ifndef ORT_PERSISTENT_WAVES
 #define ORT_PERSISTENT_WAVES 6
 #endif
@@ -268,8 +268,9 @@ __global__ void __launch_bounds__(kBlock) ort_raygen_kernel(PipeArgs A) {
 #define ORT_TRACE_WAVES 8
 #endif
 // Deep (depth > 8) per-lane kernel: its LDS image (24.6 KB per 256-thread workgroup at depth 10)
-// caps a CU at 6 workgroups = 6 waves/SIMD, so it may use the registers of 6 waves: 64-69
-// VGPRs without spills (at 8 the bounce-0 shading variant spilled 3; C5 +0.4 % in A/B).
+// caps a CU at 6 workgroups = 6 waves/SIMD, so it may use the registers of 6 waves: 60-64
+// VGPRs without spills.  (512-thread workgroups, whose LDS would allow 8 waves/SIMD at these
+// 64 VGPRs, measured no faster: C5 -0.1 % at 6, -0.4 % at 8 in A/B.)
 #ifndef ORT_TRACE_WAVES_DEEP
 #define ORT_TRACE_WAVES_DEEP 6
 #endif
