@@ -449,6 +449,10 @@ __device__ __forceinline__ bool shade_state(const PipeArgs& A, int k, size_t p, 
         float* o = A.out + 3 * p;
         o[0] = v.x; o[1] = v.y; o[2] = v.z;
     } else {
+        // the last sample of a final_out frame: a path that ends here writes its pixel and
+        // nothing else -- the later kernels walk the lists of alive paths only, and no sample
+        // follows to read its RNG state
+        const bool fin = A.final_out && A.sample == A.pp.ns - 1;
         if (done) {
             ort::V3 acc = ort::mk(0.0f, 0.0f, 0.0f);
             if (A.sample > 0) {
@@ -456,20 +460,20 @@ __device__ __forceinline__ bool shade_state(const PipeArgs& A, int k, size_t p, 
                 acc = ort::mk(a.x, a.y, a.z);
             }
             acc = ort::add(acc, c);
-            if (A.final_out && A.sample == A.pp.ns - 1) {  // ort_finalize_kernel's work for this pixel
+            if (fin) {  // ort_finalize_kernel's work for this pixel
                 const ort::V3 v = ort::finish_pixel(acc, A.pp.ns);
                 float* o = A.out + 3 * p;
                 o[0] = v.x; o[1] = v.y; o[2] = v.z;
             } else {
                 A.pcol[k] = make_float4(acc.x, acc.y, acc.z, 0.0f);
+                A.pd[k] = make_float4(ray.d.x, ray.d.y, ray.d.z, 0.0f);
             }
-            A.pd[k] = make_float4(ray.d.x, ray.d.y, ray.d.z, 0.0f);
         } else {
             A.po[k] = make_float4(ray.o.x, ray.o.y, ray.o.z, importance);
             A.pd[k] = make_float4(ray.d.x, ray.d.y, ray.d.z, 1.0f);
             A.pc[k] = make_float4(c.x, c.y, c.z, 0.0f);
         }
-        A.prng[k] = make_float2(st.x, st.y);
+        if (!(done && fin)) A.prng[k] = make_float2(st.x, st.y);
     }
     return !DIRECT && !done;
 }
