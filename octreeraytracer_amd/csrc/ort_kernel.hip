@@ -1040,6 +1040,7 @@ struct ort_ctx {
     int64_t n_indices = 0;
     DevBuf sph_cr, sph_ma, sph_fr;
     DevBuf node, leaf_sph, leaf_idx, planes, kid;  // compact
+    DevBuf nk;                                   // ... node records and kid entries interleaved (build_nk)
     DevBuf lds_img;                              // compact: the workgroup LDS image (k_lds_image)
     DevBuf lds_rev;                              // ... depth 9-10: the reversed-table image (persistent kernel)
     DevBuf nodeA, nodeB, cnt, indices;           // explicit
@@ -1078,7 +1079,7 @@ void free_buf(DevBuf& b) {
 }
 
 void free_scene(ort_ctx* c) {
-    DevBuf* all[] = {&c->sph_cr, &c->sph_ma, &c->sph_fr, &c->node, &c->kid, &c->leaf_sph, &c->leaf_idx,
+    DevBuf* all[] = {&c->sph_cr, &c->sph_ma, &c->sph_fr, &c->node, &c->kid, &c->nk, &c->leaf_sph, &c->leaf_idx,
                      &c->planes, &c->lds_img, &c->lds_rev, &c->nodeA, &c->nodeB, &c->cnt, &c->indices};
     for (DevBuf* b : all) free_buf(*b);
     ort::freeGpuTree(c->tree);
@@ -1106,6 +1107,29 @@ int build_lds_image(ort_ctx* ctx) {
                            rev != 0, (unsigned char*)img.p);
         HIPCHK(ctx, hipGetLastError());
     }
+    return ORT_OK;
+}
+
+__global__ void __launch_bounds__(kBlock) k_interleave_nk(const uint2* node, const uint2* kid, uint4* nk, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint2 a = node[i], b = kid[i];
+    nk[i] = make_uint4(a.x, a.y, b.x, b.y);
+}
+
+// The walks that use the rejected-sphere skip load a node's record and kid entry together
+// (fetch_rec): one 16-byte load, one cache line per record instead of one in each array.
+// Built when both arrays are there and 16 bytes per node stay under the buffer loads' 4 GiB.
+int build_nk(ort_ctx* ctx) {
+    free_buf(ctx->nk);
+    const int64_t n = (int64_t)(ctx->node.bytes / 8);
+    if (!ORT_NODE_KID || !ctx->kid.p || ctx->kid.bytes < ctx->node.bytes || n == 0 || 16 * n >= (int64_t)UINT32_MAX)
+        return ORT_OK;
+    int rc;
+    if ((rc = upload(ctx, ctx->nk, nullptr, 16 * (size_t)n))) return rc;
+    hipLaunchKernelGGL(k_interleave_nk, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, ctx->stream,
+                       (const uint2*)ctx->node.p, (const uint2*)ctx->kid.p, (uint4*)ctx->nk.p, n);
+    HIPCHK(ctx, hipGetLastError());
     return ORT_OK;
 }
 
@@ -1184,7 +1208,7 @@ int build_impl(ort_ctx* ctx, const float* cr, const float* ma, const float* fr, 
         ctx->leaf_sph = {cd.leaf_sph, cd.leaf_bytes};
         ctx->leaf_idx = {cd.leaf_idx, cd.idx_bytes};
         ctx->planes = {cd.planes, cd.plane_bytes};
-        if ((rc = build_lds_image(ctx))) {
+        if ((rc = build_lds_image(ctx)) || (rc = build_nk(ctx))) {
             ort::freeGpuTree(t);
             return rc;
         }
@@ -1242,6 +1266,7 @@ int upload_impl(ort_ctx* ctx, const ort::SceneInput& in) {
             if ((rc = upload(ctx, ctx->leaf_idx, cl.leaf_idx.data(), 4 * cl.leaf_idx.size()))) return rc;
             if ((rc = upload(ctx, ctx->planes, cl.planes.data(), 4 * cl.planes.size()))) return rc;
             if ((rc = build_lds_image(ctx))) return rc;
+            if ((rc = build_nk(ctx))) return rc;
             HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
         } else {
             const int d = ort::treeDepth(in);
@@ -1278,6 +1303,8 @@ ort::KScene device_scene(const ort_ctx* c) {
     S.n_nodes = c->n_nodes;
     S.node = (const uint2*)c->node.p;
     S.kid = c->kid_skip ? (const uint2*)c->kid.p : nullptr;
+    S.nk = c->kid_skip ? (const uint4*)c->nk.p : nullptr;
+    S.nk_bytes = (uint32_t)c->nk.bytes;
     S.tail_base = (uint32_t)c->n_indices;
     S.leaf_sph = (const float4*)c->leaf_sph.p;
     S.node_bytes = (uint32_t)c->node.bytes;
@@ -1832,7 +1859,7 @@ int ort_scene_get_info(const ort_ctx* ctx, ort_scene_info* info) {
     info->n_indices = ctx->n_indices;
     info->layout = ctx->layout;
     info->tree_depth = ctx->depth;
-    const DevBuf* all[] = {&ctx->sph_cr, &ctx->sph_ma, &ctx->sph_fr, &ctx->node, &ctx->kid, &ctx->leaf_sph, &ctx->leaf_idx,
+    const DevBuf* all[] = {&ctx->sph_cr, &ctx->sph_ma, &ctx->sph_fr, &ctx->node, &ctx->kid, &ctx->nk, &ctx->leaf_sph, &ctx->leaf_idx,
                            &ctx->planes, &ctx->lds_img, &ctx->lds_rev, &ctx->nodeA, &ctx->nodeB, &ctx->cnt, &ctx->indices};
     int64_t b = 0;
     for (const DevBuf* d : all) b += (int64_t)d->bytes;

@@ -105,6 +105,8 @@ struct KScene {
     uint32_t node_bytes;     // buffer sizes for the range-checked buffer loads (< 2^32)
     uint32_t leaf_bytes;
     const uint2* kid;        // per node: rejected-sphere skip entry (kid_table.h), or null (off)
+    const uint4* nk;         // per node: {record, kid entry} interleaved (one 16-byte load), or null
+    uint32_t nk_bytes;
     uint32_t tail_base;      // = n_indices: a one-sphere leaf's objectsOffset is tail_base + sphere
     // explicit (reference) layout
     const float4* nodeA;     // min.xyz, int bits of childrenOffset (binding 3)
@@ -591,6 +593,15 @@ ORT_FN uint2 fetch_kid(const KScene& S, int i) {
     return S.kid[i];
 #endif
 }
+ORT_FN uint4 fetch_nk(const KScene& S, int i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)S.nk, 0, (int)S.nk_bytes, 0x00020000);
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)i * 16u, 0, 0);
+    return make_uint4(v[0], v[1], v[2], v[3]);
+#else
+    return S.nk[i];
+#endif
+}
 ORT_FN float4 fetch_sphere(const KScene& S, int e) {
 #if defined(__HIP_DEVICE_COMPILE__)
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)S.leaf_sph, 0, (int)S.leaf_bytes, 0x00020000);
@@ -808,6 +819,24 @@ struct Masks64Plain : Masks64 {
     static constexpr bool kKidSkip = true;
 };
 
+// Node i's record into st.rec and, with kid (the rejected-sphere skip), its kid entry into
+// st.kd: both from the interleaved copy S.nk in one 16-byte load when the context built it
+// (ORT_NODE_KID), else from the two arrays.
+#ifndef ORT_NODE_KID
+#define ORT_NODE_KID 1
+#endif
+template <class Masks>
+ORT_FN void fetch_rec(const KScene& S, int i, bool kid, FastStateT<Masks>& st) {
+    if (ORT_NODE_KID && Masks::kKidSkip && kid && S.nk) {
+        const uint4 v = fetch_nk(S, i);
+        st.rec = make_uint2(v.x, v.y);
+        st.kd = make_uint2(v.z, v.w);
+        return;
+    }
+    st.rec = fetch_node(S, i);
+    if (kid) st.kd = fetch_kid(S, i);
+}
+
 // Root test and state setup (glsl:296-311).  Returns false when the root box is missed.
 template <class Masks>
 ORT_FN bool fast_begin(const KScene& S, const float* planes, const uint8_t* rank_lut, const Ray& r, V3 inv, float t_min,
@@ -866,8 +895,7 @@ ORT_FN bool fast_begin(const KScene& S, const float* planes, const uint8_t* rank
         }
     }
     st.node = 0;
-    st.rec = fetch_node(S, 0);
-    if (kKidPrefetch && Masks::kKidSkip && S.kid) st.kd = fetch_kid(S, 0);
+    fetch_rec(S, 0, kKidPrefetch && Masks::kKidSkip && S.kid, st);
     st.depth = 0;
     st.closest = t_max;
     st.hitEntry = -1;
@@ -1074,8 +1102,7 @@ ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks
     const int w = 1 << (D - 1 - L);  // child width in plane steps
     st.depth = L + 1;
     st.node = fr.getCo(L) + (int)((st.otab >> (4 * rk)) & 15u);
-    st.rec = fetch_node(S, st.node);
-    if (kKidPrefetch && !COUNT && Masks::kKidSkip && S.kid) st.kd = fetch_kid(S, st.node);
+    fetch_rec(S, st.node, kKidPrefetch && !COUNT && Masks::kKidSkip && S.kid, st);
     if (Masks::kRevPlanes) {
         // near plane of the level-(L+1) child: the level-L ancestor's (offset bits below 8w
         // cleared; the table start is a multiple of 4T >= 8w bytes) plus w planes on the axes
