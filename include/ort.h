@@ -101,7 +101,10 @@ typedef struct ort_scene_info {
                                       super-tiles; 0: raster order (tile b on XCD b % 8) */
 #define ORT_OPT_KID_SKIP 9         /* 1 (default): a lane skips one-sphere leaf children holding the sphere it
                                       last rejected at a tmin <= theirs (they cannot end the walk; same
-                                      pixels, kid_table.h); 0: walk them as the reference does */
+                                      pixels, kid_table.h), a node's record and kid entry loaded together
+                                      from the interleaved copy; 2: the skip with the record and kid
+                                      entry from their own arrays (testing; same pixels); 0: walk them
+                                      as the reference does */
 
 /* Traffic counters (ort_count_traffic), in the REFERENCE layout's terms. */
 #define ORT_COUNT_NODES_POPPED 0

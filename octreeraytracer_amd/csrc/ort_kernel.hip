@@ -1018,7 +1018,7 @@ struct ort_ctx {
     void* wclock = nullptr;  // ort_debug_wave_clock
     long long wclock_n = 0;
     int xcd_swizzle = 2;  // ORT_OPT_XCD_SWIZZLE: workgroup -> tile order (block_tile)
-    int kid_skip = 1;     // ORT_OPT_KID_SKIP: rejected-sphere skip of one-sphere leaf children
+    int kid_skip = 1;     // ORT_OPT_KID_SKIP: rejected-sphere skip of one-sphere leaf children (2: without nk)
     int wave_queue = 0;  // ORT_OPT_WAVE_QUEUE: per-lane walk from a wave-level block queue (opt-in)
     int packet = 0;     // ORT_OPT_PACKET: wave-level walk for camera rays (SALU-bound so far: off)
     // ORT_OPT_SORT_PATHS: order of the alive paths between bounces.  2 (default): the list the
@@ -1303,7 +1303,7 @@ ort::KScene device_scene(const ort_ctx* c) {
     S.n_nodes = c->n_nodes;
     S.node = (const uint2*)c->node.p;
     S.kid = c->kid_skip ? (const uint2*)c->kid.p : nullptr;
-    S.nk = c->kid_skip ? (const uint4*)c->nk.p : nullptr;
+    S.nk = c->kid_skip == 1 ? (const uint4*)c->nk.p : nullptr;  // 2: the separate arrays (testing)
     S.nk_bytes = (uint32_t)c->nk.bytes;
     S.tail_base = (uint32_t)c->n_indices;
     S.leaf_sph = (const float4*)c->leaf_sph.p;
@@ -1782,7 +1782,8 @@ int ort_set_option(ort_ctx* ctx, int option, int value) {
         return ORT_OK;
     }
     if (option == ORT_OPT_KID_SKIP) {
-        ctx->kid_skip = value ? 1 : 0;
+        if (value < 0 || value > 2) return fail(ctx, ORT_ERR_INVALID_ARG, "ORT_OPT_KID_SKIP: 0, 1 or 2");
+        ctx->kid_skip = value;
         return ORT_OK;
     }
     if (option == ORT_OPT_XCD_SWIZZLE) {

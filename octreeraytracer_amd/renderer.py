@@ -137,9 +137,11 @@ class Renderer:
         traces only (same pixels)."""
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_PERSISTENT, int(on)))
 
-    def set_kid_skip(self, on: bool):
-        """Rejected-sphere skip of one-sphere leaf children (kid_table.h); same pixels."""
-        self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_KID_SKIP, int(bool(on))))
+    def set_kid_skip(self, mode: int):
+        """Rejected-sphere skip of one-sphere leaf children (kid_table.h); same pixels.  0 off,
+        1 on (node records and kid entries from the interleaved copy), 2 on with the two
+        separate arrays (testing)."""
+        self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_KID_SKIP, int(mode)))
 
     def set_refill(self, lanes: int):
         """Persistent trace: refill a wave once at least `lanes` of its 64 lanes are idle."""

@@ -186,12 +186,13 @@ def test_kernel_variants_identical(ort, oracle, renderer, scene_c2, persistent, 
         renderer.set_wave_queue(False)
 
 
-@pytest.mark.parametrize("kid_skip", [1, 0])
+@pytest.mark.parametrize("kid_skip", [1, 2, 0])
 @pytest.mark.parametrize("sort", [2, 1, 0])
 @pytest.mark.parametrize("depth,mspn", [(6, 1), (10, 1)])
 def test_bounce_orders_and_skip_identical(ort, oracle, renderer, depth, mspn, sort, kid_skip):
     """Every order of the alive paths between bounces (ORT_OPT_SORT_PATHS: list sort with the
-    length read back, every-slot sort, slot order) and the rejected-sphere skip on and off give
+    length read back, every-slot sort, slot order) and the rejected-sphere skip on (records and
+    kid entries interleaved, or from their two arrays) and off give
     the oracle's pixels, on maxSpheresPerNode-1 trees (where the skip fires) of depth 6 (64-bit
     bounce walk) and 10 (96-bit), with several samples (path state carried across samples)."""
     s = ort.random_spheres(8000, 3)
