@@ -206,6 +206,8 @@ def test_bounce_orders_and_skip_identical(ort, oracle, renderer, depth, mspn, so
         got = renderer.render(p, tile)
         ref = oracle.render(s, t, p, tile.x0, tile.y0, tile.width, tile.rows)
         assert_same(got, ref, f"sort={sort} kid_skip={kid_skip} d{depth}")
+        with pytest.raises(ort.OrtError):
+            renderer.set_kid_skip(3)
     finally:
         renderer.set_sort_paths(2)  # the defaults
         renderer.set_kid_skip(1)
