@@ -9,7 +9,7 @@ import time
 from pathlib import Path
 
 if len(sys.argv) > 4 and int(sys.argv[4]) > 1:  # as bench.py: overlap needs its own HW queues
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"  # assigned, not defaulted: the gpurun boxes export 4
 
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
