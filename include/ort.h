@@ -90,9 +90,11 @@ typedef struct ort_scene_info {
 #define ORT_OPT_PACKET 5           /* 1: wave-level walk for camera rays; 0 (default): per-lane walk (same pixels) */
 #define ORT_OPT_SORT_PATHS 6       /* order of the alive paths between bounces (coherence; same pixels):
                                       2 (default) radix-sort the compacted list by direction octant +
-                                      origin cell + direction (reads the list's length back: the host
-                                      waits once per bounce); 1 sort every slot's key (no host wait);
-                                      0 slot order */
+                                      origin cell + direction; the list's length stays on the device
+                                      (the sort's size is the same bounce's length in the previous
+                                      frame of the same shape + 1/64 + 1024, read back asynchronously;
+                                      a longer list goes on unsorted): no host wait; 1 sort every
+                                      slot's key; 0 slot order */
 #define ORT_OPT_WAVE_QUEUE 7       /* 1: resident workgroups whose waves take 64-slot blocks from a queue;
                                       0 (default): one workgroup per 16x16 tile (same pixels) */
 #define ORT_OPT_XCD_SWIZZLE 8      /* workgroup -> tile order (same pixels): 2 (default) each XCD renders
@@ -105,6 +107,9 @@ typedef struct ort_scene_info {
                                       from the interleaved copy; 2: the skip with the record and kid
                                       entry from their own arrays (testing; same pixels); 0: walk them
                                       as the reference does */
+#define ORT_OPT_SORT_BOUND 10      /* testing: > 0 forces the size of the list sort (SORT_PATHS 2) to this
+                                      bound -- below the list's length the list goes on in append
+                                      order (same pixels); 0 (default): the hint described above */
 
 /* Traffic counters (ort_count_traffic), in the REFERENCE layout's terms. */
 #define ORT_COUNT_NODES_POPPED 0
@@ -171,9 +176,12 @@ int ort_get_stream(const ort_ctx* ctx, void** stream);
 
 /* Render the tile; rgb_out receives tile->rows * tile->width RGB float triples, row-major,
  * output row 0 first.  out_is_device != 0: rgb_out is a device pointer on ctx's device.
- * stream: a hipStream_t on ctx's device (stream-ordered, returns at once), or NULL for the
- * context's own stream (then the call returns after the frame is complete).  The HIP null
- * stream has the NULL handle, so passing it also means "synchronous". */
+ * stream: a hipStream_t on ctx's device (stream-ordered, returns at once -- also for
+ * multi-sample / multi-bounce frames: no step of the frame waits on the host; the first
+ * frame of a new shape may allocate, and hipMalloc/hipFree synchronise the device), or NULL
+ * for the context's own stream (then the call returns after the frame is complete).  The HIP
+ * null stream has the NULL handle, so passing it also means "synchronous".  Two frames in
+ * flight on one context must not overlap: render the next one on the same stream or wait. */
 int ort_render(ort_ctx* ctx, const ort_params* params, const ort_tile* tile,
                float* rgb_out, int out_is_device, void* stream);
 
@@ -214,18 +222,28 @@ int ort_count_traffic(ort_ctx* ctx, const ort_params* params, const ort_tile* ti
  * Calls on one group are not thread-safe. */
 typedef struct ort_group ort_group;
 #define ORT_GROUP_MAX_DEVICES 64
+#define ORT_GROUP_MAX_INFLIGHT 4
 #define ORT_GROUP_TRANSPORT_RCCL 0
 #define ORT_GROUP_TRANSPORT_COPY 1
+/* One frame in flight (= ort_group_create_pipelined(..., 1, out)). */
 int ort_group_create(const int32_t* devices, int32_t n_devices, int32_t transport, ort_group** out);
+/* frames_in_flight (1..ORT_GROUP_MAX_INFLIGHT) frame slots, each with its own context per
+ * device (its own scene copy, stream, band tiles and, with RCCL, communicators): frames
+ * submitted in turn take the slots in turn, so frame k+1's renders fill the tail of frame k's
+ * (a 1/N band tile leaves most of the GPU idle while its last blocks finish).  No reference
+ * counterpart: the GL loop renders one frame at a time (src/raytracer.cpp:480-519). */
+int ort_group_create_pipelined(const int32_t* devices, int32_t n_devices, int32_t transport,
+                               int32_t frames_in_flight, ort_group** out);
 int ort_group_destroy(ort_group* group);
 /* Last error of the group (or of the calling thread when group == NULL).  Never NULL. */
 const char* ort_group_last_error(const ort_group* group);
 int ort_group_size(const ort_group* group);
-/* The context of rank `rank` (owned by the group), e.g. for ort_scene_get_info. */
+int ort_group_frames_in_flight(const ort_group* group);
+/* The context of rank `rank` in frame slot 0 (owned by the group), e.g. for ort_scene_get_info. */
 int ort_group_context(ort_group* group, int32_t rank, ort_ctx** ctx);
-/* ort_set_option on every context. */
+/* ort_set_option on every context (every slot). */
 int ort_group_set_option(ort_group* group, int option, int value);
-/* ort_upload_scene / ort_build_scene on every context (same arguments). */
+/* ort_upload_scene / ort_build_scene on every context of every slot (same arguments). */
 int ort_group_upload_scene(ort_group* group, const float* sphere_center_radius, const float* sphere_mat_albedo,
                            const float* sphere_fuzz_ri, int32_t n_spheres, const float* node_min,
                            const float* node_max, const int32_t* children_offset, const int32_t* objects_offset,
@@ -234,11 +252,21 @@ int ort_group_upload_scene(ort_group* group, const float* sphere_center_radius, 
 int ort_group_build_scene(ort_group* group, const float* sphere_center_radius, const float* sphere_mat_albedo,
                           const float* sphere_fuzz_ri, int32_t n_spheres, int32_t max_depth,
                           int32_t max_spheres_per_node);
-/* One full frame (width x height RGB floats, row 0 = bottom) into rgb_out: host memory, or
- * (out_is_device != 0) device memory on devices[0].  Synchronous. */
+/* Enqueue one full frame (width x height RGB floats, row 0 = bottom) into rgb_out -- host
+ * memory (pinned for a fully asynchronous copy), or (out_is_device != 0) device memory on
+ * devices[0] -- and return at once with its ticket (0, 1, 2, ...).  Every rank's render is
+ * enqueued before any of them runs (no host wait inside); the only wait is for the frame that
+ * last used this frame's slot, frames_in_flight frames earlier.  rgb_out must stay untouched
+ * until ort_group_wait(ticket) returns. */
+int ort_group_submit(ort_group* group, const ort_params* params, float* rgb_out, int32_t out_is_device,
+                     int64_t* ticket);
+/* Wait until frame `ticket` is in rgb_out (gathered, assembled and, for host output, copied). */
+int ort_group_wait(ort_group* group, int64_t ticket);
+/* submit + wait for it and every earlier frame: synchronous. */
 int ort_group_render(ort_group* group, const ort_params* params, float* rgb_out, int32_t out_is_device);
-/* Device time of the last ort_group_render on devices[0]'s stream: renders, gather and
- * assembly (HIP events). */
+/* Device time, on devices[0], of the last frame ort_group_wait / ort_group_render saw complete:
+ * from its submission on devices[0]'s stream to its assembly (renders, gather, de-interleave;
+ * HIP events) -- the frame's latency, not its share of a pipelined throughput. */
 int ort_group_last_frame_ms(ort_group* group, float* ms);
 
 /* ---- host scene-build stage (kept reference API, src/raytracer.cpp + src/octree.cpp) -- */

@@ -31,6 +31,7 @@ ORT_OPT_SORT_PATHS = 6
 ORT_OPT_WAVE_QUEUE = 7
 ORT_OPT_XCD_SWIZZLE = 8
 ORT_OPT_KID_SKIP = 9
+ORT_OPT_SORT_BOUND = 10
 ORT_LAYOUT_COMPACT_EXACT_EMULATION = 2
 ORT_COUNT_N = 6
 COUNT_NAMES = ("nodes_popped", "child_records", "leaf_objects", "accepted_hits", "pixels", "traversals")
@@ -45,7 +46,8 @@ EXPORTED_SYMBOLS = (
     "ort_octree_indices", "ort_octree_free", "ort_camera_view", "ort_version",
     "ort_group_create", "ort_group_destroy", "ort_group_last_error", "ort_group_size", "ort_group_context",
     "ort_group_set_option", "ort_group_upload_scene", "ort_group_build_scene", "ort_group_render",
-    "ort_group_last_frame_ms",
+    "ort_group_last_frame_ms", "ort_group_create_pipelined", "ort_group_frames_in_flight", "ort_group_submit",
+    "ort_group_wait",
 )
 ORT_GROUP_TRANSPORT_RCCL = 0
 ORT_GROUP_TRANSPORT_COPY = 1
@@ -128,6 +130,10 @@ def _declare(lib):
         "ort_group_build_scene": (C.c_int, [_vp, _fp, _fp, _fp, C.c_int32, C.c_int32, C.c_int32]),
         "ort_group_render": (C.c_int, [_vp, C.POINTER(OrtParams), _vp, C.c_int32]),
         "ort_group_last_frame_ms": (C.c_int, [_vp, _fp]),
+        "ort_group_create_pipelined": (C.c_int, [_ip, C.c_int32, C.c_int32, C.c_int32, C.POINTER(_vp)]),
+        "ort_group_frames_in_flight": (C.c_int, [_vp]),
+        "ort_group_submit": (C.c_int, [_vp, C.POINTER(OrtParams), _vp, C.c_int32, C.POINTER(C.c_int64)]),
+        "ort_group_wait": (C.c_int, [_vp, C.c_int64]),
         "ort_debug_group_emulate": (C.c_int, [_fp, _fp, _fp, C.c_int32, _fp, _fp, _ip, _ip, _ip, C.c_int32, _ip, C.c_int64,
                                               C.c_int32, C.POINTER(OrtParams), _fp]),
         "ort_debug_emulate_render": (C.c_int, [_fp, _fp, _fp, C.c_int32, _fp, _fp, _ip, _ip, _ip, C.c_int32, _ip,

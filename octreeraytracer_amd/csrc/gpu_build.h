@@ -72,6 +72,13 @@ struct SortBuffers {
 // written by the kernels that appended the list (path_key.h) -> b.vals_out in key order.
 // Temp storage as for sortAlive with the same n bound.
 hipError_t sortList(void* temp, size_t temp_bytes, int n, const SortBuffers& b, hipStream_t s);
+// The same, stream-ordered: the list's length n is only on the device (*count).  `bound` is a
+// host-side size (a hint: last frame's length plus a margin).  Keys [n, bound) are padded with
+// the all-ones key, so the stable radix sort of `bound` pairs puts the n real ones first, in
+// key order.  If n > bound (the hint was short) the sort's output is replaced by the list in
+// append order -- the same paths, a different order, so the same pixels.  No host wait.
+hipError_t sortListBounded(void* temp, size_t temp_bytes, int bound, const int* count, const SortBuffers& b,
+                           hipStream_t s);
 size_t sortAliveTempBytes(int n);
 hipError_t sortAlive(void* temp, size_t temp_bytes, const float4* po, const float4* pd, int n, const float* root_lo,
                      const float* root_hi, const uint32_t* spread, const SortBuffers& b, int* count, hipStream_t s);

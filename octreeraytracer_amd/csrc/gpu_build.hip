@@ -689,12 +689,41 @@ __global__ void k_path_keys(const float4* po, const float4* pd, int n, MortonPla
     }
 }
 
+// sortListBounded, before the sort: keys [*count, bound) <- all ones (grid-stride; the grid
+// is sized on the host, the range on the device)
+__global__ void __launch_bounds__(kB) k_pad_keys(uint32_t* keys, const int* count, int bound) {
+    const int n = *count;
+    for (int i = n + (int)(blockIdx.x * kB + threadIdx.x); i < bound; i += (int)(gridDim.x * kB)) keys[i] = 0xffffffffu;
+}
+
+// ... after it: a list longer than the bound goes on in append order (vals_in -> vals_out)
+__global__ void __launch_bounds__(kB) k_overflow_copy(const int* vals_in, int* vals_out, const int* count, int bound) {
+    const int n = *count;
+    if (n <= bound) return;
+    for (int i = (int)(blockIdx.x * kB + threadIdx.x); i < n; i += (int)(gridDim.x * kB)) vals_out[i] = vals_in[i];
+}
+
 }  // namespace
 
 hipError_t sortList(void* temp, size_t temp_bytes, int n, const SortBuffers& b, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     return rocprim::radix_sort_pairs(temp, temp_bytes, b.keys_in, b.keys_out, b.vals_in, b.vals_out, (size_t)n, 0,
                                      kPathKeyBits, s);
+}
+
+hipError_t sortListBounded(void* temp, size_t temp_bytes, int bound, const int* count, const SortBuffers& b,
+                           hipStream_t s) {
+    if (bound <= 0) return hipSuccess;
+    constexpr int kGrid = 512;  // 128 k lanes: the pad (usually < 2 % of the list) and the rare copy
+    hipLaunchKernelGGL(k_pad_keys, dim3(kGrid), dim3(kB), 0, s, b.keys_in, count, bound);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    // stable LSD sort: a real key equal to the pad's low kPathKeyBits stays ahead of the pads
+    e = rocprim::radix_sort_pairs(temp, temp_bytes, b.keys_in, b.keys_out, b.vals_in, b.vals_out, (size_t)bound, 0,
+                                  kPathKeyBits, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_overflow_copy, dim3(kGrid), dim3(kB), 0, s, (const int*)b.vals_in, b.vals_out, count, bound);
+    return hipGetLastError();
 }
 
 size_t sortAliveTempBytes(int n) {

@@ -93,21 +93,33 @@ __global__ void __launch_bounds__(256) k_assemble(SrcTable src, int world, int w
 
 }  // namespace
 
-struct ort_group {
-    int n = 0;
-    int transport = ORT_GROUP_TRANSPORT_RCCL;
-    std::vector<int> dev;
+// One frame slot: a context per rank (its own scene copy and stream), the band tiles, the
+// gather buffers and the events of one frame in flight.  A group holds `inflight` slots and
+// takes frames in turn on them, so frame k+1's renders fill the tail of frame k's.
+struct GroupSlot {
     std::vector<ort_ctx*> ctx;
     std::vector<hipStream_t> stream;   // each context's own stream
-    std::vector<ncclComm_t> comm;
+    std::vector<ncclComm_t> comm;      // RCCL: this slot's communicators (one gather at a time each)
     std::vector<float*> tile;          // per rank, on its device: rows x W x 3
     std::vector<float*> recv;          // on devices[0]: the band tiles of ranks 1..n-1
     size_t tile_floats = 0;
     float* frame = nullptr;            // devices[0]: the assembled frame (host output path)
     size_t frame_floats = 0;
-    std::vector<hipEvent_t> done;      // per rank: its tile has been sent / copied
+    std::vector<hipEvent_t> done;      // per rank: its tile has been copied (copy transport)
+    hipEvent_t assembled = nullptr;    // devices[0]: the de-interleave has read recv[]
+    hipEvent_t finished = nullptr;     // devices[0]: the frame (and its host copy) is complete
     hipEvent_t t0 = nullptr, t1 = nullptr;
-    bool timed = false;
+    long long ticket = -1;             // the frame last submitted on this slot
+    bool assembled_once = false;
+};
+
+struct ort_group {
+    int n = 0;
+    int transport = ORT_GROUP_TRANSPORT_RCCL;
+    std::vector<int> dev;
+    std::vector<GroupSlot> slot;
+    long long next_ticket = 0;
+    int last_slot = -1;                // slot of the frame ort_group_wait saw complete last
     std::string err;
 };
 
@@ -127,46 +139,65 @@ int gfail(ort_group* g, int code, const std::string& msg) {
                          std::string(#expr) + ": " + hipGetErrorString(_e));                      \
     } while (0)
 
-int each(ort_group* g, int rc, int r) {
-    if (rc != ORT_OK) return gfail(g, rc, "device " + std::to_string(g->dev[r]) + ": " + ort_last_error(g->ctx[r]));
+int each(ort_group* g, ort_ctx* c, int rc, int r) {
+    if (rc != ORT_OK) return gfail(g, rc, "device " + std::to_string(g->dev[r]) + ": " + ort_last_error(c));
     return ORT_OK;
 }
 
-void free_buffers(ort_group* g) {
-    for (int r = 0; r < (int)g->tile.size(); ++r)
-        if (g->tile[r]) {
+void free_buffers(ort_group* g, GroupSlot& S) {
+    for (int r = 0; r < (int)S.tile.size(); ++r)
+        if (S.tile[r]) {
             (void)hipSetDevice(g->dev[r]);
-            (void)hipFree(g->tile[r]);
+            (void)hipFree(S.tile[r]);
         }
-    g->tile.assign(g->n, nullptr);
+    S.tile.assign(g->n, nullptr);
     (void)hipSetDevice(g->dev.empty() ? 0 : g->dev[0]);
-    for (float* p : g->recv)
+    for (float* p : S.recv)
         if (p) (void)hipFree(p);
-    g->recv.assign(g->n, nullptr);
-    if (g->frame) (void)hipFree(g->frame);
-    g->frame = nullptr;
-    g->tile_floats = 0;
-    g->frame_floats = 0;
+    S.recv.assign(g->n, nullptr);
+    if (S.frame) (void)hipFree(S.frame);
+    S.frame = nullptr;
+    S.tile_floats = 0;
+    S.frame_floats = 0;
 }
 
-int ensure_buffers(ort_group* g, size_t tile_floats, size_t frame_floats) {
-    if (tile_floats > g->tile_floats) {
-        free_buffers(g);
+// (Re)allocates a slot's buffers; the slot's previous frame is complete (ort_group_submit).
+int ensure_buffers(ort_group* g, GroupSlot& S, size_t tile_floats, size_t frame_floats) {
+    if (tile_floats > S.tile_floats) {
+        free_buffers(g, S);
         for (int r = 0; r < g->n; ++r) {
             GCHK(g, hipSetDevice(g->dev[r]));
-            GCHK(g, hipMalloc(&g->tile[r], tile_floats * sizeof(float)));
+            GCHK(g, hipMalloc(&S.tile[r], tile_floats * sizeof(float)));
         }
         GCHK(g, hipSetDevice(g->dev[0]));
-        for (int r = 1; r < g->n; ++r) GCHK(g, hipMalloc(&g->recv[r], tile_floats * sizeof(float)));
-        g->tile_floats = tile_floats;
+        for (int r = 1; r < g->n; ++r) GCHK(g, hipMalloc(&S.recv[r], tile_floats * sizeof(float)));
+        S.tile_floats = tile_floats;
     }
-    if (frame_floats > g->frame_floats) {
+    if (frame_floats > S.frame_floats) {
         GCHK(g, hipSetDevice(g->dev[0]));
-        if (g->frame) (void)hipFree(g->frame);
-        g->frame = nullptr;
-        GCHK(g, hipMalloc(&g->frame, frame_floats * sizeof(float)));
-        g->frame_floats = frame_floats;
+        if (S.frame) (void)hipFree(S.frame);
+        S.frame = nullptr;
+        GCHK(g, hipMalloc(&S.frame, frame_floats * sizeof(float)));
+        S.frame_floats = frame_floats;
     }
+    return ORT_OK;
+}
+
+// Every context of every slot.
+template <class F>
+int for_each_ctx(ort_group* g, F f) {
+    for (GroupSlot& S : g->slot)
+        for (int r = 0; r < g->n; ++r) {
+            const int rc = each(g, S.ctx[r], f(S.ctx[r]), r);
+            if (rc) return rc;
+        }
+    return ORT_OK;
+}
+
+int wait_slot(ort_group* g, GroupSlot& S) {
+    if (S.ticket < 0) return ORT_OK;
+    GCHK(g, hipSetDevice(g->dev[0]));
+    GCHK(g, hipEventSynchronize(S.finished));
     return ORT_OK;
 }
 
@@ -174,12 +205,16 @@ int ensure_buffers(ort_group* g, size_t tile_floats, size_t frame_floats) {
 
 extern "C" {
 
-int ort_group_create(const int32_t* devices, int32_t n_devices, int32_t transport, ort_group** out) {
+int ort_group_create_pipelined(const int32_t* devices, int32_t n_devices, int32_t transport, int32_t frames_in_flight,
+                               ort_group** out) {
     if (!out || !devices || n_devices < 1 || n_devices > ORT_GROUP_MAX_DEVICES)
         return gfail(nullptr, ORT_ERR_INVALID_ARG, "ort_group_create: need 1.." + std::to_string(ORT_GROUP_MAX_DEVICES) +
                                                        " devices and an out pointer");
     if (transport != ORT_GROUP_TRANSPORT_RCCL && transport != ORT_GROUP_TRANSPORT_COPY)
         return gfail(nullptr, ORT_ERR_INVALID_ARG, "ort_group_create: unknown transport");
+    if (frames_in_flight < 1 || frames_in_flight > ORT_GROUP_MAX_INFLIGHT)
+        return gfail(nullptr, ORT_ERR_INVALID_ARG, "ort_group_create: frames in flight must be 1.." +
+                                                       std::to_string(ORT_GROUP_MAX_INFLIGHT));
     *out = nullptr;
     if (transport == ORT_GROUP_TRANSPORT_RCCL)
         for (int i = 0; i < n_devices; ++i)
@@ -192,67 +227,83 @@ int ort_group_create(const int32_t* devices, int32_t n_devices, int32_t transpor
     g->n = n_devices;
     g->transport = transport;
     g->dev.assign(devices, devices + n_devices);
-    g->ctx.assign(n_devices, nullptr);
-    g->stream.assign(n_devices, nullptr);
-    g->tile.assign(n_devices, nullptr);
-    g->recv.assign(n_devices, nullptr);
-    g->done.assign(n_devices, nullptr);
+    g->slot.resize(frames_in_flight);
+    for (GroupSlot& S : g->slot) {
+        S.ctx.assign(n_devices, nullptr);
+        S.stream.assign(n_devices, nullptr);
+        S.tile.assign(n_devices, nullptr);
+        S.recv.assign(n_devices, nullptr);
+        S.done.assign(n_devices, nullptr);
+    }
     auto bail = [&](int rc) {
         const std::string m = g->err.empty() ? std::string(ort_last_error(nullptr)) : g->err;
         ort_group_destroy(g);
         ort::set_thread_error(m);
         return rc;
     };
-    for (int r = 0; r < n_devices; ++r) {
-        int rc = ort_create(devices[r], &g->ctx[r]);
-        if (rc != ORT_OK) return bail(rc);
-        void* s = nullptr;
-        ort_get_stream(g->ctx[r], &s);
-        g->stream[r] = (hipStream_t)s;
-        if (hipSetDevice(devices[r]) != hipSuccess || hipEventCreateWithFlags(&g->done[r], hipEventDisableTiming) != hipSuccess)
-            return bail(gfail(g, ORT_ERR_HIP, "ort_group_create: events"));
-    }
-    if (hipSetDevice(devices[0]) != hipSuccess || hipEventCreate(&g->t0) != hipSuccess || hipEventCreate(&g->t1) != hipSuccess)
-        return bail(gfail(g, ORT_ERR_HIP, "ort_group_create: timing events"));
-    if (transport == ORT_GROUP_TRANSPORT_RCCL) {
-        std::string why;
-        const Rccl& R = rccl(why);
-        if (!R.so) return bail(gfail(g, ORT_ERR_UNSUPPORTED, "ort_group_create: " + why));
-        g->comm.assign(n_devices, nullptr);
-        const ncclResult_t e = R.commInitAll(g->comm.data(), n_devices, g->dev.data());
-        if (e != ncclSuccess) {
-            g->comm.clear();
-            return bail(gfail(g, ORT_ERR_HIP, std::string("ncclCommInitAll: ") + R.errorString(e)));
+    for (GroupSlot& S : g->slot) {
+        for (int r = 0; r < n_devices; ++r) {
+            int rc = ort_create(devices[r], &S.ctx[r]);
+            if (rc != ORT_OK) return bail(rc);
+            void* s = nullptr;
+            ort_get_stream(S.ctx[r], &s);
+            S.stream[r] = (hipStream_t)s;
+            if (hipSetDevice(devices[r]) != hipSuccess ||
+                hipEventCreateWithFlags(&S.done[r], hipEventDisableTiming) != hipSuccess)
+                return bail(gfail(g, ORT_ERR_HIP, "ort_group_create: events"));
+        }
+        if (hipSetDevice(devices[0]) != hipSuccess || hipEventCreate(&S.t0) != hipSuccess ||
+            hipEventCreate(&S.t1) != hipSuccess ||
+            hipEventCreateWithFlags(&S.assembled, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&S.finished, hipEventDisableTiming) != hipSuccess)
+            return bail(gfail(g, ORT_ERR_HIP, "ort_group_create: timing events"));
+        if (transport == ORT_GROUP_TRANSPORT_RCCL) {
+            std::string why;
+            const Rccl& R = rccl(why);
+            if (!R.so) return bail(gfail(g, ORT_ERR_UNSUPPORTED, "ort_group_create: " + why));
+            S.comm.assign(n_devices, nullptr);
+            const ncclResult_t e = R.commInitAll(S.comm.data(), n_devices, g->dev.data());
+            if (e != ncclSuccess) {
+                S.comm.clear();
+                return bail(gfail(g, ORT_ERR_HIP, std::string("ncclCommInitAll: ") + R.errorString(e)));
+            }
         }
     }
     *out = g;
     return ORT_OK;
 }
 
+int ort_group_create(const int32_t* devices, int32_t n_devices, int32_t transport, ort_group** out) {
+    return ort_group_create_pipelined(devices, n_devices, transport, 1, out);
+}
+
 int ort_group_destroy(ort_group* g) {
     if (!g) return ORT_OK;
-    for (int r = 0; r < g->n; ++r)
-        if (g->ctx[r]) {
-            (void)hipSetDevice(g->dev[r]);
-            (void)hipStreamSynchronize(g->stream[r]);
+    for (GroupSlot& S : g->slot)
+        for (int r = 0; r < g->n; ++r)
+            if (S.ctx[r]) {
+                (void)hipSetDevice(g->dev[r]);
+                (void)hipStreamSynchronize(S.stream[r]);
+            }
+    for (GroupSlot& S : g->slot) {
+        if (!S.comm.empty()) {
+            std::string why;
+            const Rccl& R = rccl(why);
+            for (ncclComm_t c : S.comm)
+                if (c && R.so) (void)R.commDestroy(c);
         }
-    if (!g->comm.empty()) {
-        std::string why;
-        const Rccl& R = rccl(why);
-        for (ncclComm_t c : g->comm)
-            if (c && R.so) (void)R.commDestroy(c);
-    }
-    free_buffers(g);
-    for (int r = 0; r < g->n; ++r) {
-        if (g->done[r]) {
-            (void)hipSetDevice(g->dev[r]);
-            (void)hipEventDestroy(g->done[r]);
+        free_buffers(g, S);
+        for (int r = 0; r < g->n; ++r) {
+            if (S.done[r]) {
+                (void)hipSetDevice(g->dev[r]);
+                (void)hipEventDestroy(S.done[r]);
+            }
+            if (S.ctx[r]) ort_destroy(S.ctx[r]);
         }
-        if (g->ctx[r]) ort_destroy(g->ctx[r]);
+        if (!g->dev.empty()) (void)hipSetDevice(g->dev[0]);
+        for (hipEvent_t e : {S.t0, S.t1, S.assembled, S.finished})
+            if (e) (void)hipEventDestroy(e);
     }
-    if (!g->dev.empty()) (void)hipSetDevice(g->dev[0]);
-    if (g->t0) (void)hipEventDestroy(g->t0);
-    if (g->t1) (void)hipEventDestroy(g->t1);
     delete g;
     return ORT_OK;
 }
@@ -261,19 +312,17 @@ const char* ort_group_last_error(const ort_group* g) { return g ? g->err.c_str()
 
 int ort_group_size(const ort_group* g) { return g ? g->n : 0; }
 
+int ort_group_frames_in_flight(const ort_group* g) { return g ? (int)g->slot.size() : 0; }
+
 int ort_group_context(ort_group* g, int32_t rank, ort_ctx** ctx) {
     if (!g || !ctx || rank < 0 || rank >= g->n) return gfail(g, ORT_ERR_INVALID_ARG, "ort_group_context: bad rank");
-    *ctx = g->ctx[rank];
+    *ctx = g->slot[0].ctx[rank];
     return ORT_OK;
 }
 
 int ort_group_set_option(ort_group* g, int option, int value) {
     if (!g) return gfail(nullptr, ORT_ERR_INVALID_ARG, "ort_group_set_option: null group");
-    for (int r = 0; r < g->n; ++r) {
-        const int rc = each(g, ort_set_option(g->ctx[r], option, value), r);
-        if (rc) return rc;
-    }
-    return ORT_OK;
+    return for_each_ctx(g, [&](ort_ctx* c) { return ort_set_option(c, option, value); });
 }
 
 int ort_group_upload_scene(ort_group* g, const float* cr, const float* ma, const float* fr, int32_t n_spheres,
@@ -281,39 +330,40 @@ int ort_group_upload_scene(ort_group* g, const float* cr, const float* ma, const
                            const int32_t* objects_offset, const int32_t* object_count, int32_t n_nodes,
                            const int32_t* object_indices, int64_t n_indices) {
     if (!g) return gfail(nullptr, ORT_ERR_INVALID_ARG, "ort_group_upload_scene: null group");
-    for (int r = 0; r < g->n; ++r) {
-        const int rc = each(g, ort_upload_scene(g->ctx[r], cr, ma, fr, n_spheres, node_min, node_max, children_offset,
-                                                objects_offset, object_count, n_nodes, object_indices, n_indices), r);
-        if (rc) return rc;
-    }
-    return ORT_OK;
+    return for_each_ctx(g, [&](ort_ctx* c) {
+        return ort_upload_scene(c, cr, ma, fr, n_spheres, node_min, node_max, children_offset, objects_offset,
+                                object_count, n_nodes, object_indices, n_indices);
+    });
 }
 
 int ort_group_build_scene(ort_group* g, const float* cr, const float* ma, const float* fr, int32_t n_spheres,
                           int32_t max_depth, int32_t max_spheres_per_node) {
     if (!g) return gfail(nullptr, ORT_ERR_INVALID_ARG, "ort_group_build_scene: null group");
-    for (int r = 0; r < g->n; ++r) {
-        const int rc = each(g, ort_build_scene(g->ctx[r], cr, ma, fr, n_spheres, max_depth, max_spheres_per_node, 0), r);
-        if (rc) return rc;
-    }
-    return ORT_OK;
+    return for_each_ctx(g, [&](ort_ctx* c) {
+        return ort_build_scene(c, cr, ma, fr, n_spheres, max_depth, max_spheres_per_node, 0);
+    });
 }
 
-int ort_group_render(ort_group* g, const ort_params* p, float* rgb_out, int32_t out_is_device) {
-    if (!g || !p) return gfail(g, ORT_ERR_INVALID_ARG, "ort_group_render: null argument");
-    if (!rgb_out) return gfail(g, ORT_ERR_INVALID_ARG, "ort_group_render: null output");
-    if (p->width <= 0 || p->height <= 0) return gfail(g, ORT_ERR_INVALID_ARG, "ort_group_render: width/height must be positive");
+int ort_group_submit(ort_group* g, const ort_params* p, float* rgb_out, int32_t out_is_device, int64_t* ticket) {
+    if (!g || !p) return gfail(g, ORT_ERR_INVALID_ARG, "ort_group_submit: null argument");
+    if (!rgb_out) return gfail(g, ORT_ERR_INVALID_ARG, "ort_group_submit: null output");
+    if (p->width <= 0 || p->height <= 0) return gfail(g, ORT_ERR_INVALID_ARG, "ort_group_submit: width/height must be positive");
     const int W = p->width, H = p->height, N = g->n;
+    const long long tk = g->next_ticket;
+    GroupSlot& S = g->slot[(size_t)(tk % (long long)g->slot.size())];
+    int rc;
+    // the slot's previous frame must be complete before its buffers are reused
+    if ((rc = wait_slot(g, S))) return rc;
     const ort_tile t0 = ort::group_tile(W, H, 0, N);
     const size_t tile_floats = (size_t)t0.rows * W * 3, frame_floats = (size_t)H * W * 3;
-    int rc;
-    if ((rc = ensure_buffers(g, tile_floats, out_is_device ? 0 : frame_floats))) return rc;
+    if ((rc = ensure_buffers(g, S, tile_floats, out_is_device ? 0 : frame_floats))) return rc;
     GCHK(g, hipSetDevice(g->dev[0]));
-    GCHK(g, hipEventRecord(g->t0, g->stream[0]));
-    // 1. every rank renders its bands on its own stream (asynchronous)
+    GCHK(g, hipEventRecord(S.t0, S.stream[0]));
+    // 1. every rank renders its bands on its own stream: ort_render with a stream never waits
+    //    on the host (also for multi-bounce frames), so every rank is enqueued before any runs
     for (int r = 0; r < N; ++r) {
         const ort_tile t = ort::group_tile(W, H, r, N);
-        if ((rc = each(g, ort_render(g->ctx[r], p, &t, g->tile[r], 1, g->stream[r]), r))) return rc;
+        if ((rc = each(g, S.ctx[r], ort_render(S.ctx[r], p, &t, S.tile[r], 1, S.stream[r]), r))) return rc;
     }
     // 2. the one exchange: bands of ranks 1..N-1 to devices[0]
     if (N > 1) {
@@ -322,8 +372,8 @@ int ort_group_render(ort_group* g, const ort_params* p, float* rgb_out, int32_t 
             const Rccl& R = rccl(why);
             ncclResult_t e = R.groupStart();
             for (int r = 1; r < N && e == ncclSuccess; ++r) {
-                e = R.send(g->tile[r], tile_floats, ncclFloat32, 0, g->comm[r], g->stream[r]);
-                if (e == ncclSuccess) e = R.recv(g->recv[r], tile_floats, ncclFloat32, r, g->comm[0], g->stream[0]);
+                e = R.send(S.tile[r], tile_floats, ncclFloat32, 0, S.comm[r], S.stream[r]);
+                if (e == ncclSuccess) e = R.recv(S.recv[r], tile_floats, ncclFloat32, r, S.comm[0], S.stream[0]);
             }
             const ncclResult_t e2 = R.groupEnd();
             if (e != ncclSuccess || e2 != ncclSuccess)
@@ -331,41 +381,65 @@ int ort_group_render(ort_group* g, const ort_params* p, float* rgb_out, int32_t 
         } else {
             for (int r = 1; r < N; ++r) {
                 GCHK(g, hipSetDevice(g->dev[r]));
-                GCHK(g, hipMemcpyPeerAsync(g->recv[r], g->dev[0], g->tile[r], g->dev[r], tile_floats * sizeof(float),
-                                           g->stream[r]));
-                GCHK(g, hipEventRecord(g->done[r], g->stream[r]));
+                // recv[r] is free once this slot's previous assembly has read it
+                if (S.assembled_once) GCHK(g, hipStreamWaitEvent(S.stream[r], S.assembled, 0));
+                GCHK(g, hipMemcpyPeerAsync(S.recv[r], g->dev[0], S.tile[r], g->dev[r], tile_floats * sizeof(float),
+                                           S.stream[r]));
+                GCHK(g, hipEventRecord(S.done[r], S.stream[r]));
                 GCHK(g, hipSetDevice(g->dev[0]));
-                GCHK(g, hipStreamWaitEvent(g->stream[0], g->done[r], 0));
+                GCHK(g, hipStreamWaitEvent(S.stream[0], S.done[r], 0));
             }
         }
     }
     // 3. de-interleave on devices[0]
     GCHK(g, hipSetDevice(g->dev[0]));
     SrcTable src{};
-    src.tile[0] = g->tile[0];
-    for (int r = 1; r < N; ++r) src.tile[r] = g->recv[r];
-    float* dst = out_is_device ? rgb_out : g->frame;
-    hipLaunchKernelGGL(k_assemble, dim3((unsigned)H), dim3(256), 0, g->stream[0], src, N, W, H, dst);
+    src.tile[0] = S.tile[0];
+    for (int r = 1; r < N; ++r) src.tile[r] = S.recv[r];
+    float* dst = out_is_device ? rgb_out : S.frame;
+    hipLaunchKernelGGL(k_assemble, dim3((unsigned)H), dim3(256), 0, S.stream[0], src, N, W, H, dst);
     GCHK(g, hipGetLastError());
-    GCHK(g, hipEventRecord(g->t1, g->stream[0]));
-    g->timed = true;
-    if (!out_is_device) GCHK(g, hipMemcpyAsync(rgb_out, g->frame, frame_floats * sizeof(float), hipMemcpyDeviceToHost,
-                                               g->stream[0]));
-    // synchronous, like ort_render without a stream: every rank's stream has passed the frame
-    for (int r = 0; r < N; ++r) {
-        GCHK(g, hipSetDevice(g->dev[r]));
-        GCHK(g, hipStreamSynchronize(g->stream[r]));
-    }
-    GCHK(g, hipSetDevice(g->dev[0]));
+    GCHK(g, hipEventRecord(S.assembled, S.stream[0]));
+    S.assembled_once = true;
+    GCHK(g, hipEventRecord(S.t1, S.stream[0]));
+    if (!out_is_device)  // pageable rgb_out: the runtime may stage this copy synchronously
+        GCHK(g, hipMemcpyAsync(rgb_out, S.frame, frame_floats * sizeof(float), hipMemcpyDeviceToHost, S.stream[0]));
+    GCHK(g, hipEventRecord(S.finished, S.stream[0]));
+    S.ticket = tk;
+    g->next_ticket = tk + 1;
+    if (ticket) *ticket = tk;
     return ORT_OK;
+}
+
+int ort_group_wait(ort_group* g, int64_t ticket) {
+    if (!g) return gfail(nullptr, ORT_ERR_INVALID_ARG, "ort_group_wait: null group");
+    if (ticket < 0 || ticket >= g->next_ticket) return gfail(g, ORT_ERR_INVALID_ARG, "ort_group_wait: no such frame");
+    const int si = (int)(ticket % (long long)g->slot.size());
+    GroupSlot& S = g->slot[(size_t)si];
+    if (S.ticket != ticket) return ORT_OK;  // the slot took a later frame, so this one completed
+    int rc;
+    if ((rc = wait_slot(g, S))) return rc;
+    g->last_slot = si;
+    return ORT_OK;
+}
+
+int ort_group_render(ort_group* g, const ort_params* p, float* rgb_out, int32_t out_is_device) {
+    int64_t tk = -1;
+    int rc = ort_group_submit(g, p, rgb_out, out_is_device, &tk);
+    if (rc) return rc;
+    // synchronous, like ort_render without a stream: every earlier frame has completed too
+    for (GroupSlot& S : g->slot)
+        if ((rc = wait_slot(g, S))) return rc;
+    return ort_group_wait(g, tk);
 }
 
 int ort_group_last_frame_ms(ort_group* g, float* ms) {
     if (!g || !ms) return gfail(g, ORT_ERR_INVALID_ARG, "ort_group_last_frame_ms: null argument");
-    if (!g->timed) return gfail(g, ORT_ERR_NO_SCENE, "no frame rendered yet");
+    if (g->last_slot < 0) return gfail(g, ORT_ERR_NO_SCENE, "no frame completed yet (ort_group_wait)");
+    GroupSlot& S = g->slot[(size_t)g->last_slot];
     GCHK(g, hipSetDevice(g->dev[0]));
-    GCHK(g, hipEventSynchronize(g->t1));
-    GCHK(g, hipEventElapsedTime(ms, g->t0, g->t1));
+    GCHK(g, hipEventSynchronize(S.t1));
+    GCHK(g, hipEventElapsedTime(ms, S.t0, S.t1));
     return ORT_OK;
 }
 

@@ -1028,6 +1028,14 @@ struct ort_ctx {
     // bits ~ slot order, octant + direction bits and 16-bit atomic buckets slower than slot
     // order, a block-local sort of 4096-entry runs (rocprim block_radix_sort) 55.4 ms.
     int sort_paths = 2;
+    // The list sort without a host wait (sortListBounded): its size is a host-side bound, the
+    // list's length from the same bounce of an earlier frame (read back asynchronously into
+    // pinned memory: alive_host[sample * bounces + bounce]) plus a margin; a longer list goes
+    // on unsorted (same pixels).  hint_sig: the frame shape the hints belong to.
+    static constexpr int kHints = 64;
+    int* alive_host = nullptr;
+    unsigned long long hint_sig = 0;
+    int sort_bound = 0;  // ORT_OPT_SORT_BOUND (testing): > 0 forces this bound
     float root_lo[3] = {0, 0, 0}, root_hi[3] = {0, 0, 0};  // root box (coherence-sort key)
     DevBuf lut;         // rank LUT (global copy, for the packet kernel)
     ort::GpuTree tree;  // reference-layout tree of the last ort_build_scene(keep_tree)
@@ -1514,6 +1522,17 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
         if (listsort && ((rc = ensure(ctx, ctx->skeys, 4 * slots)) || (rc = ensure(ctx, ctx->skeys2, 4 * slots)) ||
                          (rc = ensure(ctx, ctx->svals, 4 * slots))))
             return rc;
+        if (listsort) {  // the list-length hints belong to one frame shape and scene
+            const long long v[] = {p->width, p->height, p->num_samples, p->max_depth, t->x0, t->width, t->y0,
+                                   t->rows, t->band_height, t->band_stride, ctx->n_nodes, ctx->n_spheres,
+                                   (long long)ctx->n_indices};
+            unsigned long long sig = 1469598103934665603ull;
+            for (long long x : v) sig = (sig ^ (unsigned long long)x) * 1099511628211ull;
+            if (sig != ctx->hint_sig) {
+                for (int i = 0; i < ort_ctx::kHints; ++i) ctx->alive_host[i] = -1;
+                ctx->hint_sig = sig;
+            }
+        }
         if (sorted || listsort) {  // the key tables of the current root box (built once per scene)
             const float box[6] = {ctx->root_lo[0], ctx->root_lo[1], ctx->root_lo[2],
                                   ctx->root_hi[0], ctx->root_hi[1], ctx->root_hi[2]};
@@ -1662,16 +1681,26 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                 } else {
                     cur ^= 1;  // the list just appended is the next bounce's
                     if (listsort) {
-                        // the list's length, read back (one host wait per bounce): the sort then
-                        // costs the alive paths only, not every slot (C5: 36.6 M keys, not 99.6 M)
-                        int n_alive = 0;
-                        HIPCHK(ctx, hipMemcpyAsync(&n_alive, qcnt[cur], sizeof(int), hipMemcpyDeviceToHost, s));
-                        HIPCHK(ctx, hipStreamSynchronize(s));
+                        // sort only about the alive paths, not every slot (C5: 36.6 M keys, not
+                        // 99.6 M), without reading the length back: the bound is this bounce's
+                        // length in an earlier frame of the same shape plus 1/64 + 1024 (the
+                        // same camera gives the same length), every slot when there is none
+                        const int hi = smp * bounces + b;
+                        long long bound = (long long)slots;
+                        if (ctx->sort_bound > 0) bound = ctx->sort_bound;
+                        else if (hi < ort_ctx::kHints) {
+                            const int h = ((volatile int*)ctx->alive_host)[hi];
+                            if (h >= 0) bound = (long long)h + (h >> 6) + 1024;
+                        }
+                        bound = std::min<long long>(bound, (long long)slots);
                         // (key, path) pairs as the shade / trace kernels appended them
                         const ort::SortBuffers sb{(uint32_t*)ctx->skeys.p, (uint32_t*)ctx->skeys2.p, qbuf[cur],
                                                   (int*)ctx->svals.p};
-                        e = ort::sortList(ctx->qtemp.p, qtemp_bytes, n_alive, sb, s);
+                        e = ort::sortListBounded(ctx->qtemp.p, qtemp_bytes, (int)bound, qcnt[cur], sb, s);
                         if (e != hipSuccess) return hip_fail(ctx, e, "path list sort");
+                        if (hi < ort_ctx::kHints)  // the next frame's bound (pinned: no host wait)
+                            HIPCHK(ctx, hipMemcpyAsync(ctx->alive_host + hi, qcnt[cur], sizeof(int),
+                                                       hipMemcpyDeviceToHost, s));
                     }
                     a.qlist = listsort ? (const int*)ctx->svals.p : qbuf[cur];
                     a.qcount = qcnt[cur];
@@ -1724,6 +1753,13 @@ int ort_create(int device, ort_ctx** out) {
             return rc;
         }
     }
+    if ((e = hipHostMalloc((void**)&c->alive_host, sizeof(int) * ort_ctx::kHints, hipHostMallocDefault)) != hipSuccess) {
+        c->alive_host = nullptr;
+        const int rc = hip_fail(nullptr, e, "ort_create: pinned hint buffer");
+        ort_destroy(c);
+        return rc;
+    }
+    for (int i = 0; i < ort_ctx::kHints; ++i) c->alive_host[i] = -1;
     {
         std::vector<uint8_t> lut(kRankLutBytes);
         for (size_t i = 0; i < lut.size(); ++i) lut[i] = ort::rank_lut_entry((uint32_t)i >> 8, (uint32_t)i & 255u);
@@ -1759,6 +1795,7 @@ int ort_destroy(ort_ctx* ctx) {
             if (ctx->tr1[i][j]) (void)hipEventDestroy(ctx->tr1[i][j]);
         }
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    if (ctx->alive_host) (void)hipHostFree(ctx->alive_host);
     delete ctx;
     return ORT_OK;
 }
@@ -1798,6 +1835,11 @@ int ort_set_option(ort_ctx* ctx, int option, int value) {
     if (option == ORT_OPT_SORT_PATHS) {
         if (value < 0 || value > 2) return fail(ctx, ORT_ERR_INVALID_ARG, "sort_paths must be 0, 1 or 2");
         ctx->sort_paths = value;
+        return ORT_OK;
+    }
+    if (option == ORT_OPT_SORT_BOUND) {
+        if (value < 0) return fail(ctx, ORT_ERR_INVALID_ARG, "ORT_OPT_SORT_BOUND must be >= 0");
+        ctx->sort_bound = value;
         return ORT_OK;
     }
     if (option == ORT_OPT_REFILL) {

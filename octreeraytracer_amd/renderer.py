@@ -129,7 +129,9 @@ class Renderer:
 
     def set_sort_paths(self, mode: int):
         """Order of the alive paths between bounces (same pixels): 0 slot order, 1 radix sort of
-        every slot by coherence key, 2 bucket order of the alive list (key's top 16 bits)."""
+        every slot by coherence key, 2 (default) full-key radix sort of the appended alive list,
+        sized by the same bounce's list length in the previous frame of this shape (+1/64 + 1024;
+        a longer list goes on unsorted) -- no host wait (include/ort.h ORT_OPT_SORT_PATHS)."""
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_SORT_PATHS, int(mode)))
 
     def set_persistent(self, on):
@@ -142,6 +144,10 @@ class Renderer:
         1 on (node records and kid entries from the interleaved copy), 2 on with the two
         separate arrays (testing)."""
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_KID_SKIP, int(mode)))
+
+    def set_sort_bound(self, bound: int):
+        """Testing (ORT_OPT_SORT_BOUND): force the list sort's size; 0 = the previous-frame hint."""
+        self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_SORT_BOUND, int(bound)))
 
     def set_refill(self, lanes: int):
         """Persistent trace: refill a wave once at least `lanes` of its 64 lanes are idle."""
@@ -220,7 +226,9 @@ class Renderer:
         if out is None:
             out = np.empty((tile.rows, tile.width, 3), np.float32)
         if isinstance(out, np.ndarray):
-            assert out.dtype == np.float32 and out.flags.c_contiguous and out.size >= tile.rows * tile.width * 3
+            if out.dtype != np.float32 or not out.flags.c_contiguous or out.size < tile.rows * tile.width * 3:
+                raise ValueError(f"render: out must be a C-contiguous float32 array of >= {tile.rows * tile.width * 3} "
+                                 f"elements (got {out.dtype}, {out.size}, contiguous={out.flags.c_contiguous})")
             self._check(self._lib.ort_render(self._ctx, C.byref(p), C.byref(t), out.ctypes.data_as(C.c_void_p), 0, s))
             return out
         ptr = out.data_ptr() if hasattr(out, "data_ptr") else int(out)
