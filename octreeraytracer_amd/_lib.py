@@ -136,6 +136,7 @@ def _declare(lib):
         "ort_group_wait": (C.c_int, [_vp, C.c_int64]),
         "ort_debug_group_emulate": (C.c_int, [_fp, _fp, _fp, C.c_int32, _fp, _fp, _ip, _ip, _ip, C.c_int32, _ip, C.c_int64,
                                               C.c_int32, C.POINTER(OrtParams), _fp]),
+        "ort_debug_fast_order": (C.c_int, [C.c_int32, _ip, C.POINTER(C.c_uint8)]),
         "ort_debug_emulate_render": (C.c_int, [_fp, _fp, _fp, C.c_int32, _fp, _fp, _ip, _ip, _ip, C.c_int32, _ip,
                                                C.c_int64, C.c_int32, C.POINTER(OrtParams), C.POINTER(OrtTile),
                                                _fp, _u64p]),

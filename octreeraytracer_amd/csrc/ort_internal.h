@@ -28,6 +28,11 @@ int ort_debug_group_emulate(const float* sphere_center_radius, const float* sphe
                             const float* node_max, const int32_t* children_offset, const int32_t* objects_offset,
                             const int32_t* object_count, int32_t n_nodes, const int32_t* object_indices,
                             int64_t n_indices, int32_t world, const ort_params* params, float* rgb_out);
+// TEST-ONLY: the fast walk's traversal order for direction-sign mask m = (d.z<0)<<2 |
+// (d.x<0)<<1 | (d.y<0) (render_core.h rank_perm: order[r] = perm(r) ^ m) and its rank LUT
+// rows (rank_lut_entry) for every child mask: lut256[cmask] (checked against the shader's
+// tables, tests/golden/traversal_orders.json).
+int ort_debug_fast_order(int32_t m, int32_t* order8, uint8_t* lut256);
 // ANALYSIS-ONLY: lane overlap of sampled 8x8 primary-ray blocks (tools/wave_stats.py).
 int ort_debug_wave_stats(const float* sphere_center_radius, const float* sphere_mat_albedo,
                          const float* sphere_fuzz_ri, int32_t n_spheres, const float* node_min,

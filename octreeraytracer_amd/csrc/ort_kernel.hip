@@ -2034,6 +2034,14 @@ int ort_count_traffic(ort_ctx* ctx, const ort_params* params, const ort_tile* ti
 }
 
 // ---- TEST-ONLY host emulation (see ort_internal.h) ----------------------------------
+int ort_debug_fast_order(int32_t m, int32_t* order8, uint8_t* lut256) {
+    if (m < 0 || m > 7 || !order8) return fail(nullptr, ORT_ERR_INVALID_ARG, "ort_debug_fast_order: m in 0..7");
+    for (uint32_t r = 0; r < 8; ++r) order8[r] = (int32_t)ort::rank_perm(r, (uint32_t)m);
+    if (lut256)
+        for (uint32_t c = 0; c < 256; ++c) lut256[c] = ort::rank_lut_entry((uint32_t)m, c);
+    return ORT_OK;
+}
+
 int ort_debug_emulate_render(const float* cr, const float* ma, const float* fr, int32_t n_spheres,
                              const float* node_min, const float* node_max, const int32_t* co, const int32_t* oo,
                              const int32_t* cnt, int32_t n_nodes, const int32_t* idx, int64_t n_indices,

@@ -18,14 +18,18 @@ TRANSPORT_COPY = L.ORT_GROUP_TRANSPORT_COPY
 
 
 class RenderGroup:
-    def __init__(self, devices, transport: int = TRANSPORT_RCCL):
+    def __init__(self, devices, transport: int = TRANSPORT_RCCL, inflight: int = 1):
+        """inflight: frame slots (ort_group_create_pipelined): submit() returns at once and
+        frame k+1 renders while frame k's last blocks finish."""
         self._lib = L.lib()
         self._g = C.c_void_p()
         devs = (C.c_int32 * len(devices))(*[int(d) for d in devices])
-        rc = self._lib.ort_group_create(devs, len(devices), int(transport), C.byref(self._g))
+        rc = self._lib.ort_group_create_pipelined(devs, len(devices), int(transport), int(inflight),
+                                                  C.byref(self._g))
         if rc != L.ORT_OK:
             raise L.OrtError(rc, self._lib.ort_group_last_error(None).decode())
         self.devices = list(devices)
+        self.inflight = int(inflight)
 
     def _check(self, rc):
         if rc != L.ORT_OK:
@@ -67,27 +71,44 @@ class RenderGroup:
                                                      L.fptr(t[0]), L.fptr(t[1]), L.iptr(t[2]), L.iptr(t[3]),
                                                      L.iptr(t[4]), tree.n_nodes, L.iptr(t[5]), tree.n_indices))
 
-    def render(self, params: FrameParams, out=None):
-        """Full frame: a new (H, W, 3) float32 numpy array, a numpy array, or a float32 torch
-        tensor on devices[0] (device output)."""
-        p = params.to_c()
+    def _out(self, params: FrameParams, out):
         n = params.height * params.width * 3
         if out is None:
             out = np.empty((params.height, params.width, 3), np.float32)
         if isinstance(out, np.ndarray):
             if out.dtype != np.float32 or not out.flags.c_contiguous or out.size < n:
                 raise ValueError("render: out must be a contiguous float32 array of H*W*3 elements")
-            self._check(self._lib.ort_group_render(self._g, C.byref(p), out.ctypes.data_as(C.c_void_p), 0))
-            return out
+            return out, out.ctypes.data_as(C.c_void_p), 0
         import torch
         if out.dtype != torch.float32 or not out.is_contiguous() or out.numel() < n:
             raise ValueError("render: out must be a contiguous float32 tensor of H*W*3 elements")
         if out.device.type != "cuda" or out.device.index != self.devices[0]:
             raise ValueError(f"render: out is on {out.device}, the group assembles on cuda:{self.devices[0]}")
-        self._check(self._lib.ort_group_render(self._g, C.byref(p), C.c_void_p(out.data_ptr()), 1))
+        return out, C.c_void_p(out.data_ptr()), 1
+
+    def render(self, params: FrameParams, out=None):
+        """Full frame: a new (H, W, 3) float32 numpy array, a numpy array, or a float32 torch
+        tensor on devices[0] (device output).  Synchronous."""
+        p = params.to_c()
+        out, ptr, dev = self._out(params, out)
+        self._check(self._lib.ort_group_render(self._g, C.byref(p), ptr, dev))
         return out
 
+    def submit(self, params: FrameParams, out) -> int:
+        """Enqueue a frame into `out` (as render(); keep it untouched until wait(ticket)) and
+        return its ticket at once (ort_group_submit)."""
+        p = params.to_c()
+        _, ptr, dev = self._out(params, out)
+        tk = C.c_int64(-1)
+        self._check(self._lib.ort_group_submit(self._g, C.byref(p), ptr, dev, C.byref(tk)))
+        return tk.value
+
+    def wait(self, ticket: int):
+        """Block until frame `ticket` is complete in its output (ort_group_wait)."""
+        self._check(self._lib.ort_group_wait(self._g, C.c_int64(int(ticket))))
+
     def last_frame_ms(self) -> float:
+        """Latency (device time on devices[0]) of the last frame seen complete."""
         ms = C.c_float()
         self._check(self._lib.ort_group_last_frame_ms(self._g, C.byref(ms)))
         return ms.value

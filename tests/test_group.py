@@ -83,3 +83,40 @@ def test_group_errors(ort):
         RenderGroup([], 1)
     with pytest.raises(ort.OrtError):
         RenderGroup([0], 7)  # unknown transport
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("inflight", [2, 3])
+def test_group_pipelined_frames(ort, oracle, scene_c2, inflight):
+    """ort_group_submit / ort_group_wait with frame slots on [0, 0, 0, 0] (copy transport): a
+    stream of frames with changing cameras and bounce depths, several in flight, each equal to
+    a single-context render bit for bit (the slot buffers are reused only after their frame)."""
+    torch = pytest.importorskip("torch")
+    from octreeraytracer_amd.group import RenderGroup
+    s, t = scene_c2
+    W, H = 1920, 1080
+    shots = []
+    for k in range(7):
+        pos = (0.3 * k, 2.5, -10.0 + 0.5 * k)
+        shots.append(ort.FrameParams.default_camera(W, H, max_depth=1 + (k % 3), position=pos, yaw=-90.0 + 2 * k))
+    with ort.Renderer(0) as r:
+        r.upload(s, t)
+        want = [r.render(p) for p in shots]
+    with RenderGroup([0, 0, 0, 0], 1, inflight=inflight) as g:
+        g.upload(s, t)
+        outs = [torch.empty((H, W, 3), dtype=torch.float32, device="cuda:0") for _ in shots]
+        host = np.empty((H, W, 3), np.float32)
+        tickets = [g.submit(p, o) for p, o in zip(shots, outs)]
+        assert tickets == list(range(len(shots)))
+        for tk in tickets:
+            g.wait(tk)
+        assert g.last_frame_ms() > 0
+        for k, (o, w) in enumerate(zip(outs, want)):
+            assert np.array_equal(o.cpu().numpy().view(np.uint32), w.view(np.uint32)), k
+        tk = g.submit(shots[2], host)  # host output through a slot
+        g.wait(tk)
+        assert np.array_equal(host.view(np.uint32), want[2].view(np.uint32))
+        ref = oracle.render(s, t, shots[0], 0, 500, W, 40)
+        assert np.array_equal(outs[0].cpu().numpy()[500:540].view(np.uint32), ref.view(np.uint32))
+        with pytest.raises(ort.OrtError):
+            g.wait(99)

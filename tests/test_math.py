@@ -1,5 +1,6 @@
 """Known-answer tests of the canonical builtins (include/ort_math.h) and shader tables."""
 import json
+import sys
 import math
 from pathlib import Path
 
@@ -74,28 +75,63 @@ def test_rand2D_first_value_by_hand(oracle):
     assert oracle.rand_sequence(0.25, 0.75, 1)[0] == v
 
 
-# traversal orders of glsl:352-447 for every non-zero sign vector
-GLSL_ORDERS = {
-    "cyan": ([0, 1, 2, 3, 4, 5, 6, 7], [(1, 1, 1)]),
-    "yellow": ([2, 0, 3, 1, 6, 4, 7, 5], [(-1, 1, 1), (-1, 1, 0), (0, 1, 0), (0, 1, 1)]),
-    "red": ([3, 1, 2, 0, 7, 5, 6, 4], [(-1, -1, 1), (-1, 0, 1), (0, 0, 1), (0, -1, 1), (-1, -1, 0), (0, -1, 0),
-                                        (-1, 0, 0)]),
-    "dark purple": ([1, 0, 3, 2, 5, 4, 7, 6], [(1, -1, 1), (1, 0, 1), (1, -1, 0), (1, 0, 0)]),
-    "blue": ([4, 5, 6, 7, 0, 1, 2, 3], [(1, 1, -1), (1, 0, -1), (0, 1, -1), (1, 1, 0)]),
-    "purple": ([6, 4, 7, 5, 2, 0, 3, 1], [(-1, 1, -1)]),
-    "green": ([7, 5, 6, 4, 3, 1, 2, 0], [(-1, -1, -1), (-1, 0, -1), (0, -1, -1), (0, 0, -1)]),
-    "black": ([5, 4, 7, 6, 1, 0, 3, 2], [(1, -1, -1)]),
-}
+# traversal orders of glsl:352-447 for every non-zero sign vector, derived from the shader file
+# itself by tools/extract_orders.py (not hand-typed)
+GOLDEN_ORDERS = Path(__file__).resolve().parent / "golden" / "traversal_orders.json"
+
+
+def _clauses():
+    return json.loads(GOLDEN_ORDERS.read_text())["clauses"]
 
 
 def test_traversal_order_table_covers_26_sign_vectors(oracle):
+    """The oracle's table (oracle/ort_oracle.c traversal_order) equals the shader's, clause by
+    clause, for all 26 non-zero sign vectors."""
     seen = set()
-    for order, vecs in GLSL_ORDERS.values():
-        for v in vecs:
-            assert oracle.traversal_order(tuple(0.3 * c for c in v)) == order, v
-            seen.add(v)
-    assert len(seen) == 26
+    for c in _clauses():
+        for v in c["sign_vectors"]:
+            assert oracle.traversal_order(tuple(0.3 * x for x in v)) == c["order"], (c["name"], v)
+            seen.add(tuple(v))
+    assert len(seen) == 26 and (0, 0, 0) not in seen
     # SURVEY.md 8(c) examples (shader table, not test.py's formula)
     assert oracle.traversal_order((-1, 0, 0)) == [3, 1, 2, 0, 7, 5, 6, 4]
     assert oracle.traversal_order((-1, -1, -1)) == [7, 5, 6, 4, 3, 1, 2, 0]
     assert oracle.traversal_order((0, 1, 0)) == [2, 0, 3, 1, 6, 4, 7, 5]
+
+
+def test_kernel_closed_form_orders_match_shader_tables(ort):
+    """The kernel's fast walk uses order[r] = perm(r) ^ m (render_core.h rank_perm) for rays
+    with no zero direction component, and a rank LUT built from it; both against the shader's
+    tables for the 8 all-non-zero sign vectors."""
+    import ctypes as C
+
+    from octreeraytracer_amd import _lib as L
+    lib = L.lib()
+    by_vec = {tuple(v): c["order"] for c in _clauses() for v in c["sign_vectors"]}
+    for sx in (-1, 1):
+        for sy in (-1, 1):
+            for sz in (-1, 1):
+                m = (int(sz < 0) << 2) | (int(sx < 0) << 1) | int(sy < 0)
+                order = (C.c_int32 * 8)()
+                lut = (C.c_uint8 * 256)()
+                L.check(lib.ort_debug_fast_order(m, order, lut))
+                want = by_vec[(sx, sy, sz)]
+                assert list(order) == want, (sx, sy, sz)
+                # LUT row: child mask (octant space) -> reversed rank bits (rank r = bit 7 - r)
+                for cmask in range(256):
+                    bits = sum(0x80 >> r for r in range(8) if (cmask >> want[r]) & 1)
+                    assert lut[cmask] == bits, (m, cmask)
+
+
+def test_order_fixture_is_current():
+    """tests/golden/traversal_orders.json was generated from the reference shader (checked
+    against the file when the reference is present, i.e. in the build container)."""
+    import hashlib
+    rec = json.loads(GOLDEN_ORDERS.read_text())
+    shader = Path("/root/reference/shaders/octree_fragment_shader.glsl")
+    assert rec["generator"] == "tools/extract_orders.py" and len(rec["clauses"]) == 8
+    if shader.exists():
+        assert hashlib.sha256(shader.read_bytes()).hexdigest() == rec["source_sha256"]
+        sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "tools"))
+        import extract_orders
+        assert extract_orders.extract(shader.read_text()) == rec["clauses"]

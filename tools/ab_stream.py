@@ -21,7 +21,7 @@ sys.path.insert(0, str(ROOT))
 import numpy as np  # noqa: E402
 
 
-def worker(spec, config, block, max_depth=0):
+def worker(spec, config, block, max_depth=0, world=1):
     import ctypes as C
 
     import torch
@@ -42,7 +42,9 @@ def worker(spec, config, block, max_depth=0):
         getattr(r, "set_" + name)(int(val))
     r.build_scene(ort.random_spheres(N, 42), D, M)
     p = ort.FrameParams.default_camera(W, H, num_samples=NS, max_depth=MD)
-    out = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+    from octreeraytracer_amd.distributed import rank_tile
+    tile = rank_tile(W, H, 0, world)  # world > 1: rank 0's band tile of an N-GPU frame
+    out = torch.empty((tile.rows, W, 3), dtype=torch.float32, device="cuda")
     st = torch.cuda.ExternalStream(r.stream_handle())
     print("ready", flush=True)
     for line in sys.stdin:
@@ -52,7 +54,7 @@ def worker(spec, config, block, max_depth=0):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(block):
-            r.render(p, out=out, stream=st.cuda_stream)
+            r.render(p, tile, out=out, stream=st.cuda_stream)
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / block * 1e3
         print(dt, float(np.median(r.trace_times_ms(block))), flush=True)
@@ -65,17 +67,19 @@ def main():
     ap.add_argument("--rounds", type=int, default=12)
     ap.add_argument("--block", type=int, default=10)
     ap.add_argument("--max-depth", type=int, default=0, help="override the config's ray bounce depth")
+    ap.add_argument("--world", type=int, default=1, help="time rank 0's band tile of this many GPUs")
     ap.add_argument("--worker", action="store_true")
     args = ap.parse_args()
     if args.worker:
-        return worker(args.libs[0], args.config, args.block, args.max_depth)
+        return worker(args.libs[0], args.config, args.block, args.max_depth, args.world)
     import bench
     W, H, N, D, M, NS, MD = bench.CONFIGS[args.config]
     MD = args.max_depth or MD
     procs = []
     for spec in args.libs:
         procs.append(subprocess.Popen([sys.executable, "-u", __file__, spec, "--worker", "--config", args.config,
-                                       "--block", str(args.block), "--max-depth", str(args.max_depth)], stdin=subprocess.PIPE, stdout=subprocess.PIPE,
+                                       "--block", str(args.block), "--max-depth", str(args.max_depth),
+                                       "--world", str(args.world)], stdin=subprocess.PIPE, stdout=subprocess.PIPE,
                                       text=True, cwd=str(ROOT)))
         while procs[-1].stdout.readline().strip() != "ready":
             if procs[-1].poll() is not None:
@@ -110,7 +114,7 @@ def main():
     for i, spec in enumerate(args.libs):
         f, tr = np.median(per_frame[i]), np.median(trace[i])
         print(f"{args.config} {spec.split('/')[-1]:24s} frame {f:.4f} ms (min {np.min(per_frame[i]):.4f})  "
-              f"trace {tr:.4f} ms  -> {W * H * NS / f / 1e3:.1f} Mrays/s  "
+              f"trace {tr:.4f} ms  -> {W * H * NS / args.world / f / 1e3:.1f} M camera rays/s  "
               f"({base / f:.3f}x of {args.libs[0].split('/')[-1]})")
 
 
