@@ -85,6 +85,10 @@ def parse(argv=None):
                     help="testing only, no GPU: every rank renders its tile with the host build of the kernel's "
                     "per-pixel code and the bands are gathered with gloo (exercises the launcher, partition and "
                     "gather on CPU; never a measurement)")
+    ap.add_argument("--group", action="store_true",
+                    help="one process drives all N GPUs through the C-ABI group (ort_group_*: a context per device, "
+                    "RCCL ncclSend/ncclRecv gather over xGMI); with --rehearse-one-gpu every rank is GPU 0 and the "
+                    "gather uses device copies")
     ap.add_argument("--save", default="", help="rank 0: save the assembled frame (.pfm/.png)")
     return ap.parse_args(argv)
 
@@ -144,6 +148,25 @@ def lib_sha() -> str:
     return hashlib.sha256(p.read_bytes()).hexdigest()[:16] if p.exists() else ""
 
 
+def device_sha() -> str:
+    """SHA-256 (16 hex) of libort.so's .hip_fatbin section: the gfx950 code objects only, so a
+    PMC record stays valid across host-only rebuilds and goes stale with any kernel change."""
+    import struct
+    p = ROOT / "octreeraytracer_amd" / "lib" / "libort.so"
+    if not p.exists():
+        return ""
+    b = p.read_bytes()
+    shoff = struct.unpack_from("<Q", b, 0x28)[0]
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", b, 0x3A)
+    hdr = [struct.unpack_from("<IIQQQQIIQQ", b, shoff + i * shentsize) for i in range(shnum)]
+    names = hdr[shstrndx][4]
+    for h in hdr:
+        name = b[names + h[0]:b.index(b"\0", names + h[0])]
+        if name == b".hip_fatbin":
+            return hashlib.sha256(b[h[4]:h[4] + h[5]]).hexdigest()[:16]
+    return ""
+
+
 def load_pmc(args, tile_rows) -> dict | None:
     path = Path(args.pmc_json) if args.pmc_json else ROOT / "profiles" / f"pmc_{args.config}.json"
     if not path.exists():
@@ -171,6 +194,19 @@ def roofline(pmc, counts, full_traversals, alg_bytes, trace_ms_avg, kernels_ran)
         r["note"] = "no PMC record for this config (profiles/pmc_<config>.json): issue rate unmeasured"
         return r
     tr = pmc["trace"]
+    # the record must come from the kernels that ran: its device-code hash (or, for records
+    # without one, the whole library's) against this build's
+    if pmc.get("device_sha"):
+        r["pmc_device_sha"] = pmc["device_sha"]
+        r["pmc_matches_build"] = pmc["device_sha"] == device_sha()
+    else:
+        r["pmc_build_sha"] = pmc.get("lib_sha", "")
+        r["pmc_matches_build"] = pmc.get("lib_sha", "") == lib_sha()
+    r["pmc_source"] = pmc["_path"]
+    if not r["pmc_matches_build"]:
+        r["note"] = ("the PMC record was taken with other kernels (device code hash differs): issue rate not "
+                     "reported; re-run tools/profile_box.sh + tools/summarize_profile.py for this build")
+        return r
     # per-rank share of the full-frame counters (N > 1: the rank's traversals / the frame's)
     share = counts["traversals"] / max(1, full_traversals) if full_traversals else 1.0
     insts = tr["valu_insts_per_frame"] * share
@@ -186,10 +222,7 @@ def roofline(pmc, counts, full_traversals, alg_bytes, trace_ms_avg, kernels_ran)
         r["traffic"] = int(traffic)
         r["hbm_GBs"] = round(traffic / t / 1e9, 1)
         r["hbm_frac"] = round(traffic / t / 1e9 / HBM_PEAK_GBS, 5)
-    r["pmc_source"] = pmc["_path"]
     r["pmc_trace_ms_per_frame"] = round(tr["trace_ms_per_frame"], 4)
-    r["pmc_build_sha"] = pmc.get("lib_sha", "")
-    r["pmc_matches_build"] = pmc.get("lib_sha", "") == lib_sha()
     if share != 1.0:
         r["pmc_scaled_by_traversal_share"] = round(share, 5)
     return r
@@ -198,6 +231,8 @@ def roofline(pmc, counts, full_traversals, alg_bytes, trace_ms_avg, kernels_ran)
 def main():
     args = parse()
     W, H, NSPH, DEPTH, MPN, NS, MAXD = CONFIGS[args.config]
+    if args.group:
+        return group_bench(args)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(self_launch(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -269,7 +304,10 @@ def main():
         frame = None
         with torch.cuda.stream(gstream):
             while len(pending) > keep:
-                frame = gather.finish(pending.pop(0))
+                handle, fin = pending.pop(0)
+                frame = gather.finish(handle)
+                if fin is not None:
+                    fin.record(gstream)  # the frame is assembled (rank 0) / its tile sent
         return frame
 
     def step(k, ev=None):
@@ -284,7 +322,7 @@ def main():
         rs[j].render(p, tile, out=outs[slot], stream=st.cuda_stream)
         if ev is not None:
             ev[1].record(st)
-        pending.append(gather.submit(outs[slot], slot))
+        pending.append((gather.submit(outs[slot], slot), ev[2] if ev is not None else None))
 
     for k in range(args.warmup):
         step(k)
@@ -293,7 +331,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    evs = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for _ in range(args.steps)]
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(k, evs[k])
@@ -303,7 +341,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    kern_ms = [a.elapsed_time(b) for a, b in evs]          # whole per-frame pipeline (trace+shade+sort)
+    kern_ms = [a.elapsed_time(b) for a, b, _ in evs]       # whole per-frame pipeline (trace+shade+sort)
+    latency_ms = [a.elapsed_time(c) for a, _, c in evs]    # render start -> frame gathered and assembled
     nframes0 = min(-(-args.steps // inflight), 64)          # context 0's timed frames
     first_trace_ms = r.trace_times_ms(nframes0)             # bounce-0 trace kernel of each frame
     ftrace = r.frame_trace_times_ms(nframes0)               # every trace kernel of each frame, summed
@@ -353,6 +392,10 @@ def main():
                 "all bounces and ranks",
             },
             "frame_gpu_ms_avg": round(float(np.mean(kern_ms)), 4),
+            # per frame on rank 0: its render's start to the assembled frame (gather included);
+            # with frames in flight a frame's latency exceeds ms_per_step (its share of throughput)
+            "frame_latency_ms_avg": round(float(np.mean(latency_ms)), 4),
+            "frame_latency_ms_max": round(float(np.max(latency_ms)), 4),
             "trace_kernels_ms_avg": round(float(np.mean(trace_ms)), 4),
             "trace_launches_per_frame": launches,
             "first_trace_kernel_ms_avg": round(float(np.mean(first_trace_ms)), 4),
@@ -361,6 +404,7 @@ def main():
                                  float(np.mean(trace_ms)), kernels),
             "setup": setup,
             "build_sha": lib_sha(),
+            "device_sha": device_sha(),
         }
         if world == 1 and not args.no_cpu_baseline:
             if tree is None:
@@ -378,6 +422,118 @@ def main():
         dist.destroy_process_group()
     if rank == 0:
         print(json.dumps(result), flush=True)
+
+
+def group_bench(args):
+    """--group: ONE process drives N GPUs through the C-ABI group (include/ort.h ort_group_*),
+    the path a caller of Raytracer::render() uses: a context per device per frame slot, the
+    same 16-row band partition, the bands gathered to devices[0] by RCCL ncclSend/ncclRecv
+    (grouped) and de-interleaved there -- inside the timed region.  With --rehearse-one-gpu
+    every rank is GPU 0 and the gather uses device copies (a control-path check on a one-GPU
+    box, not a scaling measurement).  The line carries a frame check: the last frame against
+    a single-context ort_render of the same scene, bit for bit."""
+    W, H, NSPH, DEPTH, MPN, NS, MAXD = CONFIGS[args.config]
+    N = args.gpus
+    inflight = args.inflight or (1 if N == 1 else 2)
+    if inflight > 1:  # as main(): frame slots overlap only on distinct hardware queues
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, max(8, 4 * inflight)))
+    import torch
+
+    import octreeraytracer_amd as ort
+    from octreeraytracer_amd.group import TRANSPORT_COPY, TRANSPORT_RCCL, RenderGroup
+    devices = [0] * N if args.rehearse_one_gpu else list(range(N))
+    transport = TRANSPORT_COPY if args.rehearse_one_gpu else TRANSPORT_RCCL
+    spheres = ort.random_spheres(NSPH, args.seed)
+    p = ort.FrameParams.default_camera(W, H, num_samples=NS, max_depth=MAXD)
+    g = RenderGroup(devices, transport, inflight=inflight)
+    t0 = time.time()
+    g.build_scene(spheres, DEPTH, MPN)
+    setup = {"group_build_scene_wall_s": round(time.time() - t0, 3)}
+    dev0 = torch.device("cuda", devices[0])
+    nslot = inflight + 1  # frame k writes outs[k % nslot]; submit(k) has waited for frame k - inflight
+    outs = [torch.empty((H, W, 3), dtype=torch.float32, device=dev0) for _ in range(nslot)]
+
+    def sync_all():
+        for d in sorted(set(devices)):
+            torch.cuda.synchronize(d)
+
+    tickets = [g.submit(p, outs[k % nslot]) for k in range(args.warmup)]
+    for tk in tickets:
+        g.wait(tk)
+    sync_all()
+    t0 = time.perf_counter()
+    tickets = [g.submit(p, outs[k % nslot]) for k in range(args.steps)]
+    for tk in tickets:
+        g.wait(tk)
+    sync_all()
+    elapsed = time.perf_counter() - t0
+    latency = g.last_frame_ms()  # the last frame: submission on devices[0] -> assembled
+    last = outs[(args.steps - 1) % nslot]
+    frame = last.cpu().numpy()
+    # single-frame phase: one frame in flight at a time (render() = submit + wait), latency
+    single = []
+    for _ in range(max(3, min(args.steps, 10))):
+        t1 = time.perf_counter()
+        g.render(p, out=outs[0])
+        single.append((time.perf_counter() - t1) * 1e3)
+    single_lat = g.last_frame_ms()
+    counts = [g.count_traffic(p, r) for r in range(N)]
+    rays_per_frame = sum(c["traversals"] for c in counts)
+    nframes0 = min(-(-args.steps // inflight), 64)
+    ftrace = g.frame_trace_times_ms(0, nframes0)
+    trace_ms = [m for m, _ in ftrace]
+    info = None
+    with ort.Renderer(devices[0]) as ref:  # the frame check: one context, the whole frame
+        ref.build_scene(spheres, DEPTH, MPN)
+        info = ref.info()
+        want = ref.render(p)
+    same = bool(np.array_equal(frame.view(np.uint32), want.view(np.uint32)))
+    pmc = load_pmc(args, 0)
+    alg_bytes = ort.algorithmic_bytes(counts[0])
+    value = rays_per_frame * args.steps / elapsed / 1e6
+    result = {
+        "metric": metric_name(args.config),
+        "value": round(value, 2),
+        "unit": "Mrays/s",
+        "n_gpus": N,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (seeded generateRandomSpheres restatement, mt19937 seed %d)" % args.seed,
+        "config": {
+            "workload": f"{args.config}: {W}x{H} camera rays (spp={NS}, bounces={MAXD}), {NSPH} spheres, "
+                        f"octree depth {DEPTH}, maxSpheresPerNode {MPN}",
+            "width": W, "height": H, "spheres": NSPH, "octree_depth": DEPTH, "max_spheres_per_node": MPN,
+            "num_samples": NS, "max_bounces": MAXD, "nodes": info["n_nodes"], "indices": info["n_indices"],
+            "layout": info["layout"], "driver": "C-ABI group (ort_group_submit/ort_group_wait), one process",
+            "devices": devices,
+            "partition": "16-row bands round-robin + " + ("device-copy gather (rehearsal on one GPU: NOT a "
+                                                          "scaling measurement)" if args.rehearse_one_gpu
+                                                          else "RCCL ncclSend/ncclRecv gather to devices[0]"),
+            "frames_in_flight": inflight, "rays_per_step": rays_per_frame,
+            "rays": "traced rays (octree traversals), all bounces and ranks",
+        },
+        "frame_latency_ms": round(latency, 4),
+        "single_frame": {"frames_in_flight": 1, "ms_per_frame_wall": round(float(np.median(single)), 4),
+                         "value": round(rays_per_frame / float(np.median(single)) / 1e3, 2),
+                         "frame_latency_ms": round(single_lat, 4)},
+        "trace_kernels_ms_avg_rank0": round(float(np.mean(trace_ms)), 4),
+        "roofline": roofline(pmc, counts[0], (pmc or {}).get("traversals_per_frame"), alg_bytes,
+                             float(np.mean(trace_ms)), trace_kernel_names(args.config, info, MAXD, NS)),
+        "frame_check": ("bit-identical to a single-context ort_render of the same scene" if same
+                        else "MISMATCH against a single-context ort_render"),
+        "setup": setup,
+        "build_sha": lib_sha(),
+        "device_sha": device_sha(),
+    }
+    g.close()
+    print(json.dumps(result), flush=True)
+    if not same:
+        raise SystemExit("group frame differs from the single-context render")
 
 
 def trace_kernel_names(cfg, info, maxd, ns):

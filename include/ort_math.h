@@ -72,7 +72,16 @@ ORT_HD int ort__rem_pio2(double x, double* r) {
     const int64_t k = (int64_t)kd;
     return (int)(k & 3);
 }
+#if defined(ORT_MEASURE_NATIVE_MATH) && defined(__HIP_DEVICE_COMPILE__)
+/* MEASUREMENT ONLY (tools/build_variant.sh ... -DORT_MEASURE_NATIVE_MATH): the hardware
+ * v_sin/v_cos/v_log/v_exp in place of the canonical kernels, to price them in A/B.  Changes
+ * pixels; never in a product build. */
+#define ORT_NATIVE_MATH 1
+#endif
 ORT_HD float ort_sinf(float xf) {
+#ifdef ORT_NATIVE_MATH
+    return __builtin_amdgcn_sinf(xf * 0.15915494309189535f);
+#endif
     if (!(xf == xf) || xf == ort__inff() || xf == -ort__inff()) return ort__nanf();
     double r; const int q = ort__rem_pio2((double)xf, &r);
     double v;
@@ -85,6 +94,9 @@ ORT_HD float ort_sinf(float xf) {
     return (float)v;
 }
 ORT_HD float ort_cosf(float xf) {
+#ifdef ORT_NATIVE_MATH
+    return __builtin_amdgcn_cosf(xf * 0.15915494309189535f);
+#endif
     if (!(xf == xf) || xf == ort__inff() || xf == -ort__inff()) return ort__nanf();
     double r; const int q = ort__rem_pio2((double)xf, &r);
     double v;
@@ -144,6 +156,9 @@ ORT_HD double ort__exp_d(double z) {
 }
 /* GLSL pow(x, y): undefined for x < 0 (we return NaN, as exp2(y*log2(x)) would). */
 ORT_HD float ort_powf(float x, float y) {
+#ifdef ORT_NATIVE_MATH
+    return __builtin_amdgcn_exp2f(y * __builtin_amdgcn_logf(x));
+#endif
     if (!(x == x) || !(y == y)) return ort__nanf();
     if (x < 0.0f) return ort__nanf();
     if (y == 0.0f) return 1.0f;

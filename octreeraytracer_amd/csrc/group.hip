@@ -19,6 +19,7 @@
 #include <rccl/rccl.h>
 
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <string>
 #include <type_traits>
@@ -41,37 +42,37 @@ struct Rccl {
     const char* (*errorString)(ncclResult_t) = nullptr;
 };
 
-// Loaded once per process; failures leave so == nullptr and a message.
+// Loaded once per process (std::call_once: groups may be created from several threads);
+// failures leave so == nullptr and a message.
 const Rccl& rccl(std::string& err) {
     static Rccl r;
     static std::string why;
-    static bool tried = false;
-    if (!tried) {
-        tried = true;
+    static std::once_flag once;
+    std::call_once(once, [] {
         const char* names[] = {"librccl.so.1", "/opt/rocm/lib/librccl.so.1", "librccl.so"};
         for (const char* n : names)
             if ((r.so = dlopen(n, RTLD_NOW | RTLD_LOCAL))) break;
         if (!r.so) {
             why = std::string("RCCL not loadable: ") + dlerror();
-        } else {
-            bool ok = true;
-            auto sym = [&](auto& f, const char* name) {
-                f = reinterpret_cast<std::remove_reference_t<decltype(f)>>(dlsym(r.so, name));
-                ok = ok && f;
-            };
-            sym(r.commInitAll, "ncclCommInitAll");
-            sym(r.commDestroy, "ncclCommDestroy");
-            sym(r.send, "ncclSend");
-            sym(r.recv, "ncclRecv");
-            sym(r.groupStart, "ncclGroupStart");
-            sym(r.groupEnd, "ncclGroupEnd");
-            sym(r.errorString, "ncclGetErrorString");
-            if (!ok) {
-                why = "RCCL lacks a needed symbol";
-                r.so = nullptr;
-            }
+            return;
         }
-    }
+        bool ok = true;
+        auto sym = [&](auto& f, const char* name) {
+            f = reinterpret_cast<std::remove_reference_t<decltype(f)>>(dlsym(r.so, name));
+            ok = ok && f;
+        };
+        sym(r.commInitAll, "ncclCommInitAll");
+        sym(r.commDestroy, "ncclCommDestroy");
+        sym(r.send, "ncclSend");
+        sym(r.recv, "ncclRecv");
+        sym(r.groupStart, "ncclGroupStart");
+        sym(r.groupEnd, "ncclGroupEnd");
+        sym(r.errorString, "ncclGetErrorString");
+        if (!ok) {
+            why = "RCCL lacks a needed symbol";
+            r.so = nullptr;
+        }
+    });
     err = why;
     return r;
 }

@@ -134,6 +134,13 @@ __global__ void __launch_bounds__(kBlock) k_lds_image(const float* planes, int D
 // REV: the reversed-table image of a depth 9-10 tree (S.lds_rev), for NB-thread workgroups.
 template <bool WITH_LUT, int NB = kBlock, bool REV = false>
 __device__ inline LdsView setup_lds(unsigned char* smem, const ort::KScene& S) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    // The reversed plane tables rely on absolute LDS addresses aligned to their 4T-byte
+    // blocks (1 KiB at depth <= 8, up to 4 KiB in the depth 9-10 reversed image); dynamic
+    // LDS follows any static LDS (append_slots' counters), so check it.  The address is a
+    // link-time constant: the check folds away when it holds and traps loudly when not.
+    if (reinterpret_cast<uintptr_t>(smem) & (REV ? 4095u : 1023u)) __builtin_trap();
+#endif
     const int n16 = REV ? S.lds_rev_n16 : (WITH_LUT ? S.lds_img_n16 : S.lds_img_p16);
     const uint4* src = REV ? S.lds_rev : S.lds_img;
     uint4* dst = reinterpret_cast<uint4*>(smem);

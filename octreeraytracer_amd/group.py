@@ -107,6 +107,33 @@ class RenderGroup:
         """Block until frame `ticket` is complete in its output (ort_group_wait)."""
         self._check(self._lib.ort_group_wait(self._g, C.c_int64(int(ticket))))
 
+    def context(self, rank: int):
+        """Rank `rank`'s context of frame slot 0 (owned by the group)."""
+        c = C.c_void_p()
+        self._check(self._lib.ort_group_context(self._g, int(rank), C.byref(c)))
+        return c
+
+    def count_traffic(self, params: FrameParams, rank: int) -> dict:
+        """Reference-layout work counters (ort_count_traffic) of rank `rank`'s band tile."""
+        from .distributed import rank_tile
+        c = self.context(rank)
+        p, t = params.to_c(), rank_tile(params.width, params.height, rank, len(self.devices)).to_c()
+        counts = (C.c_uint64 * L.ORT_COUNT_N)()
+        rc = self._lib.ort_count_traffic(c, C.byref(p), C.byref(t), counts)
+        if rc != L.ORT_OK:
+            raise L.OrtError(rc, self._lib.ort_last_error(c).decode())
+        return dict(zip(L.COUNT_NAMES, [int(v) for v in counts]))
+
+    def frame_trace_times_ms(self, rank: int, n: int):
+        """Per frame of rank `rank`'s slot-0 context (last n <= 64): (summed trace-kernel ms, launches)."""
+        c = self.context(rank)
+        buf = (C.c_float * max(1, n))()
+        nl = (C.c_int32 * max(1, n))()
+        k = self._lib.ort_frame_trace_times_ms(c, int(n), buf, nl)
+        if k < 0:
+            raise L.OrtError(-k, self._lib.ort_last_error(c).decode())
+        return [(buf[i], nl[i]) for i in range(k)]
+
     def last_frame_ms(self) -> float:
         """Latency (device time on devices[0]) of the last frame seen complete."""
         ms = C.c_float()

@@ -55,3 +55,20 @@ def test_struct_layouts_match_header(ort):
     from octreeraytracer_amd import _lib
     assert ctypes.sizeof(_lib.OrtParams) == 4 * (5 + 16 + 3 + 1)
     assert ctypes.sizeof(_lib.OrtTile) == 24
+
+
+@pytest.mark.parametrize("bad", ["float16", "strided", "short"])
+def test_render_rejects_a_bad_numpy_out_before_the_abi(ort, bad):
+    """Renderer.render checks a numpy `out` with ValueError (not assert: it must hold under
+    python -O), before anything reaches ort_render -- a wrong buffer would be overrun."""
+    import numpy as np
+    r = object.__new__(ort.Renderer)  # no GPU context needed: the check comes first
+    r._ctx = ctypes.c_void_p()
+    r._lib = None
+    r.device = 0
+    p = ort.FrameParams.default_camera(32, 16)
+    out = {"float16": np.empty((16, 32, 3), np.float16),
+           "strided": np.empty((16, 64, 3), np.float32)[:, ::2],
+           "short": np.empty((15, 32, 3), np.float32)}[bad]
+    with pytest.raises(ValueError):
+        r.render(p, out=out)

@@ -2,6 +2,7 @@
 renders its band tile with the host build of the kernel's per-pixel code; rank 0 gathers
 with the same FrameGather the GPU bench uses and must reproduce the single-render frame."""
 import os
+import sys
 import socket
 
 import numpy as np
@@ -148,3 +149,17 @@ def test_bench_self_launch(world):
     t = ort.build_octree(s, 4, 0)
     ref = oracle.render(s, t, ort.FrameParams.default_camera(256, 256))
     assert line["frame_sha256"] == hashlib.sha256(np.ascontiguousarray(ref).tobytes()).hexdigest()
+
+
+def test_bench_group_arguments(monkeypatch):
+    """`bench.py --group` runs in this process (no torch.distributed.run self-launch even with
+    --gpus N) and reaches group_bench with the parsed options."""
+    import bench
+    seen = {}
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--group", "--gpus", "8", "--rehearse-one-gpu", "--config", "c1",
+                                      "--inflight", "3", "--steps", "2"])
+    monkeypatch.setattr(bench, "self_launch", lambda args: (_ for _ in ()).throw(AssertionError("self-launched")))
+    monkeypatch.setattr(bench, "group_bench", lambda args: seen.update(vars(args)))
+    bench.main()
+    assert seen["group"] and seen["gpus"] == 8 and seen["rehearse_one_gpu"] and seen["inflight"] == 3
+    assert seen["config"] == "c1" and seen["steps"] == 2

@@ -51,3 +51,25 @@ def test_bench_ranks_assemble_the_c3_frame(c3_frame, world, tmp_path):
     got = image.read_pfm(out)
     assert got.shape == c3_frame.shape and got.dtype == np.float32
     assert np.array_equal(got.view(np.uint32), c3_frame.view(np.uint32))
+
+
+@pytest.mark.parametrize("world,inflight", [(4, 2), (8, 0)])
+def test_bench_group_rehearsal_is_bit_identical(world, inflight):
+    """`bench.py --group --rehearse-one-gpu`: one process, the C-ABI group with `world` ranks on
+    GPU 0 (device-copy gather), frames submitted with slots in flight; the line's frame check
+    compares the last frame with a single-context render bit for bit."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--group", "--gpus", str(world), "--rehearse-one-gpu",
+           "--config", "c3", "--steps", "4", "--warmup", "1", "--no-cpu-baseline"]
+    if inflight:
+        cmd += ["--inflight", str(inflight)]
+    r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:] + r.stdout[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    line = json.loads(lines[0])
+    assert line["frame_check"].startswith("bit-identical"), line["frame_check"]
+    assert line["n_gpus"] == world and line["config"]["devices"] == [0] * world
+    assert line["config"]["rays_per_step"] == 3840 * 2160
+    assert line["config"]["frames_in_flight"] == (inflight or 2)
+    assert line["frame_latency_ms"] > 0 and line["single_frame"]["frame_latency_ms"] > 0

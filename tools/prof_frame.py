@@ -46,5 +46,5 @@ if a.meta:
     counts = r.count_traffic(p)  # COUNT=true kernel instances: excluded from the PMC sums by name
     Path(a.meta).write_text(json.dumps({"config": a.config, "frames": a.frames * (2 if a.both else 1),
                                         "traversals_per_frame": counts["traversals"], "counts": counts,
-                                        "lib_sha": bench.lib_sha(), "tile_rows": H}))
+                                        "lib_sha": bench.lib_sha(), "device_sha": bench.device_sha(), "tile_rows": H}))
 r.close()

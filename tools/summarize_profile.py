@@ -111,14 +111,14 @@ if trace["trace_ms_per_frame"]:
         # GRBM_GUI_ACTIVE: summed over the 8 XCDs (MI355X_MICROARCH.md DVFS); PMC-run clock
         trace["grbm_clock_GHz_vs_trace_time"] = g / 8 / (trace["trace_ms_per_frame"] * 1e6)
 
-res = {"config": cfg, "source": str(src), "lib_sha": meta.get("lib_sha", ""), "frames_profiled": frames,
+res = {"config": cfg, "source": str(src), "lib_sha": meta.get("lib_sha", ""), "device_sha": meta.get("device_sha", ""), "frames_profiled": frames,
        "bench_frames": bench_frames, "traversals_per_frame": meta["traversals_per_frame"], "tile_rows": meta["tile_rows"],
        "trace": trace, "kernels": kernels, "kernel_stats": stats}
 dst.parent.mkdir(parents=True, exist_ok=True)
 Path(str(dst) + ".json").write_text(json.dumps(res, indent=1))
 if record:
     (dst.parent / f"pmc_{cfg}.json").write_text(json.dumps({
-        "config": cfg, "tile_rows": meta["tile_rows"], "lib_sha": meta.get("lib_sha", ""),
+        "config": cfg, "tile_rows": meta["tile_rows"], "lib_sha": meta.get("lib_sha", ""), "device_sha": meta.get("device_sha", ""),
         "traversals_per_frame": meta["traversals_per_frame"], "trace": trace,
         "method": "rocprofv3 separate --pmc passes over tools/prof_frame.py (production kernels only), summed over "
                   "each frame's trace-kernel launches; FETCH_SIZE*1024*2 (gfx950: FETCH_SIZE reads 1/2 of the "
