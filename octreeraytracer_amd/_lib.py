@@ -89,9 +89,7 @@ _u64p = C.POINTER(C.c_uint64)
 _vp = C.c_void_p
 
 
-def _declare(lib, strict: bool = True):
-    """Set restype/argtypes of every entry point; strict=False skips symbols an older build
-    lacks (tools/ab_stream.py loads earlier builds for A/B timing)."""
+def _declare(lib):
     sig = {
         "ort_create": (C.c_int, [C.c_int, C.POINTER(_vp)]),
         "ort_destroy": (C.c_int, [_vp]),
@@ -144,8 +142,6 @@ def _declare(lib, strict: bool = True):
                                                _fp, _u64p]),
     }
     for name, (res, args) in sig.items():
-        if not strict and not hasattr(lib, name):
-            continue
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args

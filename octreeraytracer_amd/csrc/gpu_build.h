@@ -40,7 +40,6 @@ std::string gpuBuildOctree(const float4* spheres, int32_t n, int32_t maxDepth, i
 struct CompactDev {
     uint2* node = nullptr;
     uint2* kid = nullptr;  // rejected-sphere skip entries (kid_table.h), one per node
-    uint2* pnode = nullptr;  // depth <= 8: records with packed leaf children (leafkids_pack.h)
     float4* leaf_sph = nullptr;
     int32_t* leaf_idx = nullptr;
     float* planes = nullptr;

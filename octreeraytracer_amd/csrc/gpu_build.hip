@@ -30,7 +30,6 @@
 
 #include "gpu_build.h"
 #include "kid_table.h"
-#include "leafkids_pack.h"
 #include "path_key.h"
 
 namespace ort {
@@ -233,7 +232,7 @@ __global__ void k_keys_to_idx(const unsigned long long* keys, int64_t n, int32_t
 
 // ---- compact / explicit layouts on the device (see layout.h for the compact format) ----
 __global__ void k_compact_nodes(const int32_t* co, const int32_t* oo, const int32_t* cnt, const int32_t* idx, int64_t n,
-                                int64_t ni, uint2* node, uint2* kid, uint2* pnode) {
+                                int64_t ni, uint2* node, uint2* kid) {
     for (int64_t i = blockIdx.x * (int64_t)kB + threadIdx.x; i < n; i += (int64_t)gridDim.x * kB) {
         const int32_t c = co[i];
         if (c != -1) {
@@ -248,13 +247,7 @@ __global__ void k_compact_nodes(const int32_t* co, const int32_t* oo, const int3
                 if (co[j] == -1) leaves |= 1u << k;
             }
             // bits 8-15: the existing children that are leaves (render_core.h ORT_LEAFMASK_SHIFT)
-            const uint32_t y = 0x80000000u | (leafkids ? 0x40000000u : 0u) | (leaves << 8) | mask;
-            node[i] = make_uint2((uint32_t)c, y);
-            if (pnode) {  // the camera walk's record with packed leaf children (leafkids_pack.h)
-                uint32_t px, py;
-                pack_leafkids(y, c, oo, cnt, px, py);
-                pnode[i] = make_uint2(px, py);
-            }
+            node[i] = make_uint2((uint32_t)c, 0x80000000u | (leafkids ? 0x40000000u : 0u) | (leaves << 8) | mask);
             int32_t sid[8];
             for (int k = 0; k < 8; ++k) {
                 const int64_t j = (int64_t)c + k;
@@ -268,7 +261,6 @@ __global__ void k_compact_nodes(const int32_t* co, const int32_t* oo, const int3
             const int32_t v = cnt[i] > 0 ? cnt[i] : 0;
             // one-sphere leaves point into the per-sphere tail (layout.h)
             node[i] = make_uint2(v == 1 ? (uint32_t)(ni + idx[oo[i]]) : (v > 0 ? (uint32_t)oo[i] : 0u), (uint32_t)v);
-            if (pnode) pnode[i] = node[i];
         }
     }
 }
@@ -605,7 +597,7 @@ bool gpuCompactLayout(const GpuTree& t, const float4* sp, int maxDepth, hipStrea
     }
     auto fail = [&](const std::string& e) {
         why = e;
-        void* all[] = {out.node, out.leaf_sph, out.leaf_idx, out.planes, out.kid, out.pnode};
+        void* all[] = {out.node, out.leaf_sph, out.leaf_idx, out.planes, out.kid};
         for (void* p : all)
             if (p) (void)hipFree(p);
         out = CompactDev();
@@ -618,7 +610,6 @@ bool gpuCompactLayout(const GpuTree& t, const float4* sp, int maxDepth, hipStrea
     if (!(e = dalloc(out.node, n)).empty() || !(e = dalloc(out.kid, n)).empty() || !(e = dalloc(out.leaf_sph, ne)).empty() ||
         !(e = dalloc(out.leaf_idx, ne)).empty() || !(e = dalloc(out.planes, np)).empty())
         return fail(e);
-    if (D <= 8 && !(e = dalloc(out.pnode, n)).empty()) return fail(e);
     out.node_bytes = (size_t)n * 8;
     out.leaf_bytes = (size_t)std::max<int64_t>(ne, 1) * 16;
     out.idx_bytes = (size_t)std::max<int64_t>(ne, 1) * 4;
@@ -630,7 +621,7 @@ bool gpuCompactLayout(const GpuTree& t, const float4* sp, int maxDepth, hipStrea
         ~Free() { (void)hipFree(p); }
     } fb{bad};
     hipLaunchKernelGGL(k_compact_nodes, dim3(grid_for(n)), dim3(kB), 0, s, t.co, t.oo, t.cnt, t.idx, n, ni, out.node,
-                       out.kid, out.pnode);
+                       out.kid);
     if (ne > 0)
         hipLaunchKernelGGL(k_leaf_gather, dim3(grid_for(ne)), dim3(kB), 0, s, t.idx, ni, ne, sp, out.leaf_sph,
                            out.leaf_idx);

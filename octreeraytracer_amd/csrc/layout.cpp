@@ -4,7 +4,6 @@
 #include <cstring>
 
 #include "kid_table.h"
-#include "leafkids_pack.h"
 #include "render_core_flags.h"
 
 namespace ort {
@@ -156,15 +155,6 @@ bool buildCompactLayout(const SceneInput& in, int maxDepth, CompactLayout& out, 
                                                : (cntv > 0 ? (uint32_t)in.oo[i] : 0u);
             out.node[2 * (size_t)i + 1] = (uint32_t)cntv;
         }
-    }
-    // The camera walk's records with packed leaf children (depth <= 8 trees only).
-    out.pnode.clear();
-    if (out.depth <= 8) {
-        out.pnode = out.node;
-        for (int32_t i = 0; i < n; ++i)
-            if (in.co[i] != -1)
-                pack_leafkids(out.node[2 * (size_t)i + 1], in.co[i], in.oo, in.cnt, out.pnode[2 * (size_t)i],
-                              out.pnode[2 * (size_t)i + 1]);
     }
     // Leaf entries, then the per-sphere tail (entry n_indices + s = sphere s).
     const int64_t ne = in.n_indices + in.n_spheres;

@@ -60,9 +60,6 @@ struct CompactLayout {
     std::vector<float> leaf_sph;   // 4 per index entry
     std::vector<int32_t> leaf_idx; // 1 per index entry
     std::vector<uint32_t> kid;     // 2 per node: rejected-sphere skip entries (kid_table.h)
-    // 2 per node, depth <= 8 only: node with packed leaf-children records (leafkids_pack.h),
-    // read by the camera walk that tests leaf children inline; empty for deeper trees
-    std::vector<uint32_t> pnode;
     // Every reachable box has min <= max and no NaN coordinate: then the plane tables are
     // monotone and the kernel's sign-decided fast walk applies; otherwise every ray takes
     // the exact (GLSL min/max) walk.

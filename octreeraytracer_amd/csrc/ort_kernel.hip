@@ -1056,7 +1056,6 @@ struct ort_ctx {
     DevBuf sph_cr, sph_ma, sph_fr;
     DevBuf node, leaf_sph, leaf_idx, planes, kid;  // compact
     DevBuf nk;                                   // ... node records and kid entries interleaved (build_nk)
-    DevBuf pnode;                                // ... depth <= 8: packed leaf-children records (leafkids_pack.h)
     DevBuf lds_img;                              // compact: the workgroup LDS image (k_lds_image)
     DevBuf lds_rev;                              // ... depth 9-10: the reversed-table image (persistent kernel)
     DevBuf nodeA, nodeB, cnt, indices;           // explicit
@@ -1095,7 +1094,7 @@ void free_buf(DevBuf& b) {
 }
 
 void free_scene(ort_ctx* c) {
-    DevBuf* all[] = {&c->sph_cr, &c->sph_ma, &c->sph_fr, &c->node, &c->kid, &c->nk, &c->pnode, &c->leaf_sph, &c->leaf_idx,
+    DevBuf* all[] = {&c->sph_cr, &c->sph_ma, &c->sph_fr, &c->node, &c->kid, &c->nk, &c->leaf_sph, &c->leaf_idx,
                      &c->planes, &c->lds_img, &c->lds_rev, &c->nodeA, &c->nodeB, &c->cnt, &c->indices};
     for (DevBuf* b : all) free_buf(*b);
     ort::freeGpuTree(c->tree);
@@ -1221,7 +1220,6 @@ int build_impl(ort_ctx* ctx, const float* cr, const float* ma, const float* fr, 
         ctx->layout = ORT_LAYOUT_COMPACT;
         ctx->node = {cd.node, cd.node_bytes};
         ctx->kid = {cd.kid, cd.node_bytes};
-        ctx->pnode = {cd.pnode, cd.pnode ? cd.node_bytes : 0};
         ctx->leaf_sph = {cd.leaf_sph, cd.leaf_bytes};
         ctx->leaf_idx = {cd.leaf_idx, cd.idx_bytes};
         ctx->planes = {cd.planes, cd.plane_bytes};
@@ -1279,7 +1277,6 @@ int upload_impl(ort_ctx* ctx, const ort::SceneInput& in) {
             ctx->ordered = cl.ordered;
             if ((rc = upload(ctx, ctx->node, cl.node.data(), 4 * cl.node.size()))) return rc;
             if ((rc = upload(ctx, ctx->kid, cl.kid.data(), 4 * cl.kid.size()))) return rc;
-            if (!cl.pnode.empty() && (rc = upload(ctx, ctx->pnode, cl.pnode.data(), 4 * cl.pnode.size()))) return rc;
             if ((rc = upload(ctx, ctx->leaf_sph, cl.leaf_sph.data(), 4 * cl.leaf_sph.size()))) return rc;
             if ((rc = upload(ctx, ctx->leaf_idx, cl.leaf_idx.data(), 4 * cl.leaf_idx.size()))) return rc;
             if ((rc = upload(ctx, ctx->planes, cl.planes.data(), 4 * cl.planes.size()))) return rc;
@@ -1323,7 +1320,6 @@ ort::KScene device_scene(const ort_ctx* c) {
     S.kid = c->kid_skip ? (const uint2*)c->kid.p : nullptr;
     S.nk = c->kid_skip == 1 ? (const uint4*)c->nk.p : nullptr;  // 2: the separate arrays (testing)
     S.nk_bytes = (uint32_t)c->nk.bytes;
-    S.pnode = (const uint2*)c->pnode.p;
     S.tail_base = (uint32_t)c->n_indices;
     S.leaf_sph = (const float4*)c->leaf_sph.p;
     S.node_bytes = (uint32_t)c->node.bytes;
@@ -1484,8 +1480,6 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     if (!ctx->has_scene) return fail(ctx, ORT_ERR_NO_SCENE, "ort_render: no scene uploaded");
     const int mode = (p->use_octree == 1) ? (ctx->layout == ORT_LAYOUT_COMPACT ? 0 : 1) : 2;
     if (mode != 2 && ctx->n_nodes <= 0) return fail(ctx, ORT_ERR_NO_SCENE, "ort_render: scene has no octree");
-    if (mode == 0 && ctx->depth <= 8 && ORT_PACKED_LEAFKIDS && !ctx->pnode.p)  // the camera walk reads them
-        return fail(ctx, ORT_ERR_INTERNAL, "ort_render: compact depth <= 8 scene without packed leaf-children records");
     const size_t pix = (size_t)t->width * (size_t)t->rows;
     if (!out && pix > 0) return fail(ctx, ORT_ERR_INVALID_ARG, "ort_render: null output");
     if (pix == 0) return ORT_OK;
@@ -1915,7 +1909,7 @@ int ort_scene_get_info(const ort_ctx* ctx, ort_scene_info* info) {
     info->n_indices = ctx->n_indices;
     info->layout = ctx->layout;
     info->tree_depth = ctx->depth;
-    const DevBuf* all[] = {&ctx->sph_cr, &ctx->sph_ma, &ctx->sph_fr, &ctx->node, &ctx->kid, &ctx->nk, &ctx->pnode, &ctx->leaf_sph, &ctx->leaf_idx,
+    const DevBuf* all[] = {&ctx->sph_cr, &ctx->sph_ma, &ctx->sph_fr, &ctx->node, &ctx->kid, &ctx->nk, &ctx->leaf_sph, &ctx->leaf_idx,
                            &ctx->planes, &ctx->lds_img, &ctx->lds_rev, &ctx->nodeA, &ctx->nodeB, &ctx->cnt, &ctx->indices};
     int64_t b = 0;
     for (const DevBuf* d : all) b += (int64_t)d->bytes;
@@ -2091,7 +2085,6 @@ int ort_debug_emulate_render(const float* cr, const float* ma, const float* fr, 
                 mode = 0;
                 S.node = (const uint2*)cl.node.data();
                 S.kid = (const uint2*)cl.kid.data();
-                S.pnode = cl.pnode.empty() ? nullptr : (const uint2*)cl.pnode.data();
                 S.tail_base = (uint32_t)in.n_indices;
                 S.leaf_sph = (const float4*)cl.leaf_sph.data();
                 S.leaf_idx = cl.leaf_idx.data();
@@ -2198,7 +2191,6 @@ int ort_debug_wave_stats(const float* cr, const float* ma, const float* fr, int3
         S.n_nodes = n_nodes;
         S.node = (const uint2*)cl.node.data();
         S.kid = (const uint2*)cl.kid.data();
-        S.pnode = cl.pnode.empty() ? nullptr : (const uint2*)cl.pnode.data();
         S.tail_base = (uint32_t)in.n_indices;
         S.leaf_sph = (const float4*)cl.leaf_sph.data();
         S.leaf_idx = cl.leaf_idx.data();
@@ -2307,7 +2299,6 @@ int64_t ort_debug_walk_steps(const float* cr, const float* ma, const float* fr, 
         S.n_nodes = n_nodes;
         S.node = (const uint2*)cl.node.data();
         S.kid = (const uint2*)cl.kid.data();
-        S.pnode = cl.pnode.empty() ? nullptr : (const uint2*)cl.pnode.data();
         S.tail_base = (uint32_t)in.n_indices;
         S.leaf_sph = (const float4*)cl.leaf_sph.data();
         S.leaf_idx = cl.leaf_idx.data();
@@ -2333,7 +2324,7 @@ int64_t ort_debug_walk_steps(const float* cr, const float* ma, const float* fr, 
                     const ort::V3 inv = ort::mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
                     ort::FastStateT<ort::Masks64> fs;
                     if (ort::fast_path_ok(ray, inv, 0.001f, ORT_MAXFLOAT) &&
-                        ort::fast_begin<true>(S, fplanes.data(), lut.data(), ray, inv, 0.001f, ORT_MAXFLOAT, fs)) {
+                        ort::fast_begin(S, fplanes.data(), lut.data(), ray, inv, 0.001f, ORT_MAXFLOAT, fs)) {
                         for (bool done = false; !done;) {
                             ort::Counters cc;
                             for (int k = 0; k < 6; ++k) cc.v[k] = 0;

@@ -106,8 +106,6 @@ struct KScene {
     uint32_t leaf_bytes;
     const uint2* kid;        // per node: rejected-sphere skip entry (kid_table.h), or null (off)
     const uint4* nk;         // per node: {record, kid entry} interleaved (one 16-byte load), or null
-    const uint2* pnode;      // depth <= 8: records with packed leaf children (leafkids_pack.h), read by
-                             // the camera walk that tests leaf children inline (kPackedLeafKids)
     uint32_t nk_bytes;
     uint32_t tail_base;      // = n_indices: a one-sphere leaf's objectsOffset is tail_base + sphere
     // explicit (reference) layout
@@ -586,15 +584,6 @@ ORT_FN uint2 fetch_node(const KScene& S, int i) {
     return S.node[i];
 #endif
 }
-ORT_FN uint2 fetch_pnode(const KScene& S, int i) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)S.pnode, 0, (int)S.node_bytes, 0x00020000);
-    const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, (uint32_t)i * 8u, 0, 0);
-    return make_uint2(v[0], v[1]);
-#else
-    return S.pnode[i];
-#endif
-}
 ORT_FN uint2 fetch_kid(const KScene& S, int i) {
 #if defined(__HIP_DEVICE_COMPILE__)
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)S.kid, 0, (int)S.node_bytes, 0x00020000);
@@ -633,15 +622,6 @@ ORT_FN float4 fetch_sphere(const KScene& S, int e) {
 #define ORT_WALK_PRIO 0
 #endif
 constexpr bool kKidPrefetch = ORT_KID_PREFETCH;
-// The depth <= 8 camera walk (inline leaf children) reads the packed records (S.pnode,
-// leafkids_pack.h): a leaf child's sphere range comes from its parent's record instead of a
-// dependent load of its own.  The counting walks read the plain records (their counters need
-// the children offsets).
-#ifndef ORT_PACKED_LEAFKIDS
-#define ORT_PACKED_LEAFKIDS 1
-#endif
-template <class Masks, bool COUNT>
-constexpr bool packed_walk() { return ORT_PACKED_LEAFKIDS && Masks::kInlineLeaves && !COUNT; }
 
 // Plane idx of a ray-order table (base[idx]; see fast_begin for the reversed copies).
 ORT_FN float plane_at(const float* base, int idx) { return base[idx]; }
@@ -849,13 +829,8 @@ struct Masks64Plain : Masks64 {
 #ifndef ORT_NODE_KID
 #define ORT_NODE_KID 1
 #endif
-template <bool PK = false, class Masks>
+template <class Masks>
 ORT_FN void fetch_rec(const KScene& S, int i, bool kid, FastStateT<Masks>& st) {
-    if (PK) {
-        st.rec = fetch_pnode(S, i);
-        if (kid) st.kd = fetch_kid(S, i);
-        return;
-    }
     if (ORT_NODE_KID && Masks::kKidSkip && kid && S.nk) {
         const uint4 v = fetch_nk(S, i);
         st.rec = make_uint2(v.x, v.y);
@@ -867,7 +842,7 @@ ORT_FN void fetch_rec(const KScene& S, int i, bool kid, FastStateT<Masks>& st) {
 }
 
 // Root test and state setup (glsl:296-311).  Returns false when the root box is missed.
-template <bool COUNT = false, class Masks>
+template <class Masks>
 ORT_FN bool fast_begin(const KScene& S, const float* planes, const uint8_t* rank_lut, const Ray& r, V3 inv, float t_min,
                        float t_max, FastStateT<Masks>& st) {
     const int D = S.depth;
@@ -924,7 +899,7 @@ ORT_FN bool fast_begin(const KScene& S, const float* planes, const uint8_t* rank
         }
     }
     st.node = 0;
-    fetch_rec<packed_walk<Masks, COUNT>()>(S, 0, kKidPrefetch && !COUNT && Masks::kKidSkip && S.kid, st);
+    fetch_rec(S, 0, kKidPrefetch && Masks::kKidSkip && S.kid, st);
     st.depth = 0;
     st.closest = t_max;
     st.hitEntry = -1;
@@ -1037,44 +1012,6 @@ ORT_FN bool leaf_kids(const KScene& S, FastStateT<Masks>& st, int co, uint32_t k
     return st.hit();
 }
 
-// leaf_kids over a packed record (leafkids_pack.h): base = the first existing child's
-// objectsOffset, fields = 2-bit (count - 1) per octant (0 for absent children), mask = the
-// existing children.  Child o's spheres start at base + (existing children below o) + (their
-// count - 1 fields summed); no load of the child's own record.
-template <bool COUNT, class Masks>
-ORT_FN bool leaf_kids_packed(const KScene& S, FastStateT<Masks>& st, uint32_t base, uint32_t ry, uint32_t keep,
-                             float tNA, float tMA, float tNB, float tMB, float nN, float nF, Counters& cnt) {
-    const uint32_t fields = (ry >> 8) & 0xffffu, mask = ry & 0xffu;
-    uint32_t todo = keep;
-    while (todo) {
-        const int hb = 31 - __builtin_clz(todo);
-        todo ^= 1u << hb;
-        const uint32_t R = 7u - (uint32_t)hb;
-        const uint32_t o = (st.otab >> (4 * R)) & 15u;
-        const uint32_t fb = fields & ((1u << (2 * o)) - 1u);
-        const int off = (int)(base + (uint32_t)__builtin_popcount(mask & ((1u << o) - 1u)) +
-                              (uint32_t)__builtin_popcount(fb & 0x5555u) + 2u * (uint32_t)__builtin_popcount(fb & 0xaaaau));
-        const int n = (int)((fields >> (2 * o)) & 3u) + 1;
-        if (COUNT) cnt.v[0] += 1;
-#if defined(__HIP_DEVICE_COMPILE__)
-        float eA, eB, eC;
-        {
-            uint32_t m;
-            asm("v_bfe_i32 %[m], %[R], 1, 1\n\tv_bfi_b32 %[a], %[m], %[MA], %[NA]\n\t"
-                "v_bfe_i32 %[m], %[R], 0, 1\n\tv_bfi_b32 %[b], %[m], %[MB], %[NB]\n\t"
-                "v_bfe_i32 %[m], %[R], 2, 1\n\tv_bfi_b32 %[c], %[m], %[CF], %[CN]"
-                : [a] "=&v"(eA), [b] "=&v"(eB), [c] "=&v"(eC), [m] "=&v"(m)
-                : [R] "v"(R), [MA] "v"(tMA), [NA] "v"(tNA), [MB] "v"(tMB), [NB] "v"(tNB), [CF] "v"(nF), [CN] "v"(nN));
-        }
-#else
-        const float eA = (R & 2u) ? tMA : tNA, eB = (R & 1u) ? tMB : tNB, eC = (R & 4u) ? nF : nN;
-#endif
-        const bool h = leaf_tests<COUNT>(S, st, off, n, fmax3(eA, eB, eC), cnt);
-        todo = h ? 0u : todo;
-    }
-    return st.hit();
-}
-
 // One node of the walk: visit st.node (push its surviving children, or test its spheres),
 // then pop the next node.  Returns true when the walk is over (hit found, or stack empty).
 template <bool COUNT, class Masks, class Frames>
@@ -1128,11 +1065,7 @@ ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks
         if (Masks::kInlineLeaves && (rec.y & ORT_LEAFKIDS_FLAG)) {
             // Every existing child is a leaf, so the reference pops the surviving ones next,
             // consecutively in rank order (a leaf pushes nothing): test them right here.
-            if (packed_walk<Masks, COUNT>()) {
-                if (leaf_kids_packed<COUNT>(S, st, rec.x, rec.y, keep, tNA, tMA, tNB, tMB, nN, nF, cnt)) return true;
-            } else if (leaf_kids<COUNT>(S, st, co, keep, tNA, tMA, tNB, tMB, nN, nF, cnt)) {
-                return true;
-            }
+            if (leaf_kids<COUNT>(S, st, co, keep, tNA, tMA, tNB, tMB, nN, nF, cnt)) return true;
         } else if (Masks::kLeadLeaves) {
             // The surviving leaf children ranked before every surviving internal child are the
             // nodes the reference pops next, consecutively (a leaf pushes nothing): test them
@@ -1173,7 +1106,7 @@ ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks
     const int w = 1 << (D - 1 - L);  // child width in plane steps
     st.depth = L + 1;
     st.node = fr.getCo(L) + (int)((st.otab >> (4 * rk)) & 15u);
-    fetch_rec<packed_walk<Masks, COUNT>()>(S, st.node, kKidPrefetch && !COUNT && Masks::kKidSkip && S.kid, st);
+    fetch_rec(S, st.node, kKidPrefetch && !COUNT && Masks::kKidSkip && S.kid, st);
     if (Masks::kRevPlanes) {
         // near plane of the level-(L+1) child: the level-L ancestor's (offset bits below 8w
         // cleared; the table start is a multiple of 4T >= 8w bytes) plus w planes on the axes
@@ -1221,7 +1154,7 @@ ORT_FN bool traverse_fast_t(const KScene& S, const float* planes, const uint8_t*
                             float t_min, float t_max, int& hitEntry, float& hitT, Frames& fr, Counters& cnt,
                             Ray* walked = nullptr) {
     FastStateT<Masks> st;
-    const bool in = fast_begin<COUNT>(S, planes, rank_lut, r, inv, t_min, t_max, st);
+    const bool in = fast_begin(S, planes, rank_lut, r, inv, t_min, t_max, st);
 #if ORT_WALK_PRIO > 0 && defined(__HIP_DEVICE_COMPILE__)
     // experiment: a wave that has walked long raises its issue priority (s_setprio), so the
     // heavy blocks that would form a frame's tail get more of the SIMD while it is full
