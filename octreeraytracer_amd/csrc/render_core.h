@@ -617,10 +617,6 @@ ORT_FN float4 fetch_sphere(const KScene& S, int e) {
 #ifndef ORT_KID_PREFETCH
 #define ORT_KID_PREFETCH 1
 #endif
-// > 0: a walking wave raises its issue priority after that many steps (traverse_fast_t)
-#ifndef ORT_WALK_PRIO
-#define ORT_WALK_PRIO 0
-#endif
 constexpr bool kKidPrefetch = ORT_KID_PREFETCH;
 
 // Plane idx of a ray-order table (base[idx]; see fast_begin for the reversed copies).
@@ -1155,23 +1151,9 @@ ORT_FN bool traverse_fast_t(const KScene& S, const float* planes, const uint8_t*
                             Ray* walked = nullptr) {
     FastStateT<Masks> st;
     const bool in = fast_begin(S, planes, rank_lut, r, inv, t_min, t_max, st);
-#if ORT_WALK_PRIO > 0 && defined(__HIP_DEVICE_COMPILE__)
-    // experiment: a wave that has walked long raises its issue priority (s_setprio), so the
-    // heavy blocks that would form a frame's tail get more of the SIMD while it is full
-    if (in) {
-        int it = 0;
-        while (!fast_step<COUNT>(S, rank_lut, st, fr, cnt)) {
-            ++it;
-            if (it == ORT_WALK_PRIO) __builtin_amdgcn_s_setprio(1);
-            else if (it == 2 * ORT_WALK_PRIO) __builtin_amdgcn_s_setprio(2);
-            else if (it == 4 * ORT_WALK_PRIO) __builtin_amdgcn_s_setprio(3);
-        }
-    }
-#else
     if (in)
         while (!fast_step<COUNT>(S, rank_lut, st, fr, cnt)) {
         }
-#endif
     // the ray back from the walk state (bit-identical to r; no extra registers across the walk)
     if (walked) *walked = st.ray();
     if (!in) return false;

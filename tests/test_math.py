@@ -135,3 +135,18 @@ def test_order_fixture_is_current():
         sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "tools"))
         import extract_orders
         assert extract_orders.extract(shader.read_text()) == rec["clauses"]
+
+
+def test_canonical_builtins_sweep(tmp_path):
+    """tools/math_check.c: sin/cos over |x| <= 8 and pow(x, y) over x in (0, 4] for the shader's
+    exponents (1/2.2, 1/3, 5) and two others, against libm rounded to float -- every result
+    within 1 ulp.  Strided here (seconds); the every-float sweep (stride 1) is recorded in
+    profiles/r03_math_check_exhaustive.log."""
+    import subprocess
+    root = Path(__file__).resolve().parents[1]
+    exe = tmp_path / "math_check"
+    subprocess.run(["gcc", "-O2", "-std=c99", "-ffp-contract=off", "-I", str(root / "include"),
+                    str(root / "tools" / "math_check.c"), "-lm", "-o", str(exe)], check=True)
+    r = subprocess.run([str(exe), "4099"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "OK: every result within 1 ulp" in r.stdout
