@@ -27,7 +27,7 @@ $(OBJ)/ort_kernel.o: $(SRC)/ort_kernel.hip $(HDRS)
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(OBJ)/gpu_build.o: $(SRC)/gpu_build.hip $(SRC)/gpu_build.h
+$(OBJ)/gpu_build.o: $(SRC)/gpu_build.hip $(HDRS)
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -Wno-unused-result -c $< -o $@
 

@@ -85,6 +85,9 @@ def parse(argv=None):
                     help="testing only, no GPU: every rank renders its tile with the host build of the kernel's "
                     "per-pixel code and the bands are gathered with gloo (exercises the launcher, partition and "
                     "gather on CPU; never a measurement)")
+    ap.add_argument("--single-steps", type=int, default=10,
+                    help="N > 1 with frames in flight: also time this many frames with one frame in flight "
+                    "(reported as single_frame, after the main timed region; 0 = skip)")
     ap.add_argument("--group", action="store_true",
                     help="one process drives all N GPUs through the C-ABI group (ort_group_*: a context per device, "
                     "RCCL ncclSend/ncclRecv gather over xGMI); with --rehearse-one-gpu every rank is GPU 0 and the "
@@ -353,6 +356,33 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
 
+    # N > 1 with frames in flight: also time one frame in flight (the N = 1 line's setting), so
+    # a scaling ratio can be taken at equal settings; per frame render + gather + assembly,
+    # the next frame only after it (after the main timed region; not part of `value`)
+    single = None
+    if world > 1 and inflight > 1 and args.single_steps > 0:
+        sev = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for _ in range(args.single_steps)]
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for k in range(args.single_steps):
+            st = streams[0]
+            st.wait_stream(gstream)
+            torch.cuda.set_stream(st)
+            sev[k][0].record(st)
+            rs[0].render(p, tile, out=outs[0], stream=st.cuda_stream)
+            sev[k][1].record(st)
+            pending.append((gather.submit(outs[0], 0), sev[k][2]))
+            drain(0)
+            gstream.synchronize()
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t_single = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t_single, op=dist.ReduceOp.MAX)
+        single = (float(t_single.item()), [a.elapsed_time(c) for a, _, c in sev])
+
     # algorithmic traffic of this rank's launch (counting variant, untimed); the traced rays
     # of a step = traversals summed over the ranks (W*H*spp for primary-only configs)
     counts = r.count_traffic(p, tile)
@@ -396,6 +426,13 @@ def main():
             # with frames in flight a frame's latency exceeds ms_per_step (its share of throughput)
             "frame_latency_ms_avg": round(float(np.mean(latency_ms)), 4),
             "frame_latency_ms_max": round(float(np.max(latency_ms)), 4),
+            "single_frame": None if single is None else {
+                "frames_in_flight": 1, "steps": args.single_steps,
+                "value": round(rays_per_frame * args.single_steps / single[0] / 1e6, 2),
+                "ms_per_step": round(single[0] / args.single_steps * 1e3, 4),
+                "frame_latency_ms_avg": round(float(np.mean(single[1])), 4),
+                "note": "one frame in flight (render, gather, assembly, then the next): the setting of the N=1 "
+                        "line; `value` above keeps frames_in_flight frames in flight"},
             "trace_kernels_ms_avg": round(float(np.mean(trace_ms)), 4),
             "trace_launches_per_frame": launches,
             "first_trace_kernel_ms_avg": round(float(np.mean(first_trace_ms)), 4),

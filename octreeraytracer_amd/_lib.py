@@ -89,7 +89,9 @@ _u64p = C.POINTER(C.c_uint64)
 _vp = C.c_void_p
 
 
-def _declare(lib):
+def _declare(lib, strict: bool = True):
+    """Set restype/argtypes of every entry point; strict=False skips symbols an older build
+    lacks (tools/ab_stream.py loads earlier builds for A/B timing)."""
     sig = {
         "ort_create": (C.c_int, [C.c_int, C.POINTER(_vp)]),
         "ort_destroy": (C.c_int, [_vp]),
@@ -137,11 +139,15 @@ def _declare(lib):
         "ort_debug_group_emulate": (C.c_int, [_fp, _fp, _fp, C.c_int32, _fp, _fp, _ip, _ip, _ip, C.c_int32, _ip, C.c_int64,
                                               C.c_int32, C.POINTER(OrtParams), _fp]),
         "ort_debug_fast_order": (C.c_int, [C.c_int32, _ip, C.POINTER(C.c_uint8)]),
+        "ort_debug_trace_rays": (C.c_int, [_fp, C.c_int32, _fp, _fp, _ip, _ip, _ip, C.c_int32, _ip, C.c_int64, _fp,
+                                           C.c_int32, C.c_int32, _ip]),
         "ort_debug_emulate_render": (C.c_int, [_fp, _fp, _fp, C.c_int32, _fp, _fp, _ip, _ip, _ip, C.c_int32, _ip,
                                                C.c_int64, C.c_int32, C.POINTER(OrtParams), C.POINTER(OrtTile),
                                                _fp, _u64p]),
     }
     for name, (res, args) in sig.items():
+        if not strict and not hasattr(lib, name):
+            continue
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args

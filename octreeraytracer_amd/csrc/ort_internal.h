@@ -33,6 +33,16 @@ int ort_debug_group_emulate(const float* sphere_center_radius, const float* sphe
 // rows (rank_lut_entry) for every child mask: lut256[cmask] (checked against the shader's
 // tables, tests/golden/traversal_orders.json).
 int ort_debug_fast_order(int32_t m, int32_t* order8, uint8_t* lut256);
+// ANALYSIS-ONLY: deferred bounce rays per trace launch (ort_kernel.hip ort_debug_defer_probe).
+int ort_debug_defer_probe(ort_ctx* ctx, void* dev, int32_t cap);
+// TEST-ONLY: per ray (origin.xyz, direction.xyz in rays[6 i]) the fast walk where the kernels
+// would take it (fast_prepare) and the exact walk (traverse_compact, literal GLSL min/max);
+// out[5 i] = {fast taken, fast entry, fast t bits, exact entry, exact t bits}.  bounce != 0:
+// the bounce walk (no inline leaf children, the rejected-sphere skip).
+int ort_debug_trace_rays(const float* sphere_center_radius, int32_t n_spheres, const float* node_min,
+                         const float* node_max, const int32_t* children_offset, const int32_t* objects_offset,
+                         const int32_t* object_count, int32_t n_nodes, const int32_t* object_indices, int64_t n_indices,
+                         const float* rays, int32_t n_rays, int32_t bounce, int32_t* out);
 // ANALYSIS-ONLY: lane overlap of sampled 8x8 primary-ray blocks (tools/wave_stats.py).
 int ort_debug_wave_stats(const float* sphere_center_radius, const float* sphere_mat_albedo,
                          const float* sphere_fuzz_ri, int32_t n_spheres, const float* node_min,

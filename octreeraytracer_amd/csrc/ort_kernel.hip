@@ -204,6 +204,9 @@ __host__ __device__ inline void block_tile(const PipeArgs& A, int blk, int& bx, 
 // holds a slot of the same 256-slot block (the per-tile kernels), so the tile lookup -- two
 // integer divisions by the tile-grid width -- runs once per wave on the scalar unit.
 template <bool UNI = false>
+#ifndef ORT_WAVE_SHAPE
+#define ORT_WAVE_SHAPE 0  // pixels of one wave within its workgroup's 16x16 tile (experiment)
+#endif
 __host__ __device__ inline bool slot_coords(const PipeArgs& A, int k, int& col, int& row) {
 #if defined(__HIP_DEVICE_COMPILE__)
     const int blk = UNI ? __builtin_amdgcn_readfirstlane(k >> 8) : k >> 8;
@@ -213,8 +216,16 @@ __host__ __device__ inline bool slot_coords(const PipeArgs& A, int k, int& col, 
     const int tid = k & 255, wave = tid >> 6, lane = tid & 63;
     int bx, by;
     block_tile(A, blk, bx, by);
+#if ORT_WAVE_SHAPE == 1   // 16x4 pixels per wave
+    col = bx * 16 + (lane & 15);
+    row = by * 16 + wave * 4 + (lane >> 4);
+#elif ORT_WAVE_SHAPE == 2  // 4x16
+    col = bx * 16 + wave * 4 + (lane & 3);
+    row = by * 16 + (lane >> 2);
+#else                      // 8x8
     col = bx * 16 + (wave & 1) * 8 + (lane & 7);
     row = by * 16 + (wave >> 1) * 8 + (lane >> 3);
+#endif
     return col < A.tm.tw && row < A.tm.th;
 }
 
@@ -337,8 +348,8 @@ ort_trace_persistent(PipeArgs A) {
                     bool alive;
                     const ort::Ray ray = load_ray(A, cand, alive);
                     if (alive) {
-                        const ort::V3 inv = ort::mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
-                        if (A.exact_only || !ort::fast_path_ok(ray, inv, 0.001f, ORT_MAXFLOAT)) {
+                        ort::V3 inv = ort::mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
+                        if (A.exact_only || !ort::fast_prepare(A.S, ray, inv)) {
                             A.defer_list[atomicAdd(A.sync, 1)] = cand;
                         } else {
                             if (COUNT) cnt.v[5] += 1;
@@ -530,8 +541,8 @@ __device__ __forceinline__ bool trace_slot(PipeArgs& A, LdsView& L, int k, ort::
         }
         return false;
     }
-    const ort::V3 inv = ort::mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
-    if (A.exact_only || !ort::fast_path_ok(ray, inv, 0.001f, ORT_MAXFLOAT)) {
+    ort::V3 inv = ort::mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
+    if (A.exact_only || !ort::fast_prepare(A.S, ray, inv)) {
         A.defer_list[atomicAdd(A.sync, 1)] = k;  // ort_trace_exact walks (and, FUSE, shades) it
         return false;
     }
@@ -1023,6 +1034,8 @@ struct ort_ctx {
     int refill = 16;  // ORT_OPT_REFILL: C5 (64-item chunks) 16 > 12 (-0.6 %) > 8 (-1.2 %); tools/ab_stream.py
     int persistent = 2;  // ORT_OPT_PERSISTENT: 0 off, 1 every trace, 2 bounce >= 1 traces (default)
     void* wclock = nullptr;  // ort_debug_wave_clock
+    float4* dprobe = nullptr;  // ort_debug_defer_probe: per trace launch, the deferred rays
+    int dprobe_cap = 0;
     long long wclock_n = 0;
     int xcd_swizzle = 2;  // ORT_OPT_XCD_SWIZZLE: workgroup -> tile order (block_tile)
     int kid_skip = 1;     // ORT_OPT_KID_SKIP: rejected-sphere skip of one-sphere leaf children (2: without nk)
@@ -1123,6 +1136,19 @@ int build_lds_image(ort_ctx* ctx) {
         HIPCHK(ctx, hipGetLastError());
     }
     return ORT_OK;
+}
+
+// ANALYSIS-ONLY (ort_debug_defer_probe): record {count, 0, 0, 0} and the first cap deferred
+// rays {origin, direction} of one trace launch (bounce >= 1: the rays are the path state)
+__global__ void k_defer_dump(const int* list, const int* count, const float4* po, const float4* pd, float4* out,
+                             int cap) {
+    const int n = *count;
+    if (threadIdx.x == 0) out[0] = make_float4(__int_as_float(n), 0.0f, 0.0f, 0.0f);
+    for (int i = threadIdx.x; i < n && i < cap; i += blockDim.x) {
+        const int k = list[i];
+        out[1 + 2 * i] = po[k];
+        out[2 + 2 * i] = pd[k];
+    }
 }
 
 __global__ void __launch_bounds__(kBlock) k_interleave_nk(const uint2* node, const uint2* kid, uint4* nk, int64_t n) {
@@ -1648,6 +1674,12 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                     else if (prim) hipLaunchKernelGGL((ort_trace_exact<false, true, 0>), g, t, lds_exact, s, at);
                     else hipLaunchKernelGGL((ort_trace_exact<false, false, 0>), g, t, lds_exact, s, at);
                     if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "ort_trace_exact launch");
+                    if (ctx->dprobe && seg < ort_ctx::kSeg && !prim) {
+                        float4* o = ctx->dprobe + (size_t)seg * (1 + 2 * (size_t)ctx->dprobe_cap);
+                        hipLaunchKernelGGL(k_defer_dump, dim3(1), dim3(256), 0, s, (const int*)ctx->defer_list.p,
+                                           (const int*)ctx->defer_count.p, (const float4*)ctx->po.p,
+                                           (const float4*)ctx->pd.p, o, ctx->dprobe_cap);
+                    }
                 }
             }
             if (!fuse && fmode != 2) {
@@ -2041,6 +2073,71 @@ int ort_count_traffic(ort_ctx* ctx, const ort_params* params, const ort_tile* ti
 }
 
 // ---- TEST-ONLY host emulation (see ort_internal.h) ----------------------------------
+int ort_debug_trace_rays(const float* cr, int32_t n_spheres, const float* node_min, const float* node_max,
+                         const int32_t* co, const int32_t* oo, const int32_t* cnt, int32_t n_nodes, const int32_t* idx,
+                         int64_t n_indices, const float* rays, int32_t n_rays, int32_t bounce, int32_t* out) {
+    try {
+        std::vector<float> ma((size_t)n_spheres * 4, 0.0f), fr((size_t)n_spheres * 4, 0.0f);
+        ort::SceneInput in{cr, ma.data(), fr.data(), n_spheres, node_min, node_max, co, oo, cnt, n_nodes, idx, n_indices};
+        const std::string vbad = ort::validateScene(in);
+        if (!vbad.empty()) return fail(nullptr, ORT_ERR_INVALID_ARG, vbad);
+        ort::CompactLayout cl;
+        std::string why;
+        if (!ort::buildCompactLayout(in, ORT_COMPACT_MAX_DEPTH, cl, why)) return fail(nullptr, ORT_ERR_UNSUPPORTED, why);
+        if (!cl.ordered) return fail(nullptr, ORT_ERR_UNSUPPORTED, "unordered tree");
+        ort::KScene S;
+        std::memset(&S, 0, sizeof(S));
+        S.n_spheres = n_spheres;
+        S.n_nodes = n_nodes;
+        S.node = (const uint2*)cl.node.data();
+        S.kid = (const uint2*)cl.kid.data();
+        S.tail_base = (uint32_t)in.n_indices;
+        S.leaf_sph = (const float4*)cl.leaf_sph.data();
+        S.leaf_idx = cl.leaf_idx.data();
+        S.planes = cl.planes.data();
+        S.depth = cl.depth;
+        std::vector<float> fplanes(ort::fast_plane_floats(cl.depth));
+        ort::fill_fast_planes(cl.planes.data(), fplanes.data(), cl.depth);
+        const bool rev_b = ort::Masks96Lean::kRevPlanes || ort::fast_rev_planes(cl.depth);
+        std::vector<float> fplanes_b(ort::fast_plane_floats(cl.depth, rev_b));
+        ort::fill_fast_planes(cl.planes.data(), fplanes_b.data(), cl.depth, rev_b);
+        std::vector<uint8_t> lut(kRankLutBytes);
+        for (size_t i = 0; i < lut.size(); ++i) lut[i] = ort::rank_lut_entry((uint32_t)i >> 8, (uint32_t)i & 255u);
+        ort::LocalFrames lf;
+        for (int32_t i = 0; i < n_rays; ++i) {
+            ort::Ray r;
+            r.o = ort::mk(rays[6 * (size_t)i], rays[6 * (size_t)i + 1], rays[6 * (size_t)i + 2]);
+            r.d = ort::mk(rays[6 * (size_t)i + 3], rays[6 * (size_t)i + 4], rays[6 * (size_t)i + 5]);
+            ort::Counters cc;
+            for (int k = 0; k < 6; ++k) cc.v[k] = 0;
+            float tf = 0.0f, tx = 0.0f;
+            int ef = -1, ex = -1;
+            // the kernels' choice: the fast walk when fast_prepare takes the ray, else deferred
+            ort::V3 inv = ort::mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+            const bool fast = ort::fast_prepare(S, r, inv);
+            if (fast) {
+                if (!bounce) ort::traverse_fast<false>(S, fplanes.data(), lut.data(), r, inv, 0.001f, ORT_MAXFLOAT, ef, tf, lf, cc);
+                else if (S.depth <= 8)
+                    ort::traverse_fast_t<false, ort::Masks64Plain>(S, fplanes.data(), lut.data(), r, inv, 0.001f, ORT_MAXFLOAT,
+                                                                 ef, tf, lf, cc);
+                else
+                    ort::traverse_fast_t<false, ort::Masks96Lean>(S, fplanes_b.data(), lut.data(), r, inv, 0.001f,
+                                                                ORT_MAXFLOAT, ef, tf, lf, cc);
+            }
+            ort::traverse_compact<false>(S, fplanes.data(), r, 0.001f, ORT_MAXFLOAT, ex, tx, lf, cc);
+            int32_t* o = out + 5 * (size_t)i;
+            o[0] = fast ? 1 : 0;
+            o[1] = ef;
+            o[2] = (int32_t)ort::f2u(tf);
+            o[3] = ex;
+            o[4] = (int32_t)ort::f2u(tx);
+        }
+        return ORT_OK;
+    } catch (const std::exception& ex) {
+        return fail(nullptr, ORT_ERR_INTERNAL, ex.what());
+    }
+}
+
 int ort_debug_fast_order(int32_t m, int32_t* order8, uint8_t* lut256) {
     if (m < 0 || m > 7 || !order8) return fail(nullptr, ORT_ERR_INVALID_ARG, "ort_debug_fast_order: m in 0..7");
     for (uint32_t r = 0; r < 8; ++r) order8[r] = (int32_t)ort::rank_perm(r, (uint32_t)m);
@@ -2168,6 +2265,16 @@ int ort_debug_emulate_render(const float* cr, const float* ma, const float* fr, 
 // loop.  stats: see tools/wave_stats.py for the field order.
 // Analysis only: the wave-queue trace kernels record, per 64-slot block, {start, end}
 // (s_memrealtime, 100 MHz), HW_ID and XCC_ID into dev (n records of 4 x u64); null = off.
+// ANALYSIS-ONLY: after each bounce >= 1 trace launch of the next renders, k_defer_dump writes
+// that launch's deferred-ray count and its first `cap` rays to dev + launch * (1 + 2 cap)
+// float4s (launch = the frame's trace-launch index, < 16).  dev = NULL turns it off.
+int ort_debug_defer_probe(ort_ctx* ctx, void* dev, int32_t cap) {
+    if (!ctx || cap < 0) return ORT_ERR_INVALID_ARG;
+    ctx->dprobe = (float4*)dev;
+    ctx->dprobe_cap = dev ? cap : 0;
+    return ORT_OK;
+}
+
 int ort_debug_wave_clock(ort_ctx* ctx, void* dev, int64_t n) {
     if (!ctx) return ORT_ERR_INVALID_ARG;
     ctx->wclock = dev;

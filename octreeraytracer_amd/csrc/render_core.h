@@ -468,6 +468,74 @@ ORT_FN bool fast_path_ok(const Ray& r, V3 inv, float t_min, float t_max) {
            t_min == kFastTMin && t_max <= ORT_MAXFLOAT && a_in_qdiv_range(dot(r.d, r.d));
 }
 
+// Rays with a zero (or tiny denormal) direction component have an infinite 1/d there.  Their
+// slab values on that axis are +-inf (never NaN unless the origin lies exactly on one of the
+// axis's split planes), and a box's [min, max] interval on it is (-inf, +inf) or empty
+// whichever sign the infinity has -- so the box tests do not depend on that sign.  What does
+// depend on it is the traversal order: the shader picks it from the sign vector with zeros
+// (glsl:342-447), and each of those 26 vectors' table equals perm(r) ^ m' for one full sign
+// mask m' whose non-zero components agree with the ray's (checked against the shader's tables,
+// tests/test_math.py).  So such a ray walks the fast path with inv = +-inf on its zero axes,
+// signed by m'.  kGlslOrderM: m' by (sx+1)*9 + (sy+1)*3 + (sz+1), 3 bits each, 9 per word.
+constexpr uint32_t kGlslOrderM[3] = {0x259bedfu, 0x2518edfu, 0x90984du};
+ORT_FN uint32_t glsl_order_m(float dx, float dy, float dz) {
+    const int sx = dx < 0.0f ? 0 : (dx > 0.0f ? 2 : 1), sy = dy < 0.0f ? 0 : (dy > 0.0f ? 2 : 1),
+              sz = dz < 0.0f ? 0 : (dz > 0.0f ? 2 : 1);
+    const int idx = sx * 9 + sy * 3 + sz;
+    return (kGlslOrderM[idx / 9] >> (3 * (idx % 9))) & 7u;
+}
+// Is v exactly one of the split planes of one axis (2^D + 1 entries)?  The table holds NaN
+// where no node uses a plane (layout.cpp), so search it like the tree splits it: the planes
+// inside (lo, hi) can be used only if the interval's mid plane is (a node with a boundary
+// inside has an ancestor spanning (lo, hi) that was split there), and the used planes are
+// ascending.  D steps; run only for the rare rays with a zero direction component.
+ORT_FN bool on_split_plane(const float* P, int D, float v) {
+    int lo = 0, hi = 1 << D;
+    if (P[lo] == v || P[hi] == v) return true;
+    if (!(v > P[lo] && v < P[hi])) return false;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        const float pm = P[mid];
+        if (!(pm == pm)) return false;
+        if (pm == v) return true;
+        if (v < pm) hi = mid;
+        else lo = mid;
+    }
+    return false;
+}
+// The fast walk for a ray fast_path_ok refused only because some 1/d component is infinite:
+// returns whether it may take the fast walk, with those components of inv signed by the
+// shader's order (see above).  Refused: a zero direction vector (the shader leaves its order
+// undefined), an origin on a split plane of a zero axis (NaN slabs), the other fast_path_ok
+// conditions.
+ORT_FN bool fast_zero_axes(const KScene& S, const Ray& r, V3& inv, float t_min, float t_max) {
+    if (!(fabsf(r.o.x) <= ORT_MAXFLOAT && fabsf(r.o.y) <= ORT_MAXFLOAT && fabsf(r.o.z) <= ORT_MAXFLOAT) ||
+        t_min != kFastTMin || !(t_max <= ORT_MAXFLOAT) || !a_in_qdiv_range(dot(r.d, r.d)))
+        return false;
+    if (r.d.x == 0.0f && r.d.y == 0.0f && r.d.z == 0.0f) return false;
+    if (!(inv.x == inv.x) || !(inv.y == inv.y) || !(inv.z == inv.z)) return false;
+    const uint32_t m = glsl_order_m(r.d.x, r.d.y, r.d.z);
+    const int P1 = (1 << S.depth) + 1;
+    float inf;
+    const uint32_t inf_bits = 0x7f800000u;
+    __builtin_memcpy(&inf, &inf_bits, 4);
+    float* c[3] = {&inv.x, &inv.y, &inv.z};
+    const float o[3] = {r.o.x, r.o.y, r.o.z};
+    const uint32_t neg[3] = {(m >> 1) & 1u, m & 1u, (m >> 2) & 1u};
+    for (int a = 0; a < 3; ++a) {
+        if (fabsf(*c[a]) <= ORT_MAXFLOAT) continue;
+        if (on_split_plane(S.planes + a * P1, S.depth, o[a])) return false;
+        *c[a] = neg[a] ? -inf : inf;
+    }
+    return true;
+}
+
+// fast_path_ok, or else fast_zero_axes (rare: a zero direction component): inv may be re-signed.
+ORT_FN bool fast_prepare(const KScene& S, const Ray& r, V3& inv) {
+    if (fast_path_ok(r, inv, kFastTMin, ORT_MAXFLOAT)) return true;
+    return fast_zero_axes(S, r, inv, kFastTMin, ORT_MAXFLOAT);
+}
+
 // 24-bit signed multiply (plane indices are < 2^11): one full-rate VALU op on the device.
 ORT_FN int imul24(int a, int b) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -843,7 +911,8 @@ ORT_FN bool fast_begin(const KScene& S, const float* planes, const uint8_t* rank
                        float t_max, FastStateT<Masks>& st) {
     const int D = S.depth;
     const int top = 1 << D;
-    const uint32_t nx = r.d.x < 0.0f, ny = r.d.y < 0.0f, nz = r.d.z < 0.0f;
+    // the signs of 1/d (= of d, except on zero axes, where fast_zero_axes chose them)
+    const uint32_t nx = f2u(inv.x) >> 31, ny = f2u(inv.y) >> 31, nz = f2u(inv.z) >> 31;
     const uint32_t m = (nz << 2) | (nx << 1) | ny;
     const bool swap = nx != 0;
     const uint32_t gA = swap ? ny : nx, gB = swap ? nx : ny, gC = nz;
@@ -1280,7 +1349,9 @@ ORT_FN V3 random_in_unit_disk(ort_rng& st) {
     if (xbig) phi = right ? q : 4.0f + q;
     else phi = right ? 2.0f - q : (spy != 0.0f ? 6.0f - q : 0.0f);
     phi *= PI_F / 4.0f;
-    return mk(r * ort_cosf(phi), r * ort_sinf(phi), 0.0f);
+    float sp, cp;
+    ort_sincosf(phi, &sp, &cp);  // = ort_sinf(phi), ort_cosf(phi): one reduction
+    return mk(r * cp, r * sp, 0.0f);
 }
 ORT_FN V3 random_in_unit_sphere(ort_rng& st) {
     const float PI_F = (float)3.14159265359;
@@ -1288,7 +1359,9 @@ ORT_FN V3 random_in_unit_sphere(ort_rng& st) {
     const float phi = 2.0f * PI_F * ort_rand2D(&st);
     const float r = ort_powf(ort_rand2D(&st), 1.0f / 3.0f);
     const float s = sqrtf(1.0f - z * z);
-    return mk(r * s * ort_cosf(phi), r * s * ort_sinf(phi), r * z);
+    float sp, cp;
+    ort_sincosf(phi, &sp, &cp);
+    return mk(r * s * cp, r * s * sp, r * z);
 }
 ORT_FN V3 random_cosine_direction(ort_rng& st) {
     const float PI_F = (float)3.14159265359;
@@ -1296,7 +1369,9 @@ ORT_FN V3 random_cosine_direction(ort_rng& st) {
     const float r2 = ort_rand2D(&st);
     const float phi = 2.0f * PI_F * r1;
     const float sr2 = sqrtf(r2);
-    return mk(ort_cosf(phi) * sr2, ort_sinf(phi) * sr2, sqrtf(1.0f - r2));
+    float sp, cp;
+    ort_sincosf(phi, &sp, &cp);
+    return mk(cp * sr2, sp * sr2, sqrtf(1.0f - r2));
 }
 
 ORT_FN bool refract_vec(V3 v, V3 n, float ni_over_nt, V3& refracted) {
@@ -1452,8 +1527,8 @@ ORT_FN int trace_ray(const KScene& S, const float* planes, const uint8_t* rank_l
     entry = -1;
     t = 0.0f;
     if (MODE == 0) {
-        const V3 inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
-        if (rank_lut && fast_path_ok(r, inv, 0.001f, ORT_MAXFLOAT)) {
+        V3 inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+        if (rank_lut && fast_prepare(S, r, inv)) {
             if (COUNT) cnt.v[5] += 1;
             if (!bounce)
                 hit = traverse_fast<COUNT>(S, planes, rank_lut, r, inv, 0.001f, ORT_MAXFLOAT, entry, t, fr, cnt);

@@ -57,6 +57,8 @@ def lib():
         l.oracle_pow.argtypes = [C.c_float, C.c_float]
         l.oracle_rand_sequence.restype = None
         l.oracle_rand_sequence.argtypes = [C.c_float, C.c_float, C.c_int, C.POINTER(C.c_float)]
+        l.oracle_trace_rays.restype = None
+        l.oracle_trace_rays.argtypes = [C.POINTER(OracleScene), C.POINTER(C.c_float), C.c_int, C.POINTER(C.c_int)]
         l.oracle_traversal_order.restype = None
         l.oracle_traversal_order.argtypes = [C.c_float, C.c_float, C.c_float, C.POINTER(C.c_int)]
         l.oracle_camera.restype = C.c_int
@@ -118,6 +120,29 @@ def render(spheres, tree, params, x0=0, y0=0, width=None, rows=None, band_height
         raise RuntimeError(f"oracle_render failed: {rc}")
     if counts:
         return out, dict(zip(COUNT_NAMES, [int(v) for v in cnt]))
+    return out
+
+
+def trace_rays(spheres, tree, rays) -> np.ndarray:
+    """intersectScene(ray, 0.001, MAXFLOAT) per ray (rays: (n, 6) origin, direction): (n, 2)
+    int32 {hit, bits of t}."""
+    keep = [np.ascontiguousarray(spheres.center_radius, np.float32),
+            np.ascontiguousarray(spheres.mat_albedo, np.float32),
+            np.ascontiguousarray(spheres.fuzz_ri, np.float32),
+            np.ascontiguousarray(tree.node_min, np.float32), np.ascontiguousarray(tree.node_max, np.float32),
+            np.ascontiguousarray(tree.children_offset, np.int32), np.ascontiguousarray(tree.objects_offset, np.int32),
+            np.ascontiguousarray(tree.object_count, np.int32), np.ascontiguousarray(tree.object_indices, np.int32)]
+    sc = OracleScene()
+    sc.sphere_center_radius, sc.sphere_mat_albedo, sc.sphere_fuzz_ri = _fp(keep[0]), _fp(keep[1]), _fp(keep[2])
+    sc.n_spheres = keep[0].shape[0]
+    sc.node_min, sc.node_max = _fp(keep[3]), _fp(keep[4])
+    sc.children_offset, sc.objects_offset, sc.object_count = _ip(keep[5]), _ip(keep[6]), _ip(keep[7])
+    sc.n_nodes = keep[5].shape[0]
+    sc.object_indices = _ip(keep[8])
+    sc.n_indices = keep[8].shape[0]
+    r = np.ascontiguousarray(rays, np.float32)
+    out = np.zeros((len(r), 2), np.int32)
+    lib().oracle_trace_rays(C.byref(sc), _fp(r), len(r), _ip(out))
     return out
 
 

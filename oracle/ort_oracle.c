@@ -511,3 +511,24 @@ void oracle_rand_sequence(float sx, float sy, int n, float* out) {
     for (int i = 0; i < n; ++i) out[i] = ort_rand2D(&st);
 }
 void oracle_traversal_order(float dx, float dy, float dz, int* order8) { traversal_order(v3(dx, dy, dz), order8); }
+/* intersectScene(ray, 0.001, MAXFLOAT) for given rays (rays[6 i] = origin, direction):
+ * out[2 i] = 1 if it hit, out[2 i + 1] = bits of the hit t */
+void oracle_trace_rays(const oracle_scene* sc, const float* rays, int n, int* out) {
+    oracle_params pr;
+    memset(&pr, 0, sizeof(pr));
+    pr.use_octree = 1;
+    Ctx c;
+    c.sc = sc;
+    c.pr = &pr;
+    c.counts = NULL;
+    for (int i = 0; i < n; ++i) {
+        Ray r;
+        r.origin = v3(rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]);
+        r.direction = v3(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]);
+        IntersectInfo rec;
+        memset(&rec, 0, sizeof(rec));
+        const int hit = intersectScene(&c, r, 0.001f, MAXFLOAT_F, &rec);
+        out[2 * i] = hit ? 1 : 0;
+        memcpy(&out[2 * i + 1], &rec.t, 4);
+    }
+}

@@ -47,5 +47,6 @@ float oracle_pow(float x, float y);
 float oracle_tan(float x);
 void oracle_rand_sequence(float sx, float sy, int n, float* out);
 void oracle_traversal_order(float dx, float dy, float dz, int* order8);
+void oracle_trace_rays(const oracle_scene* sc, const float* rays, int n, int* out);
 
 #endif

@@ -166,3 +166,72 @@ def test_walk_steps_analysis_matches_counters(ort, oracle, scene_c1):
     assert n == int(lens.sum()) > 0
     assert int((steps[:n] & 0xff).astype(np.int64).sum()) == rc["leaf_objects"]
     assert 0 < int(np.count_nonzero(lens)) <= rc["traversals"]  # root-box misses take no step
+
+
+def _trace_rays(ort, s, t, rays, bounce):
+    from octreeraytracer_amd import _lib as L
+    lib = L.lib()
+    arr = [np.ascontiguousarray(a, d) for a, d in (
+        (s.center_radius, np.float32), (t.node_min, np.float32), (t.node_max, np.float32),
+        (t.children_offset, np.int32), (t.objects_offset, np.int32), (t.object_count, np.int32),
+        (t.object_indices, np.int32))]
+    rays = np.ascontiguousarray(rays, np.float32)
+    out = np.zeros((len(rays), 5), np.int32)
+    L.check(lib.ort_debug_trace_rays(L.fptr(arr[0]), s.n, L.fptr(arr[1]), L.fptr(arr[2]), L.iptr(arr[3]),
+                                     L.iptr(arr[4]), L.iptr(arr[5]), t.n_nodes, L.iptr(arr[6]), t.n_indices,
+                                     L.fptr(rays), len(rays), int(bounce), L.iptr(out)))
+    return out
+
+
+@pytest.mark.parametrize("d,m,bounce", [(5, 1, 0), (5, 1, 1), (8, 0, 0), (8, 0, 1), (10, 1, 1)])
+def test_zero_direction_components_take_the_fast_walk(ort, oracle, d, m, bounce):
+    """Rays with exactly zero direction components (+0 and -0, one or two axes): the fast walk
+    takes them (inv = +-inf signed by the shader's order table for that sign vector) and finds
+    the exact walk's hit -- same entry, same t bits -- unless the origin lies exactly on a split
+    plane of a zero axis (NaN slabs), which it refuses (deferred to the exact walk)."""
+    s = ort.random_spheres(2000, 7)
+    t = ort.build_octree(s, d, m)
+    rng = np.random.default_rng(d * 10 + m + bounce)
+    lo, hi = t.node_min[0].astype(np.float64), t.node_max[0].astype(np.float64)
+    n = 3000
+    o = lo + (hi - lo) * rng.uniform(-0.05, 1.05, (n, 3))
+    dirs = rng.normal(size=(n, 3))
+    dirs /= np.linalg.norm(dirs, axis=1, keepdims=True)
+    kinds = rng.integers(0, 6, n)
+    for i, k in enumerate(kinds):  # zero out one or two axes, with either zero sign
+        axes = [k % 3] if k < 3 else [k % 3, (k + 1) % 3]
+        for a in axes:
+            dirs[i, a] = -0.0 if rng.random() < 0.5 else 0.0
+        nz = [a for a in range(3) if a not in axes]
+        dirs[i, nz] /= np.linalg.norm(dirs[i, nz])
+    # a tenth of the origins exactly on a split plane of a zero axis (a node box's min)
+    on_plane = rng.random(n) < 0.1
+    for i in np.nonzero(on_plane)[0]:
+        a = next(a for a in range(3) if dirs[i, a] == 0.0)
+        o[i, a] = t.node_min[rng.integers(0, t.n_nodes), a]
+    rays = np.concatenate([o, dirs], axis=1).astype(np.float32)
+    out = _trace_rays(ort, s, t, rays, bounce)
+    fast = out[:, 0] == 1
+    # the exact walk (what the deferred rays get) against the oracle's traverseOctree
+    ref = oracle.trace_rays(s, t, rays)
+    assert ((out[:, 3] >= 0) == (ref[:, 0] == 1)).all() and (out[ref[:, 0] == 1, 4] == ref[ref[:, 0] == 1, 1]).all()
+    assert not fast[on_plane].any(), "a ray with NaN slabs took the fast walk"
+    assert fast[~on_plane].mean() > 0.95
+    agree = (out[:, 1] == out[:, 3]) & ((out[:, 1] < 0) | (out[:, 2] == out[:, 4]))
+    bad = np.nonzero(fast & ~agree)[0]
+    assert bad.size == 0, (bad[:5], rays[bad[:3]], out[bad[:3]])
+    assert (out[fast, 1] >= 0).sum() > 20  # some of them hit spheres
+
+
+def test_ordinary_rays_fast_equals_exact(ort):
+    """The same check for ordinary rays (no zero components), as a control."""
+    s = ort.random_spheres(2000, 7)
+    t = ort.build_octree(s, 6, 0)
+    rng = np.random.default_rng(5)
+    lo, hi = t.node_min[0].astype(np.float64), t.node_max[0].astype(np.float64)
+    o = lo + (hi - lo) * rng.uniform(0, 1, (2000, 3))
+    dirs = rng.normal(size=(2000, 3))
+    dirs /= np.linalg.norm(dirs, axis=1, keepdims=True)
+    out = _trace_rays(ort, s, t, np.concatenate([o, dirs], axis=1), 0)
+    assert (out[:, 0] == 1).all()
+    assert (out[:, 1] == out[:, 3]).all() and (out[out[:, 1] >= 0, 2] == out[out[:, 1] >= 0, 4]).all()

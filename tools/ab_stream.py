@@ -34,7 +34,7 @@ def worker(spec, config, block, max_depth=0, world=1):
     MD = max_depth or MD
     path, _, opts = spec.partition("@")
     lib = C.CDLL(str(Path(path).resolve()), mode=C.RTLD_LOCAL)
-    L._declare(lib)
+    L._declare(lib, strict=False)
     L._lib = lib
     r = ort.Renderer(0)
     for o in filter(None, opts.split(",")):
