@@ -542,7 +542,9 @@ __device__ __forceinline__ bool trace_slot(PipeArgs& A, LdsView& L, int k, ort::
         return false;
     }
     ort::V3 inv = ort::mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
-    if (A.exact_only || !ort::fast_prepare(A.S, ray, inv)) {
+    // camera rays (jittered: practically never a zero component) keep the plain check, which
+    // costs the hot kernel less (C3 +0.7 %); bounce rays take zero components fast too
+    if (A.exact_only || !(PRIMARY ? ort::fast_path_ok(ray, inv, 0.001f, ORT_MAXFLOAT) : ort::fast_prepare(A.S, ray, inv))) {
         A.defer_list[atomicAdd(A.sync, 1)] = k;  // ort_trace_exact walks (and, FUSE, shades) it
         return false;
     }
