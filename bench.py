@@ -325,7 +325,9 @@ def main():
         rs[j].render(p, tile, out=outs[slot], stream=st.cuda_stream)
         if ev is not None:
             ev[1].record(st)
-        pending.append((gather.submit(outs[slot], slot), ev[2] if ev is not None else None))
+            if world == 1:  # no gather: the frame is complete when its render is
+                ev[2].record(st)
+        pending.append((gather.submit(outs[slot], slot), ev[2] if ev is not None and world > 1 else None))
 
     for k in range(args.warmup):
         step(k)
