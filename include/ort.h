@@ -110,6 +110,10 @@ typedef struct ort_scene_info {
 #define ORT_OPT_SORT_BOUND 10      /* testing: > 0 forces the size of the list sort (SORT_PATHS 2) to this
                                       bound -- below the list's length the list goes on in append
                                       order (same pixels); 0 (default): the hint described above */
+#define ORT_OPT_COST_ORDER 11      /* 1 (default): each workgroup of the camera-ray trace deals its 16x16
+                                      pixels to its waves ordered by the walk steps each pixel's ray took
+                                      in the previous frame of the same shape (rays of like cost share a
+                                      wave; same pixels); 0: the fixed 8x8 block per wave */
 
 /* Traffic counters (ort_count_traffic), in the REFERENCE layout's terms. */
 #define ORT_COUNT_NODES_POPPED 0

@@ -73,6 +73,7 @@ struct PipeArgs {
     float4* pcol;     // running sum of samples
     float* out;
     unsigned long long* counters;
+    uint16_t* pcost;  // ORT_OPT_COST_ORDER: per slot, the walk steps of its last camera ray, or null
     ulonglong4* wclock;  // analysis only (ort_debug_wave_clock): per queue block {t0, t1, hw ids, 0}
     int wclock_n;
 };
@@ -546,6 +547,7 @@ __device__ __forceinline__ bool trace_slot(PipeArgs& A, LdsView& L, int k, ort::
     // costs the hot kernel less (C3 +0.7 %); bounce rays take zero components fast too
     if (A.exact_only || !(PRIMARY ? ort::fast_path_ok(ray, inv, 0.001f, ORT_MAXFLOAT) : ort::fast_prepare(A.S, ray, inv))) {
         A.defer_list[atomicAdd(A.sync, 1)] = k;  // ort_trace_exact walks (and, FUSE, shades) it
+        if (PRIMARY && A.pcost) A.pcost[k] = 0;
         return false;
     }
     if (COUNT) cnt.v[5] += 1;
@@ -553,8 +555,20 @@ __device__ __forceinline__ bool trace_slot(PipeArgs& A, LdsView& L, int k, ort::
     int entry = -1;
     using Masks = typename std::conditional<DEEP, ort::Masks96, ort::Masks64>::type;
     ort::Ray walked;
+    int steps = 0;
     const bool hit = ort::traverse_fast_t<COUNT, Masks>(A.S, L.planes, L.lut, ray, inv, 0.001f, ORT_MAXFLOAT, entry, t,
-                                                        L.fr, cnt, FUSE ? &walked : nullptr);
+                                                        L.fr, cnt, FUSE ? &walked : nullptr, PRIMARY ? &steps : nullptr);
+    if (PRIMARY) {  // the cost order's record for the next frame (cost_order_slot)
+#if defined(__HIP_DEVICE_COMPILE__)
+        typedef __attribute__((address_space(4))) const PipeArgs KernArgs;
+        KernArgs* kp = (KernArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(kp));
+        uint16_t* pc = kp->pcost;
+#else
+        uint16_t* pc = A.pcost;
+#endif
+        if (pc) pc[k] = (uint16_t)min(steps, 65535);
+    }
     if (FUSE) {
         // shade with the ray rebuilt from the walk state (bit-identical, no registers held
         // across the walk) and the RNG state kept from the camera ray (2 registers) -- 4 %
@@ -583,11 +597,66 @@ __device__ __forceinline__ bool trace_slot(PipeArgs& A, LdsView& L, int k, ort::
     return false;
 }
 
+// Cost order (ORT_OPT_COST_ORDER): a wave runs as long as its slowest lane, and the camera
+// rays of one 8x8 block differ by up to several times in walk steps (background next to a
+// sphere's silhouette).  Each workgroup deals its 256 slots to its 4 waves by the walk steps
+// their rays took in the previous frame (pcost, a bucket per 4 steps, stable counting sort:
+// equal buckets keep tile order), so rays of like cost share a wave.  Only which lane walks
+// which slot changes -- every slot's ray, path state and pixel are the same (bit-identical
+// frames).  A first frame (pcost cleared) keeps tile order.  Scratch: the first 512 ints of the
+// frame columns (free before the walk; lds_bytes >= 2 levels).
+#ifndef ORT_COST_SHIFT
+#define ORT_COST_SHIFT 2  // bucket = steps >> shift (64 buckets)
+#endif
+__device__ __forceinline__ int cost_order_slot(const uint16_t* pcost, int* sc, int k) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const uint32_t b = min((uint32_t)pcost[k] >> ORT_COST_SHIFT, 63u);
+    uint64_t m = ~0ull;  // the lanes of this wave in the same bucket
+    for (int i = 0; i < 6; ++i) {
+        const uint64_t bal = __ballot((b >> i) & 1u);
+        m &= ((b >> i) & 1u) ? bal : ~bal;
+    }
+    const int below = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    int* cnt = sc;         // [wave][bucket]: lanes, then first position
+    int* perm = sc + 256;  // position -> thread of the natural order
+    cnt[tid] = 0;
+    __syncthreads();
+    if (below == 0) cnt[wave * 64 + b] = __popcll(m);
+    __syncthreads();
+    if (wave == 0) {  // lane = bucket: exclusive scan of the bucket totals
+        const int c0 = cnt[lane], c1 = cnt[64 + lane], c2 = cnt[128 + lane], c3 = cnt[192 + lane];
+        const int tot = c0 + c1 + c2 + c3;
+        int incl = tot;
+        for (int off = 1; off < 64; off <<= 1) {
+            const int v = __shfl_up(incl, off);
+            if (lane >= off) incl += v;
+        }
+        const int base = incl - tot;
+        cnt[lane] = base;
+        cnt[64 + lane] = base + c0;
+        cnt[128 + lane] = base + c0 + c1;
+        cnt[192 + lane] = base + c0 + c1 + c2;
+    }
+    __syncthreads();
+    perm[cnt[wave * 64 + b] + below] = tid;
+    __syncthreads();
+    const int kk = (k & ~(kBlock - 1)) | perm[tid];
+    __syncthreads();  // the frame columns are the walk's from here
+    return kk;
+#else
+    (void)pcost;
+    (void)sc;
+    return k;
+#endif
+}
+
 template <bool COUNT, bool PRIMARY, bool DEEP, int FUSE>
 __device__ __forceinline__ void trace_compact_body(PipeArgs& A, unsigned char* smem) {
     if (!PRIMARY && A.qlist && (int)(blockIdx.x * kBlock) >= *A.qcount) return;  // whole block past the list
     LdsView L = setup_lds<true>(smem, A.S);
     int k = blockIdx.x * kBlock + threadIdx.x;
+    if (PRIMARY && A.pcost) k = cost_order_slot(A.pcost, L.fr.co, k);
     if (!PRIMARY && !list_slot(A, k)) return;
     ort::Counters cnt;
     for (int q = 0; q < 6; ++q) cnt.v[q] = 0;
@@ -1058,6 +1127,11 @@ struct ort_ctx {
     int* alive_host = nullptr;
     unsigned long long hint_sig = 0;
     int sort_bound = 0;  // ORT_OPT_SORT_BOUND (testing): > 0 forces this bound
+    // ORT_OPT_COST_ORDER (cost_order_slot): per slot the walk steps of its last camera ray,
+    // cleared when the frame shape or scene changes (cost_sig)
+    int cost_order = 1;
+    DevBuf pcost;
+    unsigned long long cost_sig = 0;
     float root_lo[3] = {0, 0, 0}, root_hi[3] = {0, 0, 0};  // root box (coherence-sort key)
     DevBuf lut;         // rank LUT (global copy, for the packet kernel)
     ort::GpuTree tree;  // reference-layout tree of the last ort_build_scene(keep_tree)
@@ -1501,6 +1575,17 @@ int persistent_blocks(int device, bool count, bool deep, int depth, size_t lds, 
     return (int)std::max(1LL, std::min(b, needed));
 }
 
+// FNV-1a of the frame shape and scene: the previous-frame hints (list lengths, walk costs)
+// belong to one of these
+unsigned long long frame_sig(const ort_ctx* ctx, const ort_params* p, const ort_tile* t) {
+    const long long v[] = {p->width, p->height, p->num_samples, p->max_depth, t->x0, t->width, t->y0,
+                           t->rows, t->band_height, t->band_stride, ctx->n_nodes, ctx->n_spheres,
+                           (long long)ctx->n_indices, ctx->xcd_swizzle};
+    unsigned long long sig = 1469598103934665603ull;
+    for (long long x : v) sig = (sig ^ (unsigned long long)x) * 1099511628211ull;
+    return sig;
+}
+
 int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out, int out_is_device,
                 void* stream, unsigned long long* dcounters) {
     const std::string bad = check_params(p, t);
@@ -1558,11 +1643,7 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                          (rc = ensure(ctx, ctx->svals, 4 * slots))))
             return rc;
         if (listsort) {  // the list-length hints belong to one frame shape and scene
-            const long long v[] = {p->width, p->height, p->num_samples, p->max_depth, t->x0, t->width, t->y0,
-                                   t->rows, t->band_height, t->band_stride, ctx->n_nodes, ctx->n_spheres,
-                                   (long long)ctx->n_indices};
-            unsigned long long sig = 1469598103934665603ull;
-            for (long long x : v) sig = (sig ^ (unsigned long long)x) * 1099511628211ull;
+            const unsigned long long sig = frame_sig(ctx, p, t);
             if (sig != ctx->hint_sig) {
                 for (int i = 0; i < ort_ctx::kHints; ++i) ctx->alive_host[i] = -1;
                 ctx->hint_sig = sig;
@@ -1610,6 +1691,16 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     // its pixel, so the last sample writes the final pixels itself (no finalize pass)
     a.final_out = fuse_first ? 1 : 0;
     a.key_spread = (const uint32_t*)ctx->key_spread.p;
+    // the cost order: the per-workgroup camera-ray kernels (ort_trace_compact[_deep]) only
+    if (mode == 0 && ctx->cost_order && !ctx->wave_queue && !ctx->packet && !pers_all && ctx->depth >= 2) {
+        if ((rc = ensure(ctx, ctx->pcost, 2 * slots))) return rc;
+        const unsigned long long sig = frame_sig(ctx, p, t);
+        if (sig != ctx->cost_sig) {  // a new shape: tile order for the first frame
+            HIPCHK(ctx, hipMemsetAsync(ctx->pcost.p, 0, 2 * slots, s));
+            ctx->cost_sig = sig;
+        }
+        a.pcost = (uint16_t*)ctx->pcost.p;
+    }
     const size_t lds = lds_bytes(mode, ctx->depth, false);
     const size_t lds_exact = lds_bytes(mode, ctx->depth, true);
     const int pblocks = (mode == 0 && ctx->persistent) ? persistent_blocks(ctx->device, dcounters != nullptr, ctx->depth > 8, ctx->depth, lds, blocks) : 0;
@@ -1876,6 +1967,11 @@ int ort_set_option(ort_ctx* ctx, int option, int value) {
     if (option == ORT_OPT_SORT_PATHS) {
         if (value < 0 || value > 2) return fail(ctx, ORT_ERR_INVALID_ARG, "sort_paths must be 0, 1 or 2");
         ctx->sort_paths = value;
+        return ORT_OK;
+    }
+    if (option == ORT_OPT_COST_ORDER) {
+        if (value < 0 || value > 1) return fail(ctx, ORT_ERR_INVALID_ARG, "ORT_OPT_COST_ORDER: 0 or 1");
+        ctx->cost_order = value;
         return ORT_OK;
     }
     if (option == ORT_OPT_SORT_BOUND) {

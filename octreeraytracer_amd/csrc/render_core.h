@@ -1217,12 +1217,15 @@ ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks
 template <bool COUNT, class Masks, class Frames>
 ORT_FN bool traverse_fast_t(const KScene& S, const float* planes, const uint8_t* rank_lut, const Ray& r, V3 inv,
                             float t_min, float t_max, int& hitEntry, float& hitT, Frames& fr, Counters& cnt,
-                            Ray* walked = nullptr) {
+                            Ray* walked = nullptr, int* steps = nullptr) {
     FastStateT<Masks> st;
     const bool in = fast_begin(S, planes, rank_lut, r, inv, t_min, t_max, st);
+    int n = 0;  // walk steps (steps: the cost order's record; folds away without it)
     if (in)
         while (!fast_step<COUNT>(S, rank_lut, st, fr, cnt)) {
+            ++n;
         }
+    if (steps) *steps = in ? n + 1 : 0;
     // the ray back from the walk state (bit-identical to r; no extra registers across the walk)
     if (walked) *walked = st.ray();
     if (!in) return false;

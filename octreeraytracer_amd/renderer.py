@@ -149,6 +149,10 @@ class Renderer:
         """Testing (ORT_OPT_SORT_BOUND): force the list sort's size; 0 = the previous-frame hint."""
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_SORT_BOUND, int(bound)))
 
+    def set_cost_order(self, on: int):
+        """ORT_OPT_COST_ORDER: 1 (default) camera rays dealt to waves by last frame's walk cost; 0 fixed blocks."""
+        self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_COST_ORDER, int(on)))
+
     def set_refill(self, lanes: int):
         """Persistent trace: refill a wave once at least `lanes` of its 64 lanes are idle."""
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_REFILL, int(lanes)))

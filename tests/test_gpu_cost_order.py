@@ -1,0 +1,73 @@
+"""Cost order (include/ort.h ORT_OPT_COST_ORDER): the camera-ray trace deals each 16x16 tile's
+pixels to its waves by the walk steps their rays took in the previous frame.  Only which lane
+walks which pixel changes, so every frame -- the first (tile order), later ones (ordered by
+exact costs), after a camera move (stale costs), after a shape change (costs cleared) -- must
+be bit-identical to the fixed-block order, and to the oracle (reference: one invocation per
+pixel, glsl:597-633, whatever the invocation order)."""
+import numpy as np
+import pytest
+
+from test_gpu_parity import assert_same
+
+pytestmark = pytest.mark.gpu
+
+
+def _frames(ort, r, s, t, params, tiles):
+    out = []
+    for p, tile in zip(params, tiles):
+        out.append(r.render(p, tile))
+    return out
+
+
+@pytest.mark.parametrize("ns,md", [(1, 1), (2, 3)])
+def test_cost_order_frames_match_block_order(ort, oracle, scene_c2, ns, md):
+    """C2 scene at 640x360: a static camera (frames 1-2), a moved camera (3), a band tile (4,
+    a new shape: costs cleared), the full frame again (5).  Cost order on vs off: bit-exact."""
+    from octreeraytracer_amd.scene import DEFAULT_YAW, DEFAULT_PITCH
+    s, t = scene_c2
+    W, H = 640, 360
+    p0 = ort.FrameParams.default_camera(W, H, num_samples=ns, max_depth=md)
+    p1 = ort.FrameParams.default_camera(W, H, num_samples=ns, max_depth=md, yaw=DEFAULT_YAW + 4.0,
+                                        pitch=DEFAULT_PITCH - 2.0)
+    full = ort.Tile(0, W, 0, H)
+    band = ort.Tile(0, W, 8, 64, band_height=8, band_stride=32)
+    params = [p0, p0, p1, p0, p0]
+    tiles = [full, full, full, band, full]
+    got = {}
+    for on in (1, 0):
+        with ort.Renderer(0) as r:
+            r.upload(s, t)
+            r.set_cost_order(on)
+            got[on] = _frames(ort, r, s, t, params, tiles)
+    for i, (a, b) in enumerate(zip(got[1], got[0])):
+        assert_same(a, b, f"frame {i}: cost order vs block order")
+    ref = oracle.render(s, t, p1, 0, 200, W, 16, threads=0)
+    assert_same(got[1][2][200:216], ref, "moved camera, stale costs vs oracle")
+
+
+def test_cost_order_deep_tree(ort, oracle):
+    """Depth 9 (the 96-bit-mask camera kernel, ort_trace_compact_deep, with shading fused into
+    bounce 0 of a multi-bounce frame): two frames with cost order, bit-exact vs block order and
+    the oracle."""
+    s = ort.random_spheres(20000, 42)
+    t = ort.build_octree(s, 9, 0)
+    W, H = 480, 270
+    p = ort.FrameParams.default_camera(W, H, num_samples=1, max_depth=3)
+    got = {}
+    for on in (1, 0):
+        with ort.Renderer(0) as r:
+            r.upload(s, t)
+            r.set_cost_order(on)
+            got[on] = [r.render(p) for _ in range(2)]
+    assert_same(got[1][1], got[0][1], "depth 9, second frame: cost order vs block order")
+    assert_same(got[1][0], got[0][0], "depth 9, first frame")
+    ref = oracle.render(s, t, p, 0, 100, W, 8, threads=0)
+    assert_same(got[1][1][100:108], ref, "depth 9 cost order vs oracle")
+
+
+def test_cost_order_option_range(ort):
+    with ort.Renderer(0) as r:
+        with pytest.raises(ort.OrtError):
+            r.set_cost_order(2)
+        r.set_cost_order(0)
+        r.set_cost_order(1)

@@ -3,6 +3,7 @@ GPU, device output, each build's frames back to back on its own stream (no host 
 frame), builds alternating in blocks of --block frames in ABBA order so clock and thermal
 drift hit every build alike.  Also checks that every build writes bit-identical frames.
 usage: python tools/ab_stream.py LIB_A LIB_B [...] [--config c3] [--rounds 12] [--block 10]
+       [--world N] [--max-depth D] [--yaw-step DEG]
 A build may carry options: path@option=value,... with option one of the Renderer setters
 (e.g. build/ab/libA.so@xcd_swizzle=0).
 
@@ -21,7 +22,7 @@ sys.path.insert(0, str(ROOT))
 import numpy as np  # noqa: E402
 
 
-def worker(spec, config, block, max_depth=0, world=1):
+def worker(spec, config, block, max_depth=0, world=1, yaw_step=0.0):
     import ctypes as C
 
     import torch
@@ -42,6 +43,10 @@ def worker(spec, config, block, max_depth=0, world=1):
         getattr(r, "set_" + name)(int(val))
     r.build_scene(ort.random_spheres(N, 42), D, M)
     p = ort.FrameParams.default_camera(W, H, num_samples=NS, max_depth=MD)
+    from octreeraytracer_amd.scene import DEFAULT_YAW
+    moving = [ort.FrameParams.default_camera(W, H, num_samples=NS, max_depth=MD, yaw=DEFAULT_YAW + yaw_step * j)
+              for j in range(64)] if yaw_step else [p]
+    frame = 0
     from octreeraytracer_amd.distributed import rank_tile
     tile = rank_tile(W, H, 0, world)  # world > 1: rank 0's band tile of an N-GPU frame
     out = torch.empty((tile.rows, W, 3), dtype=torch.float32, device="cuda")
@@ -53,8 +58,10 @@ def worker(spec, config, block, max_depth=0, world=1):
             continue
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(block):
-            r.render(p, tile, out=out, stream=st.cuda_stream)
+        for _ in range(block):  # a moving camera (--yaw-step) turns back and forth over 64 frames
+            j = frame % (2 * len(moving))
+            r.render(moving[min(j, 2 * len(moving) - 1 - j)], tile, out=out, stream=st.cuda_stream)
+            frame += 1
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / block * 1e3
         print(dt, float(np.median(r.trace_times_ms(block))), flush=True)
@@ -68,10 +75,11 @@ def main():
     ap.add_argument("--block", type=int, default=10)
     ap.add_argument("--max-depth", type=int, default=0, help="override the config's ray bounce depth")
     ap.add_argument("--world", type=int, default=1, help="time rank 0's band tile of this many GPUs")
+    ap.add_argument("--yaw-step", type=float, default=0.0, help="moving camera: degrees of yaw per frame")
     ap.add_argument("--worker", action="store_true")
     args = ap.parse_args()
     if args.worker:
-        return worker(args.libs[0], args.config, args.block, args.max_depth, args.world)
+        return worker(args.libs[0], args.config, args.block, args.max_depth, args.world, args.yaw_step)
     import bench
     W, H, N, D, M, NS, MD = bench.CONFIGS[args.config]
     MD = args.max_depth or MD
@@ -79,7 +87,7 @@ def main():
     for spec in args.libs:
         procs.append(subprocess.Popen([sys.executable, "-u", __file__, spec, "--worker", "--config", args.config,
                                        "--block", str(args.block), "--max-depth", str(args.max_depth),
-                                       "--world", str(args.world)], stdin=subprocess.PIPE, stdout=subprocess.PIPE,
+                                       "--world", str(args.world), "--yaw-step", str(args.yaw_step)], stdin=subprocess.PIPE, stdout=subprocess.PIPE,
                                       text=True, cwd=str(ROOT)))
         while procs[-1].stdout.readline().strip() != "ready":
             if procs[-1].poll() is not None:
