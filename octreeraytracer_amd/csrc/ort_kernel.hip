@@ -547,7 +547,7 @@ __device__ __forceinline__ bool trace_slot(PipeArgs& A, LdsView& L, int k, ort::
     // costs the hot kernel less (C3 +0.7 %); bounce rays take zero components fast too
     if (A.exact_only || !(PRIMARY ? ort::fast_path_ok(ray, inv, 0.001f, ORT_MAXFLOAT) : ort::fast_prepare(A.S, ray, inv))) {
         A.defer_list[atomicAdd(A.sync, 1)] = k;  // ort_trace_exact walks (and, FUSE, shades) it
-        if (PRIMARY && A.pcost) A.pcost[k] = 0;
+        if (PRIMARY && !COUNT && A.pcost) A.pcost[k] = 0;
         return false;
     }
     if (COUNT) cnt.v[5] += 1;
@@ -557,8 +557,9 @@ __device__ __forceinline__ bool trace_slot(PipeArgs& A, LdsView& L, int k, ort::
     ort::Ray walked;
     int steps = 0;
     const bool hit = ort::traverse_fast_t<COUNT, Masks>(A.S, L.planes, L.lut, ray, inv, 0.001f, ORT_MAXFLOAT, entry, t,
-                                                        L.fr, cnt, FUSE ? &walked : nullptr, PRIMARY ? &steps : nullptr);
-    if (PRIMARY) {  // the cost order's record for the next frame (cost_order_slot)
+                                                        L.fr, cnt, FUSE ? &walked : nullptr,
+                                                        (PRIMARY && !COUNT) ? &steps : nullptr);
+    if (PRIMARY && !COUNT) {  // the cost order's record for the next frame (cost_order_slot)
 #if defined(__HIP_DEVICE_COMPILE__)
         typedef __attribute__((address_space(4))) const PipeArgs KernArgs;
         KernArgs* kp = (KernArgs*)__builtin_amdgcn_kernarg_segment_ptr();
@@ -656,7 +657,7 @@ __device__ __forceinline__ void trace_compact_body(PipeArgs& A, unsigned char* s
     if (!PRIMARY && A.qlist && (int)(blockIdx.x * kBlock) >= *A.qcount) return;  // whole block past the list
     LdsView L = setup_lds<true>(smem, A.S);
     int k = blockIdx.x * kBlock + threadIdx.x;
-    if (PRIMARY && A.pcost) k = cost_order_slot(A.pcost, L.fr.co, k);
+    if (PRIMARY && !COUNT && A.pcost) k = cost_order_slot(A.pcost, L.fr.co, k);  // (the counting pass: tile order)
     if (!PRIMARY && !list_slot(A, k)) return;
     ort::Counters cnt;
     for (int q = 0; q < 6; ++q) cnt.v[q] = 0;

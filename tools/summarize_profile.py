@@ -41,11 +41,15 @@ if ks:
 trace_ns_total = 0.0
 trace_launches = 0
 kt = next(src.glob("trace/**/*kernel_trace.csv"), None)
-if kt:
-    for r in csv.DictReader(open(kt)):
-        if is_trace(r["Kernel_Name"]):
-            trace_ns_total += float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
-            trace_launches += 1
+if kt:  # the timed steps only (bench.py's warm-up frames include the cost order's first frame)
+    durs = [(float(r["Start_Timestamp"]), float(r["End_Timestamp"]) - float(r["Start_Timestamp"]))
+            for r in csv.DictReader(open(kt)) if is_trace(r["Kernel_Name"])]
+    durs.sort()
+    warm_b = bargs.get("warmup", 3)
+    durs = durs[warm_b * len(durs) // bench_frames:]
+    bench_frames -= warm_b
+    trace_ns_total = sum(d for _, d in durs)
+    trace_launches = len(durs)
 else:  # from the stats: production trace kernels' total time
     for n, st in stats.items():
         if is_trace(n):
@@ -53,14 +57,21 @@ else:  # from the stats: production trace kernels' total time
             trace_launches += int(st["Calls"])
 
 # PMC passes over tools/prof_frame.py (meta["frames"] production frames + one counting pass)
+# (trace kernels: the first warm_frames frames' launches are left out -- the cost order's first
+# frame walks in tile order)
 per_kernel = defaultdict(lambda: defaultdict(float))
 launches = defaultdict(lambda: defaultdict(int))
-for f in src.glob("pmc_*/**/pmc_counter_collection.csv"):
-    for r in csv.DictReader(open(f)):
-        n = short(r["Kernel_Name"])
-        per_kernel[n][r["Counter_Name"]] += float(r["Counter_Value"])
-        launches[n][r["Counter_Name"]] += 1
 frames = meta["frames"]
+warm = meta.get("warm_frames", 0)
+for f in src.glob("pmc_*/**/pmc_counter_collection.csv"):
+    rows = defaultdict(list)  # (kernel, counter) -> values in dispatch order
+    for r in sorted(csv.DictReader(open(f)), key=lambda r: int(r.get("Dispatch_Id") or 0)):
+        rows[(short(r["Kernel_Name"]), r["Counter_Name"])].append(float(r["Counter_Value"]))
+    for (n, c), vals in rows.items():
+        if is_trace(n) and warm:
+            vals = vals[warm * len(vals) // (frames + warm):]
+        per_kernel[n][c] += sum(vals)
+        launches[n][c] += len(vals)
 kernels = {}
 for n, cs in per_kernel.items():
     k = {"trace": is_trace(n)}
@@ -112,6 +123,7 @@ if trace["trace_ms_per_frame"]:
         trace["grbm_clock_GHz_vs_trace_time"] = g / 8 / (trace["trace_ms_per_frame"] * 1e6)
 
 res = {"config": cfg, "source": str(src), "lib_sha": meta.get("lib_sha", ""), "device_sha": meta.get("device_sha", ""), "frames_profiled": frames,
+       "warm_frames_excluded": warm,
        "bench_frames": bench_frames, "traversals_per_frame": meta["traversals_per_frame"], "tile_rows": meta["tile_rows"],
        "trace": trace, "kernels": kernels, "kernel_stats": stats}
 dst.parent.mkdir(parents=True, exist_ok=True)
