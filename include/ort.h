@@ -114,6 +114,12 @@ typedef struct ort_scene_info {
                                       pixels to its waves ordered by the walk steps each pixel's ray took
                                       in the previous frame of the same shape (rays of like cost share a
                                       wave; same pixels); 0: the fixed 8x8 block per wave */
+#define ORT_OPT_HEAVY_FIRST 12     /* T > 0 (default 64): the sorted bounce lists (SORT_PATHS 2, persistent
+                                      trace) order paths by the steps their walk at that bounce took in
+                                      the previous frame of the same shape -- >= 4T first, then >= 2T,
+                                      >= T, the rest, each class in coherence order -- so the longest
+                                      walks start early rather than in the launch's drain tail (same
+                                      pixels); 0: coherence order only */
 
 /* Traffic counters (ort_count_traffic), in the REFERENCE layout's terms. */
 #define ORT_COUNT_NODES_POPPED 0

@@ -33,6 +33,7 @@ ORT_OPT_XCD_SWIZZLE = 8
 ORT_OPT_KID_SKIP = 9
 ORT_OPT_SORT_BOUND = 10
 ORT_OPT_COST_ORDER = 11
+ORT_OPT_HEAVY_FIRST = 12
 ORT_LAYOUT_COMPACT_EXACT_EMULATION = 2
 ORT_COUNT_N = 6
 COUNT_NAMES = ("nodes_popped", "child_records", "leaf_objects", "accepted_hits", "pixels", "traversals")

@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "path_key.h"
+
 #include <cstdint>
 #include <string>
 #include <vector>
@@ -77,8 +79,9 @@ hipError_t sortList(void* temp, size_t temp_bytes, int n, const SortBuffers& b, 
 // the all-ones key, so the stable radix sort of `bound` pairs puts the n real ones first, in
 // key order.  If n > bound (the hint was short) the sort's output is replaced by the list in
 // append order -- the same paths, a different order, so the same pixels.  No host wait.
+// key_bits: the keys' width (kPathKeyBits, or one more with the heavy-first bit).
 hipError_t sortListBounded(void* temp, size_t temp_bytes, int bound, const int* count, const SortBuffers& b,
-                           hipStream_t s);
+                           hipStream_t s, int key_bits = kPathKeyBits);
 size_t sortAliveTempBytes(int n);
 hipError_t sortAlive(void* temp, size_t temp_bytes, const float4* po, const float4* pd, int n, const float* root_lo,
                      const float* root_hi, const uint32_t* spread, const SortBuffers& b, int* count, hipStream_t s);

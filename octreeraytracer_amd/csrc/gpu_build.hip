@@ -712,15 +712,15 @@ hipError_t sortList(void* temp, size_t temp_bytes, int n, const SortBuffers& b, 
 }
 
 hipError_t sortListBounded(void* temp, size_t temp_bytes, int bound, const int* count, const SortBuffers& b,
-                           hipStream_t s) {
+                           hipStream_t s, int key_bits) {
     if (bound <= 0) return hipSuccess;
     constexpr int kGrid = 512;  // 128 k lanes: the pad (usually < 2 % of the list) and the rare copy
     hipLaunchKernelGGL(k_pad_keys, dim3(kGrid), dim3(kB), 0, s, b.keys_in, count, bound);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    // stable LSD sort: a real key equal to the pad's low kPathKeyBits stays ahead of the pads
+    // stable LSD sort: a real key equal to the pad's low key_bits stays ahead of the pads
     e = rocprim::radix_sort_pairs(temp, temp_bytes, b.keys_in, b.keys_out, b.vals_in, b.vals_out, (size_t)bound, 0,
-                                  kPathKeyBits, s);
+                                  key_bits, s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_overflow_copy, dim3(kGrid), dim3(kB), 0, s, (const int*)b.vals_in, b.vals_out, count, bound);
     return hipGetLastError();

@@ -74,6 +74,9 @@ struct PipeArgs {
     float* out;
     unsigned long long* counters;
     uint16_t* pcost;  // ORT_OPT_COST_ORDER: per slot, the walk steps of its last camera ray, or null
+    uint16_t* bcost_w;        // ORT_OPT_HEAVY_FIRST: the persistent bounce trace records each walk's steps here
+    const uint16_t* bcost_r;  // ... the kernels appending the next bounce's list read that bounce's last-frame steps
+    int heavy;                // ... walks of at least this many steps are heavy: they sort first
     ulonglong4* wclock;  // analysis only (ort_debug_wave_clock): per queue block {t0, t1, hw ids, 0}
     int wclock_n;
 };
@@ -90,7 +93,10 @@ constexpr size_t kRankLutBytes = 8 * 256;  // ort::rank_lut_entry table
 // workgroups over the reversed-table image (fast_rev_planes: 32.8 KB at depth 10, the rank
 // LUT in its gap), 53.3 KB of LDS with 512 lanes' frames -- 3 workgroups = 6 waves/SIMD.
 constexpr bool kRevBounce = ORT_REV_BOUNCE;
-constexpr int kPersistDeepBlock = kRevBounce ? 512 : kBlock;
+#ifndef ORT_PERSIST_DEEP_BLOCK
+#define ORT_PERSIST_DEEP_BLOCK 512
+#endif
+constexpr int kPersistDeepBlock = kRevBounce ? ORT_PERSIST_DEEP_BLOCK : kBlock;
 
 // with_tm: the exact walk also keeps a per-level tmin column; the fast walk needs none.
 // rev / nb: the image layout and workgroup size (the deep persistent kernel's: true, 512).
@@ -297,6 +303,9 @@ __global__ void __launch_bounds__(kBlock) ort_raygen_kernel(PipeArgs A) {
 // window of about (waves x kChunk) consecutive list items -- neighbouring paths, overlapping
 // node sets, one L2 working set: C5 frame 58.2 (256) -> 56.7 (128) -> 55.8 ms (64; 32: 56.0)
 // in A/B.  (One queue per XCD over 8 contiguous list ranges measured no better: -0.4 %.)
+#ifndef ORT_PERSIST_CLOCK
+#define ORT_PERSIST_CLOCK 0
+#endif
 #ifndef ORT_CHUNK
 #define ORT_CHUNK 64
 #endif
@@ -321,10 +330,16 @@ ort_trace_persistent(PipeArgs A) {
     using Masks = typename std::conditional<DEEP, ort::Masks96Lean, ort::Masks64Plain>::type;
     ort::FastStateT<Masks> st;
     int k = -1;
+    int nst = 0;             // steps of the lane's walk (ORT_OPT_HEAVY_FIRST's record)
     int next = 0, end = 0;   // wave-uniform: remaining work items [next, end) of the wave's chunk
     bool drained = false;    // wave-uniform: the global cursor passed the item count
     // items: the compacted (sorted) alive-path list of a bounce >= 1, or every slot
     const int total = A.qlist ? *A.qcount : A.total;
+#if ORT_PERSIST_CLOCK  // analysis builds only (tools/build_variant.sh): per-wave timeline
+    const unsigned long long clk0 = __builtin_amdgcn_s_memrealtime();
+    unsigned long long clk_drain = 0;
+    int n_items = 0;
+#endif
     for (;;) {
         const unsigned long long idle = __ballot(k < 0);
         const int n_idle = __popcll(idle);
@@ -336,8 +351,14 @@ ort_trace_persistent(PipeArgs A) {
                 base = __shfl(base, 0);
                 if (base >= total) {
                     drained = true;
+#if ORT_PERSIST_CLOCK
+                    clk_drain = __builtin_amdgcn_s_memrealtime();
+#endif
                     continue;
                 }
+#if ORT_PERSIST_CLOCK
+                n_items += min(base + kChunk, total) - base;
+#endif
                 next = base;
                 end = min(base + kChunk, total);
             }
@@ -354,6 +375,7 @@ ort_trace_persistent(PipeArgs A) {
                             A.defer_list[atomicAdd(A.sync, 1)] = cand;
                         } else {
                             if (COUNT) cnt.v[5] += 1;
+                            nst = 0;
                             if (ort::fast_begin(A.S, L.planes, lut, ray, inv, 0.001f, ORT_MAXFLOAT, st)) k = cand;
                             else A.hit[cand] = make_int2(-1, 0);
                         }
@@ -364,12 +386,22 @@ ort_trace_persistent(PipeArgs A) {
             continue;
         }
         if (k >= 0) {
+            ++nst;
             if (ort::fast_step<COUNT>(A.S, lut, st, L.fr, cnt)) {
                 A.hit[k] = make_int2(st.hitEntry, __float_as_int(st.closest));
+                if (!COUNT && A.bcost_w) A.bcost_w[k] = (uint16_t)min(nst, 65535);
                 k = -1;
             }
         }
     }
+#if ORT_PERSIST_CLOCK
+    const int gw = (int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+    if (A.wclock && lane == 0 && gw < A.wclock_n) {
+        const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);  // XCC_ID
+        A.wclock[gw] = make_ulonglong4(clk0, clk_drain, __builtin_amdgcn_s_memrealtime(),
+                                       (unsigned long long)(xcc & 15u) | ((unsigned long long)n_items << 8));
+    }
+#endif
     flush_counts<COUNT>(cnt, A.counters);
 }
 
@@ -522,6 +554,26 @@ __device__ inline void append_slots(bool go, int k, uint32_t key, int* list, uin
     }
 }
 
+// Heavy first (ORT_OPT_HEAVY_FIRST): the key of a path appended to the next bounce's list gets
+// a 2-bit cost class above its coherence bits, from the steps c that bounce's walk took in
+// the previous frame of the same shape: 0 for c >= 4T, 1 for >= 2T, 2 for >= T, 3 below (T =
+// A.heavy) -- the list sort then puts the longest walks first, each class in coherence order,
+// and the persistent trace starts them early instead of in its drain tail.
+#ifndef ORT_HEAVY_LEVELS
+#define ORT_HEAVY_LEVELS 3  // classes above the lightest (1: one threshold)
+#endif
+#ifndef ORT_HEAVY_RATIO_LOG2
+#define ORT_HEAVY_RATIO_LOG2 1  // class thresholds T, 2T, 4T
+#endif
+constexpr int kHeavyKeyBits = ORT_HEAVY_LEVELS > 1 ? 2 : 1;
+__device__ __forceinline__ uint32_t light_bit(const uint16_t* bcost_r, int heavy, int k) {
+    if (!bcost_r) return 0u;
+    const int c = bcost_r[k];
+    uint32_t cls = ORT_HEAVY_LEVELS;
+    for (int l = 0; l < ORT_HEAVY_LEVELS; ++l) cls -= c >= (heavy << (ORT_HEAVY_RATIO_LOG2 * l)) ? 1u : 0u;
+    return cls << ort::kPathKeyBits;
+}
+
 // One ray per lane over the compact layout (default): the tile-block order of the path
 // slots keeps each wave on an 8x8 pixel block, whose rays walk nearly the same nodes.
 // DEEP: trees deeper than 8 levels need the 96-bit level masks (ort_trace_compact_deep).
@@ -667,7 +719,8 @@ __device__ __forceinline__ void trace_compact_body(PipeArgs& A, unsigned char* s
         typedef __attribute__((address_space(4))) const PipeArgs KernArgs;
         KernArgs* kp = (KernArgs*)__builtin_amdgcn_kernarg_segment_ptr();
         uint32_t key = 0;
-        if (go && kp->qnext_keys) key = ort::path_key(kp->po[k], kp->pd[k], kp->mp, kp->key_spread);  // the state just stored
+        if (go && kp->qnext_keys)  // the state just stored
+            key = ort::path_key(kp->po[k], kp->pd[k], kp->mp, kp->key_spread) | light_bit(kp->bcost_r, kp->heavy, k);
         append_slots(go, k, key, kp->qnext, kp->qnext_keys, kp->qnext_count);
 #endif
     }
@@ -992,7 +1045,8 @@ __global__ void __launch_bounds__(kBlock) ort_trace_exact(PipeArgs A) {
             if (shade_state<0, true, false>(A, k, (size_t)row * A.tm.tw + col, ray, rng, st == ORT_TRACE_HIT ? entry : -1, t)) {
                 const int pos = atomicAdd(A.qnext_count, 1);
                 A.qnext[pos] = k;
-                if (A.qnext_keys) A.qnext_keys[pos] = ort::path_key(A.po[k], A.pd[k], A.mp, A.key_spread);
+                if (A.qnext_keys)
+                    A.qnext_keys[pos] = ort::path_key(A.po[k], A.pd[k], A.mp, A.key_spread) | light_bit(A.bcost_r, A.heavy, k);
             }
         } else {
             A.hit[k] = make_int2(st == ORT_TRACE_HIT ? entry : -1, __float_as_int(t));
@@ -1058,7 +1112,8 @@ __global__ void __launch_bounds__(kBlock) ort_shade_kernel(PipeArgs A) {
     const bool go = in && shade_slot<MODE, FIRST, DIRECT>(A, k);
     if (!DIRECT && A.qnext) {
         uint32_t key = 0;
-        if (go && A.qnext_keys) key = ort::path_key(A.po[k], A.pd[k], A.mp, A.key_spread);  // the state just stored
+        if (go && A.qnext_keys)  // the state just stored
+            key = ort::path_key(A.po[k], A.pd[k], A.mp, A.key_spread) | light_bit(A.bcost_r, A.heavy, k);
         append_slots(go, k, key, A.qnext, A.qnext_keys, A.qnext_count);
     }
 }
@@ -1090,6 +1145,9 @@ struct DevBuf {
 
 }  // namespace
 
+#ifndef ORT_HEAVY_STEPS
+#define ORT_HEAVY_STEPS 64  // ORT_OPT_HEAVY_FIRST default: classes >= 256, >= 128, >= 64 steps
+#endif
 struct ort_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -1133,6 +1191,12 @@ struct ort_ctx {
     int cost_order = 1;
     DevBuf pcost;
     unsigned long long cost_sig = 0;
+    // ORT_OPT_HEAVY_FIRST: threshold in walk steps (0 off); bcost holds, per bounce >= 1 of the
+    // first kCostBounces of a frame, every slot's last walk steps (cleared with cost_sig)
+    static constexpr int kCostBounces = 8;
+    int heavy_first = ORT_HEAVY_STEPS;
+    DevBuf bcost;
+    unsigned long long bcost_sig = 0;
     float root_lo[3] = {0, 0, 0}, root_hi[3] = {0, 0, 0};  // root box (coherence-sort key)
     DevBuf lut;         // rank LUT (global copy, for the packet kernel)
     ort::GpuTree tree;  // reference-layout tree of the last ort_build_scene(keep_tree)
@@ -1702,6 +1766,20 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
         }
         a.pcost = (uint16_t*)ctx->pcost.p;
     }
+    // heavy first: the bounce >= 1 lists of the persistent trace (sorted, default path)
+    const int nbc = std::min(ns * (maxd > 0 ? maxd : 1), ort_ctx::kCostBounces);  // recorded bounce indices
+    uint16_t* bcost = nullptr;
+    if (listsort && mode == 0 && pers_bounce && ctx->heavy_first > 0) {
+        if ((rc = ensure(ctx, ctx->bcost, 2 * slots * (size_t)nbc))) return rc;
+        const unsigned long long sig = frame_sig(ctx, p, t);
+        if (sig != ctx->bcost_sig) {  // a new shape: no heavy walks known
+            HIPCHK(ctx, hipMemsetAsync(ctx->bcost.p, 0, 2 * slots * (size_t)nbc, s));
+            ctx->bcost_sig = sig;
+        }
+        bcost = (uint16_t*)ctx->bcost.p;
+        a.heavy = ctx->heavy_first;
+    }
+    const int key_bits = bcost ? ort::kPathKeyBits + kHeavyKeyBits : ort::kPathKeyBits;
     const size_t lds = lds_bytes(mode, ctx->depth, false);
     const size_t lds_exact = lds_bytes(mode, ctx->depth, true);
     const int pblocks = (mode == 0 && ctx->persistent) ? persistent_blocks(ctx->device, dcounters != nullptr, ctx->depth > 8, ctx->depth, lds, blocks) : 0;
@@ -1744,11 +1822,21 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                 const bool prim = (b == 0) && !a.rays_stored;
                 const int pb = (pers_all || (pers_bounce && b > 0)) ? pblocks : 0;
                 PipeArgs at = a;
+                if (pb > 0 && a.wclock) {  // analysis (ORT_PERSIST_CLOCK): a record range per launch
+                    const long long nw = (long long)pb * (ctx->depth > 8 ? kPersistDeepBlock : kBlock) / 64;
+                    at.wclock = (seg + 1) * nw <= ctx->wclock_n ? a.wclock + seg * nw : nullptr;
+                    at.wclock_n = (int)nw;
+                }
                 if (fmode == 2) {  // the trace kernels append bounce 1's list (as ort_shade_kernel would)
                     HIPCHK(ctx, hipMemsetAsync(qcnt[cur ^ 1], 0, sizeof(int), s));
                     at.qnext = qbuf[cur ^ 1];
                     at.qnext_count = qcnt[cur ^ 1];
                     at.qnext_keys = listsort ? (uint32_t*)ctx->skeys.p : nullptr;
+                }
+                {   // heavy first: record index smp * bounces + b (bounces >= 1 only)
+                    const int hi = smp * bounces + b;
+                    if (bcost && pb > 0 && b > 0 && hi < nbc) at.bcost_w = bcost + (size_t)hi * slots;
+                    if (bcost && fmode == 2 && hi + 1 < nbc && b + 1 < bounces) at.bcost_r = bcost + (size_t)(hi + 1) * slots;
                 }
                 e = dcounters ? launch_trace<true>(mode, prim, at, (int)blocks, pb, lds, s, ctx->packet != 0, fmode, qblocks)
                               : launch_trace<false>(mode, prim, at, (int)blocks, pb, lds, s, ctx->packet != 0, fmode, qblocks);
@@ -1795,6 +1883,8 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                     a2.qnext = qbuf[cur ^ 1];
                     a2.qnext_count = qcnt[cur ^ 1];
                     a2.qnext_keys = listsort ? (uint32_t*)ctx->skeys.p : nullptr;
+                    const int hn = smp * bounces + b + 1;  // the next bounce's record
+                    if (bcost && hn < nbc) a2.bcost_r = bcost + (size_t)hn * slots;
                 }
                 e = launch_shade(mode, b == 0, direct, a2, (int)blocks, s);
                 if (e != hipSuccess) return hip_fail(ctx, e, "ort_shade_kernel launch");
@@ -1829,7 +1919,7 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                         // (key, path) pairs as the shade / trace kernels appended them
                         const ort::SortBuffers sb{(uint32_t*)ctx->skeys.p, (uint32_t*)ctx->skeys2.p, qbuf[cur],
                                                   (int*)ctx->svals.p};
-                        e = ort::sortListBounded(ctx->qtemp.p, qtemp_bytes, (int)bound, qcnt[cur], sb, s);
+                        e = ort::sortListBounded(ctx->qtemp.p, qtemp_bytes, (int)bound, qcnt[cur], sb, s, key_bits);
                         if (e != hipSuccess) return hip_fail(ctx, e, "path list sort");
                         if (hi < ort_ctx::kHints)  // the next frame's bound (pinned: no host wait)
                             HIPCHK(ctx, hipMemcpyAsync(ctx->alive_host + hi, qcnt[cur], sizeof(int),
@@ -1968,6 +2058,11 @@ int ort_set_option(ort_ctx* ctx, int option, int value) {
     if (option == ORT_OPT_SORT_PATHS) {
         if (value < 0 || value > 2) return fail(ctx, ORT_ERR_INVALID_ARG, "sort_paths must be 0, 1 or 2");
         ctx->sort_paths = value;
+        return ORT_OK;
+    }
+    if (option == ORT_OPT_HEAVY_FIRST) {
+        if (value < 0 || value > 65535) return fail(ctx, ORT_ERR_INVALID_ARG, "ORT_OPT_HEAVY_FIRST: 0 (off) .. 65535 steps");
+        ctx->heavy_first = value;
         return ORT_OK;
     }
     if (option == ORT_OPT_COST_ORDER) {

@@ -149,6 +149,11 @@ class Renderer:
         """Testing (ORT_OPT_SORT_BOUND): force the list sort's size; 0 = the previous-frame hint."""
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_SORT_BOUND, int(bound)))
 
+    def set_heavy_first(self, steps: int):
+        """ORT_OPT_HEAVY_FIRST: bounce lists ordered by last frame's walk steps in classes >= 4T, >= 2T,
+        >= T (T = steps, default 64), the rest last; 0 off (coherence order only).  Same pixels."""
+        self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_HEAVY_FIRST, int(steps)))
+
     def set_cost_order(self, on: int):
         """ORT_OPT_COST_ORDER: 1 (default) camera rays dealt to waves by last frame's walk cost; 0 fixed blocks."""
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_COST_ORDER, int(on)))

@@ -71,3 +71,36 @@ def test_cost_order_option_range(ort):
             r.set_cost_order(2)
         r.set_cost_order(0)
         r.set_cost_order(1)
+
+
+@pytest.mark.parametrize("depth", [6, 9])
+def test_heavy_first_frames_match_coherence_order(ort, oracle, depth):
+    """Heavy first (ORT_OPT_HEAVY_FIRST): a 4-bounce frame rendered three times (the second and
+    third sort each bounce list with the previous frame's walk steps) at thresholds 0 (off), 8
+    (most walks heavy) and 48, on the depth <= 8 and the depth 9-10 persistent kernel: every
+    frame bit-identical, and to the oracle."""
+    s = ort.random_spheres(20000, 42)
+    t = ort.build_octree(s, depth, 0)
+    W, H = 480, 270
+    p = ort.FrameParams.default_camera(W, H, num_samples=1, max_depth=4)
+    got = {}
+    for thr in (0, 8, 48):
+        with ort.Renderer(0) as r:
+            r.upload(s, t)
+            r.set_heavy_first(thr)
+            got[thr] = [r.render(p) for _ in range(3)]
+    for thr in (8, 48):
+        for i in range(3):
+            assert_same(got[thr][i], got[0][i], f"depth {depth}, heavy >= {thr}, frame {i} vs coherence order")
+    ref = oracle.render(s, t, p, 0, 120, W, 8, threads=0)
+    assert_same(got[48][2][120:128], ref, f"depth {depth} heavy first vs oracle")
+
+
+def test_heavy_first_option_range(ort):
+    with ort.Renderer(0) as r:
+        with pytest.raises(ort.OrtError):
+            r.set_heavy_first(-1)
+        with pytest.raises(ort.OrtError):
+            r.set_heavy_first(70000)
+        r.set_heavy_first(0)
+        r.set_heavy_first(384)
