@@ -50,6 +50,22 @@ CONFIGS = {
     "c3": (3840, 2160, 100_000, 8, 0, 1, 1),
     "c5": (7680, 4320, 1_000_000, 10, 1, 1, 4),
 }
+
+
+def default_inflight(config: str, world: int) -> int:
+    """Frames in flight by default: 2 when a GPU's share of a frame is at most 40 M pixel-bounces,
+    where the longest walks' drain at the end of every launch would otherwise idle much of the
+    GPU (a second frame's launches fill it); 1 for larger shares, where two frames' working
+    sets only compete for the caches.  Measured (tools/host_overhead.py, rank 0's band tile,
+    profiles/r03_host_overhead_d.log; bench.py N=1): C3 full frame 1.753 -> 1.672 ms/frame,
+    C3 1/2, 1/4, 1/8 bands 0.944 -> 0.843, 0.660 -> 0.433, 0.481 -> 0.251; C5 1/4, 1/8 bands
+    11.91 -> 11.57, 7.18 -> 6.09; but C5 full frame 42.26 -> 46.30 and C5 1/2 band 21.78 ->
+    22.93 ms/frame."""
+    W, H, _, _, _, NS, MAXD = CONFIGS[config]
+    share = W * H / max(1, world) * max(1, NS) * max(1, MAXD)
+    return 2 if share <= 40e6 else 1
+
+
 BASELINE_METRIC = "Mrays/sec at 3840x2160, 100k spheres, depth 8; 1/2/4/8-GPU scaling"
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 SIMDS = 1024                # 256 CUs x 4 SIMDs
@@ -76,8 +92,8 @@ def parse(argv=None):
                     help="PMC record of the trace kernels (default profiles/pmc_<config>.json, written by "
                     "tools/summarize_profile.py)")
     ap.add_argument("--inflight", type=int, default=0,
-                    help="frames in flight, each on its own context and stream (0 = auto: 1 on one GPU, "
-                    "2 with N>1, where a band tile's tail would otherwise idle the GPU)")
+                    help="frames in flight, each on its own context and stream (0 = auto, default_inflight: 2 "
+                    "when a GPU's share of the frame is small enough that its walks' tail would idle it)")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="testing only: every rank on GPU 0 with the gloo backend (exercises the N>1 code "
                     "path on a one-GPU box; not a measurement)")
@@ -245,7 +261,7 @@ def main():
     if args.emulate:
         return emulate(args, world, rank)
     local = 0 if args.rehearse_one_gpu else int(os.environ.get("LOCAL_RANK", "0"))
-    inflight = args.inflight or (1 if world == 1 else 2)
+    inflight = args.inflight or default_inflight(args.config, world)
     if inflight > 1:
         # frames in flight only overlap when their streams sit on different hardware queues;
         # with HIP's default 4 queues per process, RCCL's and torch's streams share them
@@ -358,31 +374,37 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
 
-    # N > 1 with frames in flight: also time one frame in flight (the N = 1 line's setting), so
-    # a scaling ratio can be taken at equal settings; per frame render + gather + assembly,
-    # the next frame only after it (after the main timed region; not part of `value`)
+    # with frames in flight: also time one frame in flight, so that lines of different frame
+    # counts can be compared at equal settings; per frame render + gather + assembly, the next
+    # frame's render queued behind them on the GPU (no host wait; after the main timed region,
+    # not part of `value`)
     single = None
-    if world > 1 and inflight > 1 and args.single_steps > 0:
+    if inflight > 1 and args.single_steps > 0:
         sev = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for _ in range(args.single_steps)]
         torch.cuda.synchronize()
-        dist.barrier()
+        if world > 1:
+            dist.barrier()
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         for k in range(args.single_steps):
             st = streams[0]
-            st.wait_stream(gstream)
+            if world > 1:
+                st.wait_stream(gstream)
             torch.cuda.set_stream(st)
             sev[k][0].record(st)
             rs[0].render(p, tile, out=outs[0], stream=st.cuda_stream)
             sev[k][1].record(st)
-            pending.append((gather.submit(outs[0], 0), sev[k][2]))
-            drain(0)
-            gstream.synchronize()
+            if world == 1:
+                sev[k][2].record(st)  # no gather: the frame is complete when its render is
+            pending.append((gather.submit(outs[0], 0), sev[k][2] if world > 1 else None))
+            drain(0)  # the next render waits (on the GPU) for this frame's gather and assembly
         torch.cuda.synchronize()
-        dist.barrier()
+        if world > 1:
+            dist.barrier()
         torch.cuda.synchronize()
         t_single = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t_single, op=dist.ReduceOp.MAX)
+        if world > 1:
+            dist.all_reduce(t_single, op=dist.ReduceOp.MAX)
         single = (float(t_single.item()), [a.elapsed_time(c) for a, _, c in sev])
 
     # algorithmic traffic of this rank's launch (counting variant, untimed); the traced rays
@@ -433,8 +455,8 @@ def main():
                 "value": round(rays_per_frame * args.single_steps / single[0] / 1e6, 2),
                 "ms_per_step": round(single[0] / args.single_steps * 1e3, 4),
                 "frame_latency_ms_avg": round(float(np.mean(single[1])), 4),
-                "note": "one frame in flight (render, gather, assembly, then the next): the setting of the N=1 "
-                        "line; `value` above keeps frames_in_flight frames in flight"},
+                "note": "one frame in flight (render, gather, assembly, then the next); `value` above keeps "
+                        "frames_in_flight frames in flight"},
             "trace_kernels_ms_avg": round(float(np.mean(trace_ms)), 4),
             "trace_launches_per_frame": launches,
             "first_trace_kernel_ms_avg": round(float(np.mean(first_trace_ms)), 4),
@@ -473,7 +495,7 @@ def group_bench(args):
     a single-context ort_render of the same scene, bit for bit."""
     W, H, NSPH, DEPTH, MPN, NS, MAXD = CONFIGS[args.config]
     N = args.gpus
-    inflight = args.inflight or (1 if N == 1 else 2)
+    inflight = args.inflight or default_inflight(args.config, N)
     if inflight > 1:  # as main(): frame slots overlap only on distinct hardware queues
         os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, max(8, 4 * inflight)))
     import torch
