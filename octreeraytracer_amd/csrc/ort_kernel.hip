@@ -310,6 +310,12 @@ __global__ void __launch_bounds__(kBlock) ort_raygen_kernel(PipeArgs A) {
 #define ORT_CHUNK 64
 #endif
 constexpr int kChunk = ORT_CHUNK;
+// Lists of at least ORT_CHUNK_ADAPT items per resident wave take chunks of 2 x kChunk: C5
+// +0.7 % (bounces 1-2 of the full frame), band tiles unchanged (tools/ab_stream.py); fixed
+// 128-item chunks lost 20 % on a 1/8 band (too few chunks per wave to balance).  0: kChunk.
+#ifndef ORT_CHUNK_ADAPT
+#define ORT_CHUNK_ADAPT 1024
+#endif
 
 // DEEP: trees deeper than 8 levels (96-bit masks, lean state); depth <= 8 takes the
 // primary-ray walk's 64-bit masks and reversed plane tables (71 VGPRs, 7 waves/SIMD).
@@ -335,6 +341,12 @@ ort_trace_persistent(PipeArgs A) {
     bool drained = false;    // wave-uniform: the global cursor passed the item count
     // items: the compacted (sorted) alive-path list of a bounce >= 1, or every slot
     const int total = A.qlist ? *A.qcount : A.total;
+#if ORT_CHUNK_ADAPT
+    // long lists (>= ORT_CHUNK_ADAPT items per resident wave): twice the chunk
+    const int chunk = total >= (int)(gridDim.x * (blockDim.x >> 6)) * ORT_CHUNK_ADAPT ? 2 * kChunk : kChunk;
+#else
+    constexpr int chunk = kChunk;
+#endif
 #if ORT_PERSIST_CLOCK  // analysis builds only (tools/build_variant.sh): per-wave timeline
     const unsigned long long clk0 = __builtin_amdgcn_s_memrealtime();
     unsigned long long clk_drain = 0;
@@ -347,7 +359,7 @@ ort_trace_persistent(PipeArgs A) {
         if (!drained && n_idle >= A.refill) {
             if (next == end) {
                 int base = 0;
-                if (lane == 0) base = atomicAdd(A.sync + 1, kChunk);
+                if (lane == 0) base = atomicAdd(A.sync + 1, chunk);
                 base = __shfl(base, 0);
                 if (base >= total) {
                     drained = true;
@@ -357,10 +369,10 @@ ort_trace_persistent(PipeArgs A) {
                     continue;
                 }
 #if ORT_PERSIST_CLOCK
-                n_items += min(base + kChunk, total) - base;
+                n_items += min(base + chunk, total) - base;
 #endif
                 next = base;
-                end = min(base + kChunk, total);
+                end = min(base + chunk, total);
             }
             const int take = min(n_idle, end - next);
             if (k < 0) {
