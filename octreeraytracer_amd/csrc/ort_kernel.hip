@@ -673,10 +673,14 @@ __device__ __forceinline__ bool trace_slot(PipeArgs& A, LdsView& L, int k, ort::
 #ifndef ORT_COST_SHIFT
 #define ORT_COST_SHIFT 2  // bucket = steps >> shift (64 buckets)
 #endif
+#ifndef ORT_COST_SHIFT_DEEP
+#define ORT_COST_SHIFT_DEEP 2  // the depth 9-10 camera kernel's bucket width
+#endif
+template <int SHIFT>
 __device__ __forceinline__ int cost_order_slot(const uint16_t* pcost, int* sc, int k) {
 #if defined(__HIP_DEVICE_COMPILE__)
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const uint32_t b = min((uint32_t)pcost[k] >> ORT_COST_SHIFT, 63u);
+    const uint32_t b = min((uint32_t)pcost[k] >> SHIFT, 63u);
     uint64_t m = ~0ull;  // the lanes of this wave in the same bucket
     for (int i = 0; i < 6; ++i) {
         const uint64_t bal = __ballot((b >> i) & 1u);
@@ -721,7 +725,7 @@ __device__ __forceinline__ void trace_compact_body(PipeArgs& A, unsigned char* s
     if (!PRIMARY && A.qlist && (int)(blockIdx.x * kBlock) >= *A.qcount) return;  // whole block past the list
     LdsView L = setup_lds<true>(smem, A.S);
     int k = blockIdx.x * kBlock + threadIdx.x;
-    if (PRIMARY && !COUNT && A.pcost) k = cost_order_slot(A.pcost, L.fr.co, k);  // (the counting pass: tile order)
+    if (PRIMARY && !COUNT && A.pcost) k = cost_order_slot<DEEP ? ORT_COST_SHIFT_DEEP : ORT_COST_SHIFT>(A.pcost, L.fr.co, k);  // (the counting pass: tile order)
     if (!PRIMARY && !list_slot(A, k)) return;
     ort::Counters cnt;
     for (int q = 0; q < 6; ++q) cnt.v[q] = 0;
