@@ -15,7 +15,10 @@
 
 namespace ort {
 
-constexpr int kMortonBits = 21;
+#ifndef ORT_MORTON_BITS
+#define ORT_MORTON_BITS 21
+#endif
+constexpr int kMortonBits = ORT_MORTON_BITS;
 constexpr int kPathKeyBits = 3 + kMortonBits + 6;  // 30: alive keys < 2^30, dead = 0xffffffff
 
 struct MortonPlan {
