@@ -705,9 +705,24 @@ __global__ void __launch_bounds__(kB) k_overflow_copy(const int* vals_in, int* v
 
 }  // namespace
 
+// The path-list sorts' rocPRIM configuration.  rocPRIM 4.2 has no tuned onesweep entry for
+// gfx950 and falls back to 4 radix bits per pass (eight passes over a 32-bit key); this is its
+// gfx942 entry for 4-byte keys with 4-byte values: 8 bits per pass, 1024 x 8 items per block.
+#ifndef ORT_SORT_RADIX_BITS
+#define ORT_SORT_RADIX_BITS 8
+#endif
+#if ORT_SORT_RADIX_BITS > 0
+using ListSortConfig = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 8>, rocprim::kernel_config<1024, 8>,
+                                        ORT_SORT_RADIX_BITS, rocprim::block_radix_rank_algorithm::match>>;
+#else
+using ListSortConfig = rocprim::default_config;
+#endif
+
 hipError_t sortList(void* temp, size_t temp_bytes, int n, const SortBuffers& b, hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    return rocprim::radix_sort_pairs(temp, temp_bytes, b.keys_in, b.keys_out, b.vals_in, b.vals_out, (size_t)n, 0,
+    return rocprim::radix_sort_pairs<ListSortConfig>(temp, temp_bytes, b.keys_in, b.keys_out, b.vals_in, b.vals_out, (size_t)n, 0,
                                      kPathKeyBits, s);
 }
 
@@ -719,7 +734,7 @@ hipError_t sortListBounded(void* temp, size_t temp_bytes, int bound, const int* 
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     // stable LSD sort: a real key equal to the pad's low key_bits stays ahead of the pads
-    e = rocprim::radix_sort_pairs(temp, temp_bytes, b.keys_in, b.keys_out, b.vals_in, b.vals_out, (size_t)bound, 0,
+    e = rocprim::radix_sort_pairs<ListSortConfig>(temp, temp_bytes, b.keys_in, b.keys_out, b.vals_in, b.vals_out, (size_t)bound, 0,
                                   key_bits, s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_overflow_copy, dim3(kGrid), dim3(kB), 0, s, (const int*)b.vals_in, b.vals_out, count, bound);
@@ -728,7 +743,7 @@ hipError_t sortListBounded(void* temp, size_t temp_bytes, int bound, const int* 
 
 size_t sortAliveTempBytes(int n) {
     size_t tb = 0;
-    (void)rocprim::radix_sort_pairs(nullptr, tb, (uint32_t*)nullptr, (uint32_t*)nullptr, (int*)nullptr, (int*)nullptr,
+    (void)rocprim::radix_sort_pairs<ListSortConfig>(nullptr, tb, (uint32_t*)nullptr, (uint32_t*)nullptr, (int*)nullptr, (int*)nullptr,
                                     (size_t)std::max(n, 1), 0, 31);
     return tb;
 }
@@ -743,7 +758,7 @@ hipError_t sortAlive(void* temp, size_t temp_bytes, const float4* po, const floa
     if ((e = hipGetLastError()) != hipSuccess) return e;
     // alive keys are < 2^30, dead keys 0xffffffff: on bits [0, 31) every dead key sorts after
     // every alive one
-    return rocprim::radix_sort_pairs(temp, temp_bytes, b.keys_in, b.keys_out, b.vals_in, b.vals_out, (size_t)n, 0, 31, s);
+    return rocprim::radix_sort_pairs<ListSortConfig>(temp, temp_bytes, b.keys_in, b.keys_out, b.vals_in, b.vals_out, (size_t)n, 0, 31, s);
 }
 
 }  // namespace ort
