@@ -379,6 +379,7 @@ def main():
     # frame's render queued behind them on the GPU (no host wait; after the main timed region,
     # not part of `value`)
     single = None
+    trace_ms_in_flight = None
     if inflight > 1 and args.single_steps > 0:
         sev = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for _ in range(args.single_steps)]
         torch.cuda.synchronize()
@@ -406,6 +407,12 @@ def main():
         if world > 1:
             dist.all_reduce(t_single, op=dist.ReduceOp.MAX)
         single = (float(t_single.item()), [a.elapsed_time(c) for a, _, c in sev])
+        # the trace kernels of these frames ran alone on the GPU: the roofline's kernel times
+        # (with frames in flight, two frames' kernels overlap and each launch lasts longer)
+        n_single = min(args.single_steps, 64)
+        first_trace_ms = r.trace_times_ms(n_single)
+        ftrace_iso = r.frame_trace_times_ms(n_single)
+        trace_ms_in_flight, trace_ms = trace_ms, [m for m, _ in ftrace_iso]
 
     # algorithmic traffic of this rank's launch (counting variant, untimed); the traced rays
     # of a step = traversals summed over the ranks (W*H*spp for primary-only configs)
@@ -458,6 +465,10 @@ def main():
                 "note": "one frame in flight (render, gather, assembly, then the next); `value` above keeps "
                         "frames_in_flight frames in flight"},
             "trace_kernels_ms_avg": round(float(np.mean(trace_ms)), 4),
+            # with frames in flight: trace_kernels_ms_avg and the first-trace figures are taken over
+            # the one-frame-in-flight phase (kernels alone on the GPU); this is the main loop's
+            "trace_kernels_ms_avg_in_flight": None if trace_ms_in_flight is None
+            else round(float(np.mean(trace_ms_in_flight)), 4),
             "trace_launches_per_frame": launches,
             "first_trace_kernel_ms_avg": round(float(np.mean(first_trace_ms)), 4),
             "first_trace_kernel_ms_min": round(float(np.min(first_trace_ms)), 4),
