@@ -72,3 +72,17 @@ def test_render_rejects_a_bad_numpy_out_before_the_abi(ort, bad):
            "short": np.empty((15, 32, 3), np.float32)}[bad]
     with pytest.raises(ValueError):
         r.render(p, out=out)
+
+
+def test_header_constants_match_the_bindings():
+    """Every #define ORT_OPT_* / ORT_ERR_* / ORT_LAYOUT_* / ORT_COUNT_* in include/ort.h has the same
+    value in octreeraytracer_amd/_lib.py (the options the Renderer setters pass through)."""
+    from octreeraytracer_amd import _lib
+    text = (ROOT / "include" / "ort.h").read_text()
+    defs = dict(re.findall(r"#define\s+(ORT_(?:OPT|ERR|LAYOUT|COUNT)_[A-Z0-9_]+)\s+(-?\d+)\b", text))
+    assert "ORT_OPT_COST_ORDER" in defs and "ORT_OPT_HEAVY_FIRST" in defs
+    missing = [k for k in defs if not hasattr(_lib, k)]
+    wrong = {k: (int(v), getattr(_lib, k)) for k, v in defs.items() if hasattr(_lib, k) and getattr(_lib, k) != int(v)}
+    assert not wrong, wrong
+    # every option has a binding constant (the setters use them)
+    assert not [k for k in missing if k.startswith("ORT_OPT_")], missing
