@@ -612,9 +612,12 @@ def trace_kernel_names(cfg, info, maxd, ns):
     """The trace kernels a frame of this config launches (ort_kernel.hip render_impl)."""
     deep = info["tree_depth"] > 8
     if maxd == 1 and ns == 1:
-        return ["ort_trace_compact%s<false, true, true> (camera rays + walk + shading)" % ("_deep" if deep else "")]
-    return ["ort_trace_compact%s<false, true, false> (camera rays + walk)" % ("_deep" if deep else ""),
-            "ort_trace_persistent<false, %s> (bounces >= 1, sorted alive paths, lane refill)" % str(deep).lower()]
+        return ["ort_trace_compact%s<false, true, 1> (camera rays + walk + shading into the frame)"
+                % ("_deep" if deep else "")]
+    return ["ort_trace_compact%s<false, true, 2> (camera rays + walk + bounce-0 shading, cost order)"
+            % ("_deep" if deep else ""),
+            "ort_trace_persistent<false, %s> (bounces >= 1, sorted alive paths heavy first, lane refill)"
+            % str(deep).lower()]
 
 
 def emulate(args, world, rank):
