@@ -699,6 +699,13 @@ struct Masks64 {  // levels 0..7: trees of depth <= 8
     static constexpr bool kLeadLeaves = false;
     static constexpr bool kRevPlanes = true;  // depth <= 8: reversed plane tables (fast_rev_planes)
     static constexpr bool kKeepNear = true;   // keep the node's near-plane pointers (FastStateT::nA..)
+    // the pop also reads the popped node's mid planes (FastStateT::tMA..), so their LDS reads
+    // overlap the record load instead of following it (most pops here are internal nodes: the
+    // leaves are tested inline)
+#ifndef ORT_PRE_MID
+#define ORT_PRE_MID 1
+#endif
+    static constexpr bool kPreMid = ORT_PRE_MID;
     // rejected-sphere skip (kid_table.h): off in the depth <= 8 camera-ray walk, whose inline
     // leaf children already avoid most leaf pops (C3 5 % slower with it); on in the bounce
     // walks and the deep camera walk (Masks96)
@@ -731,6 +738,10 @@ struct Masks64 {  // levels 0..7: trees of depth <= 8
 };
 struct Masks96 {  // levels 0..9 (ORT_COMPACT_MAX_DEPTH 10)
     static constexpr bool kInlineLeaves = false;
+#ifndef ORT_PRE_MID_DEEP
+#define ORT_PRE_MID_DEEP 0
+#endif
+    static constexpr bool kPreMid = ORT_PRE_MID_DEEP;
     // leading leaf children tested inline: C5 camera walk 19.45 -> 17.62 ms when added, but
     // with the rejected-sphere skip on (which drops most of those leaves before they are
     // pushed) 16.60 -> 15.37 ms without them (tools/ab_stream.py): off
@@ -824,6 +835,7 @@ struct FastStateT {
     const float* pC;
     int sA, sB, sC;   // +-4
     float tNA, tFA, tNB, tFB, tNC, tFC;  // near/far plane t of the current node's box
+    float tMA, tMB, tMC;                 // (kPreMid) its mid planes' t
     uint32_t cP;     // (not kRevPlanes) ray-order index of the current node's near plane, 10 bits per axis
     uint32_t otab;   // nibble r = octant of rank r; nibble 0 = m
     int node, depth;
@@ -866,6 +878,10 @@ using FastState = FastStateT<Masks96>;
 // the near-plane pointers cost occupancy, so it re-derives them from cP.
 struct Masks96Lean : Masks96 {
     static constexpr bool kKeepNear = false;
+#ifndef ORT_PRE_MID_BOUNCE
+#define ORT_PRE_MID_BOUNCE 0
+#endif
+    static constexpr bool kPreMid = ORT_PRE_MID_BOUNCE;
     // leading leaf children inline: C5 camera rays (deep kernel) 19.45 -> 17.62 ms, but the
     // persistent bounce kernel 4.8 ms slower per frame (tools/ab_stream.py): off there
 #ifndef ORT_LEAD_LEAVES_PERSISTENT
@@ -884,6 +900,7 @@ struct Masks96Lean : Masks96 {
 // (inline leaves pay off on coherent camera rays, not on scattered bounce rays).
 struct Masks64Plain : Masks64 {
     static constexpr bool kInlineLeaves = false;
+    static constexpr bool kPreMid = false;
     static constexpr bool kKidSkip = true;
 };
 
@@ -942,6 +959,11 @@ ORT_FN bool fast_begin(const KScene& S, const float* planes, const uint8_t* rank
         st.tFB = st.iB * (st.plane(st.aB + t4) - st.oB);
         st.tNC = st.iC * (st.plane(st.aC) - st.oC);
         st.tFC = st.iC * (st.plane(st.aC + t4) - st.oC);
+        if (Masks::kPreMid) {
+            st.tMA = st.iA * (st.plane(st.aA + st.h4) - st.oA);
+            st.tMB = st.iB * (st.plane(st.aB + st.h4) - st.oB);
+            st.tMC = st.iC * (st.plane(st.aC + st.h4) - st.oC);
+        }
     } else {
         const int S1 = fast_axis_floats(D);
         st.pA = planes + (swap ? S1 : 0) + (gA ? top : 0);
@@ -956,6 +978,11 @@ ORT_FN bool fast_begin(const KScene& S, const float* planes, const uint8_t* rank
         st.tFB = st.iB * (st.plB(top) - st.oB);
         st.tNC = st.iC * (st.plC(0) - st.oC);
         st.tFC = st.iC * (st.plC(top) - st.oC);
+        if (Masks::kPreMid) {
+            st.tMA = st.iA * (st.plA(top >> 1) - st.oA);
+            st.tMB = st.iB * (st.plB(top >> 1) - st.oB);
+            st.tMC = st.iC * (st.plC(top >> 1) - st.oC);
+        }
         st.cP = 0;
         if (Masks::kKeepNear) {
             st.nA = st.pA;
@@ -1093,7 +1120,11 @@ ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks
         const uint32_t rcm = rank_lut[((st.otab & 7u) << 8) | (rec.y & 0xffu)];  // LUT row m
         const int h = 1 << (D - 1 - st.depth);  // half the node's width, in plane steps
         float tMA, tMB, tMC;
-        if (Masks::kRevPlanes) {
+        if (Masks::kPreMid) {
+            tMA = st.tMA;
+            tMB = st.tMB;
+            tMC = st.tMC;
+        } else if (Masks::kRevPlanes) {
             const uint32_t h4 = st.h4;
             tMA = st.iA * (st.plane(st.aA + h4) - st.oA);
             tMB = st.iB * (st.plane(st.aB + h4) - st.oB);
@@ -1189,6 +1220,11 @@ ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks
         st.tFB = st.iB * (st.plane(st.aB + w4) - st.oB);
         st.tNC = st.iC * (st.plane(st.aC) - st.oC);
         st.tFC = st.iC * (st.plane(st.aC + w4) - st.oC);
+        if (Masks::kPreMid) {
+            st.tMA = st.iA * (st.plane(st.aA + st.h4) - st.oA);
+            st.tMB = st.iB * (st.plane(st.aB + st.h4) - st.oB);
+            st.tMC = st.iC * (st.plane(st.aC + st.h4) - st.oC);
+        }
     } else {
         const int keep = -2 * w;  // clears the offsets below the level-L ancestor
         {   // per 10-bit field: (c & keep) | (axis bit of rk ? w : 0)
@@ -1210,6 +1246,11 @@ ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks
         st.tFB = st.iB * (*st.at(nB, st.sB, w) - st.oB);
         st.tNC = st.iC * (nC[0] - st.oC);
         st.tFC = st.iC * (*st.at(nC, st.sC, w) - st.oC);
+        if (Masks::kPreMid) {  // (a leaf's half width is 0: its "mid" is never used)
+            st.tMA = st.iA * (*st.at(nA, st.sA, w >> 1) - st.oA);
+            st.tMB = st.iB * (*st.at(nB, st.sB, w >> 1) - st.oB);
+            st.tMC = st.iC * (*st.at(nC, st.sC, w >> 1) - st.oC);
+        }
     }
     return false;
 }
