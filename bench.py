@@ -63,7 +63,12 @@ def default_inflight(config: str, world: int) -> int:
     22.93 ms/frame."""
     W, H, _, _, _, NS, MAXD = CONFIGS[config]
     share = W * H / max(1, world) * max(1, NS) * max(1, MAXD)
-    return 2 if share <= 40e6 else 1
+    if share > 40e6:
+        return 1
+    # a 1/4 or 1/8 band: a third frame fills more of each frame's tail (C3 1/8 0.252 -> 0.231,
+    # 1/4 0.433 -> 0.426 ms/frame, C5 1/8 6.09 -> 5.83; a fourth was slower; at N = 1 and 2 a
+    # third changes nothing: profiles/r03_host_overhead_e.log, _f.log)
+    return 3 if world >= 4 else 2
 
 
 BASELINE_METRIC = "Mrays/sec at 3840x2160, 100k spheres, depth 8; 1/2/4/8-GPU scaling"
