@@ -46,7 +46,8 @@ def test_bench_ranks_assemble_the_c3_frame(c3_frame, world, tmp_path):
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
     line = json.loads(lines[0])
-    assert line["n_gpus"] == world and line["config"]["frames_in_flight"] == 2
+    import bench
+    assert line["n_gpus"] == world and line["config"]["frames_in_flight"] == bench.default_inflight("c3", world)
     assert line["config"]["rays_per_step"] == 3840 * 2160
     got = image.read_pfm(out)
     assert got.shape == c3_frame.shape and got.dtype == np.float32
@@ -71,5 +72,6 @@ def test_bench_group_rehearsal_is_bit_identical(world, inflight):
     assert line["frame_check"].startswith("bit-identical"), line["frame_check"]
     assert line["n_gpus"] == world and line["config"]["devices"] == [0] * world
     assert line["config"]["rays_per_step"] == 3840 * 2160
-    assert line["config"]["frames_in_flight"] == (inflight or 2)
+    import bench
+    assert line["config"]["frames_in_flight"] == (inflight or bench.default_inflight("c3", world))
     assert line["frame_latency_ms"] > 0 and line["single_frame"]["frame_latency_ms"] > 0
