@@ -211,9 +211,6 @@ __host__ __device__ inline void block_tile(const PipeArgs& A, int blk, int& bx, 
 // holds a slot of the same 256-slot block (the per-tile kernels), so the tile lookup -- two
 // integer divisions by the tile-grid width -- runs once per wave on the scalar unit.
 template <bool UNI = false>
-#ifndef ORT_WAVE_SHAPE
-#define ORT_WAVE_SHAPE 0  // pixels of one wave within its workgroup's 16x16 tile (experiment)
-#endif
 __host__ __device__ inline bool slot_coords(const PipeArgs& A, int k, int& col, int& row) {
 #if defined(__HIP_DEVICE_COMPILE__)
     const int blk = UNI ? __builtin_amdgcn_readfirstlane(k >> 8) : k >> 8;
@@ -223,16 +220,8 @@ __host__ __device__ inline bool slot_coords(const PipeArgs& A, int k, int& col, 
     const int tid = k & 255, wave = tid >> 6, lane = tid & 63;
     int bx, by;
     block_tile(A, blk, bx, by);
-#if ORT_WAVE_SHAPE == 1   // 16x4 pixels per wave
-    col = bx * 16 + (lane & 15);
-    row = by * 16 + wave * 4 + (lane >> 4);
-#elif ORT_WAVE_SHAPE == 2  // 4x16
-    col = bx * 16 + wave * 4 + (lane & 3);
-    row = by * 16 + (lane >> 2);
-#else                      // 8x8
-    col = bx * 16 + (wave & 1) * 8 + (lane & 7);
+    col = bx * 16 + (wave & 1) * 8 + (lane & 7);  // an 8x8 block per wave (16x4 and 4x16: no faster, §8)
     row = by * 16 + (wave >> 1) * 8 + (lane >> 3);
-#endif
     return col < A.tm.tw && row < A.tm.th;
 }
 
