@@ -566,7 +566,7 @@ __device__ inline void append_slots(bool go, int k, uint32_t key, int* list, uin
 #ifndef ORT_HEAVY_RATIO_LOG2
 #define ORT_HEAVY_RATIO_LOG2 1  // class thresholds T, 2T, 4T
 #endif
-constexpr int kHeavyKeyBits = ORT_HEAVY_LEVELS > 1 ? 2 : 1;
+constexpr int kHeavyKeyBits = ORT_HEAVY_LEVELS > 3 ? 3 : (ORT_HEAVY_LEVELS > 1 ? 2 : 1);
 __device__ __forceinline__ uint32_t light_bit(const uint16_t* bcost_r, int heavy, int k) {
     if (!bcost_r) return 0u;
     const int c = bcost_r[k];
