@@ -706,6 +706,7 @@ struct Masks64 {  // levels 0..7: trees of depth <= 8
 #define ORT_PRE_MID 1
 #endif
     static constexpr bool kPreMid = ORT_PRE_MID;
+    static_assert(!kPreMid || kInlineLeaves, "the pop's mid-plane reads rely on never popping a level-D leaf");
     // rejected-sphere skip (kid_table.h): off in the depth <= 8 camera-ray walk, whose inline
     // leaf children already avoid most leaf pops (C3 5 % slower with it); on in the bounce
     // walks and the deep camera walk (Masks96)
@@ -960,9 +961,10 @@ ORT_FN bool fast_begin(const KScene& S, const float* planes, const uint8_t* rank
         st.tNC = st.iC * (st.plane(st.aC) - st.oC);
         st.tFC = st.iC * (st.plane(st.aC + t4) - st.oC);
         if (Masks::kPreMid) {
-            st.tMA = st.iA * (st.plane(st.aA + st.h4) - st.oA);
-            st.tMB = st.iB * (st.plane(st.aB + st.h4) - st.oB);
-            st.tMC = st.iC * (st.plane(st.aC + st.h4) - st.oC);
+            const uint32_t hm = st.h4 & ~3u;  // (a depth-0 root is a leaf: 2 bytes, unused)
+            st.tMA = st.iA * (st.plane(st.aA + hm) - st.oA);
+            st.tMB = st.iB * (st.plane(st.aB + hm) - st.oB);
+            st.tMC = st.iC * (st.plane(st.aC + hm) - st.oC);
         }
     } else {
         const int S1 = fast_axis_floats(D);
@@ -1221,6 +1223,8 @@ ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks
         st.tNC = st.iC * (st.plane(st.aC) - st.oC);
         st.tFC = st.iC * (st.plane(st.aC + w4) - st.oC);
         if (Masks::kPreMid) {
+            // h4 is 2 bytes (a misaligned plane offset) only for a level-D node, a leaf; the
+            // kPreMid walk tests its leaves inline (kInlineLeaves), so it never pops one
             st.tMA = st.iA * (st.plane(st.aA + st.h4) - st.oA);
             st.tMB = st.iB * (st.plane(st.aB + st.h4) - st.oB);
             st.tMC = st.iC * (st.plane(st.aC + st.h4) - st.oC);
