@@ -686,6 +686,10 @@ ORT_FN float4 fetch_sphere(const KScene& S, int e) {
 #define ORT_KID_PREFETCH 1
 #endif
 constexpr bool kKidPrefetch = ORT_KID_PREFETCH;
+// The skip folded into the child mask before the node's rank-LUT read (fast_step).
+#ifndef ORT_KID_SKIP_FOLD
+#define ORT_KID_SKIP_FOLD 1
+#endif
 
 // Plane idx of a ray-order table (base[idx]; see fast_begin for the reversed copies).
 ORT_FN float plane_at(const float* base, int idx) { return base[idx]; }
@@ -1119,7 +1123,20 @@ ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks
             const long long rem = (long long)S.n_nodes - (long long)co;
             cnt.v[1] += (unsigned long long)(rem >= 8 ? 8 : (rem > 0 ? rem : 0));
         }
-        const uint32_t rcm = rank_lut[((st.otab & 7u) << 8) | (rec.y & 0xffu)];  // LUT row m
+        // rejected-sphere skip (kid_table.h): one-sphere leaf children holding the sphere this
+        // lane last rejected, at a tmin <= this node's (<= theirs), cannot end the walk; not
+        // in the counting kernels, which count the reference walk's work.  The LUT maps octant
+        // bits to rank bits one for one, so the skipped octants are cleared from the child mask
+        // before its one LUT read (lut[c & ~s] = lut[c] & ~lut[s]), branch-free.
+        uint32_t cm = rec.y & 0xffu;
+        if (ORT_KID_SKIP_FOLD && !COUNT && Masks::kKidSkip && S.kid) {
+            const uint2 kd = kKidPrefetch ? st.kd : fetch_kid(S, st.node);
+            const uint32_t m = (((kd.x & 0xffffffu) == st.kc_id) ? (kd.x >> 24) : 0u) |
+                               (((kd.y & 0xffffffu) == st.kc_id) ? (kd.y >> 24) : 0u);
+            const float ptmin = fmax_tmin(fmax3(st.tNA, st.tNB, st.tNC));
+            cm &= ~(m & (0u - (uint32_t)(st.kc_e <= ptmin)));
+        }
+        const uint32_t rcm = rank_lut[((st.otab & 7u) << 8) | cm];  // LUT row m
         const int h = 1 << (D - 1 - st.depth);  // half the node's width, in plane steps
         float tMA, tMB, tMC;
         if (Masks::kPreMid) {
@@ -1148,11 +1165,8 @@ ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks
         // exit - entry is never NaN and is +0 when equal: its sign bit is "drop".  The drop
         // bits are shifted in rank order (rank 0 ends at bit 7: the reversed layout) -- one
         // v_max3 + v_min3 + v_sub + v_alignbit per child, no compare/select.
-        // rejected-sphere skip (kid_table.h): one-sphere leaf children holding the sphere this
-        // lane last rejected, at a tmin <= this node's (<= theirs), cannot end the walk; not
-        // in the counting kernels, which count the reference walk's work
         uint32_t skip = 0;
-        if (!COUNT && Masks::kKidSkip && S.kid) {
+        if (!ORT_KID_SKIP_FOLD && !COUNT && Masks::kKidSkip && S.kid) {
             const uint2 kd = kKidPrefetch ? st.kd : fetch_kid(S, st.node);
             const uint32_t m = (((kd.x & 0xffffffu) == st.kc_id) ? (kd.x >> 24) : 0u) |
                                (((kd.y & 0xffffffu) == st.kc_id) ? (kd.y >> 24) : 0u);
