@@ -173,7 +173,11 @@ __device__ inline LdsView setup_lds(unsigned char* smem, const ort::KScene& S) {
 // run covers about a fifteenth of a tile row.  Measured (interleaved A/B): 8-tile runs are
 // best at 1920 px (120 tiles per row; 16 is 1.9 % slower), 16-tile runs at 3840 px (+1.2 %
 // over 8).
+#ifndef ORT_XRUN_LOG2
+#define ORT_XRUN_LOG2 -1  // A/B builds: a fixed run length (log2); -1: from the frame width
+#endif
 inline int xcd_run_log2(int tilesX) {
+    if (ORT_XRUN_LOG2 >= 0) return ORT_XRUN_LOG2;
     int lr = 0;
     while (lr < 6 && (2 << lr) * 15 <= tilesX) ++lr;
     return lr;
