@@ -22,6 +22,20 @@ sys.path.insert(0, str(ROOT))
 import numpy as np  # noqa: E402
 
 
+def morton_order(s):
+    """The sphere set with its spheres (ids) in Morton order of their centres (10 bits per axis)."""
+    from octreeraytracer_amd.scene import SphereSet
+    c = s.center_radius[:, :3].astype(np.float64)
+    lo, hi = c.min(0), c.max(0)
+    q = np.clip(((c - lo) / np.maximum(hi - lo, 1e-30) * 1023).astype(np.int64), 0, 1023)
+    code = np.zeros(len(c), np.int64)
+    for b in range(10):
+        for a in range(3):
+            code |= ((q[:, a] >> b) & 1) << (3 * b + a)
+    o = np.argsort(code, kind="stable")
+    return SphereSet(s.center_radius[o].copy(), s.mat_albedo[o].copy(), s.fuzz_ri[o].copy())
+
+
 def worker(spec, config, block, max_depth=0, world=1, yaw_step=0.0):
     import ctypes as C
 
@@ -38,10 +52,15 @@ def worker(spec, config, block, max_depth=0, world=1, yaw_step=0.0):
     L._declare(lib, strict=False)
     L._lib = lib
     r = ort.Renderer(0)
+    spheres = ort.random_spheres(N, 42)
     for o in filter(None, opts.split(",")):
         name, val = o.split("=")
+        if name == "morton":  # scene experiment: sphere ids renumbered in Morton order (other pixels)
+            if int(val):
+                spheres = morton_order(spheres)
+            continue
         getattr(r, "set_" + name)(int(val))
-    r.build_scene(ort.random_spheres(N, 42), D, M)
+    r.build_scene(spheres, D, M)
     p = ort.FrameParams.default_camera(W, H, num_samples=NS, max_depth=MD)
     from octreeraytracer_amd.scene import DEFAULT_YAW
     moving = [ort.FrameParams.default_camera(W, H, num_samples=NS, max_depth=MD, yaw=DEFAULT_YAW + yaw_step * j)
