@@ -742,7 +742,12 @@ struct Masks64 {  // levels 0..7: trees of depth <= 8
     }
 };
 struct Masks96 {  // levels 0..9 (ORT_COMPACT_MAX_DEPTH 10)
-    static constexpr bool kInlineLeaves = false;
+    // a leaf-children node's leaves tested inline (as in the depth <= 8 walk): C5 camera rays
+    // 14.11 -> 14.86 ms (the rejected-sphere skip already drops most of them): off
+#ifndef ORT_INLINE_LEAVES_DEEP
+#define ORT_INLINE_LEAVES_DEEP 0
+#endif
+    static constexpr bool kInlineLeaves = ORT_INLINE_LEAVES_DEEP;
 #ifndef ORT_PRE_MID_DEEP
 #define ORT_PRE_MID_DEEP 0
 #endif
@@ -882,6 +887,7 @@ using FastState = FastStateT<Masks96>;
 // The persistent kernel keeps a lane's state across refills; there three more registers for
 // the near-plane pointers cost occupancy, so it re-derives them from cP.
 struct Masks96Lean : Masks96 {
+    static constexpr bool kInlineLeaves = false;
     static constexpr bool kKeepNear = false;
 #ifndef ORT_PRE_MID_BOUNCE
 #define ORT_PRE_MID_BOUNCE 0
