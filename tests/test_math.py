@@ -123,6 +123,27 @@ def test_kernel_closed_form_orders_match_shader_tables(ort):
                     assert lut[cmask] == bits, (m, cmask)
 
 
+def test_rank_lut_is_a_bit_permutation(ort):
+    """fast_step folds the rejected-sphere skip into the child mask before its one rank-LUT read
+    (render_core.h, ORT_KID_SKIP_FOLD): lut[c & ~s] == lut[c] & ~lut[s] for every child mask c
+    and skip mask s, which holds because each LUT row maps octant bits to rank bits one for one."""
+    import ctypes as C
+
+    import numpy as np
+
+    from octreeraytracer_amd import _lib as L
+    lib = L.lib()
+    c = np.arange(256)[:, None]
+    s = np.arange(256)[None, :]
+    for m in range(8):
+        order = (C.c_int32 * 8)()
+        lut = (C.c_uint8 * 256)()
+        L.check(lib.ort_debug_fast_order(m, order, lut))
+        t = np.frombuffer(bytes(lut), np.uint8).astype(np.int64)
+        assert sorted(int(t[1 << k]) for k in range(8)) == [1 << r for r in range(8)], m  # one rank bit each
+        assert (t[c & ~s] == (t[c] & ~t[s] & 0xFF)).all(), m
+
+
 def test_order_fixture_is_current():
     """tests/golden/traversal_orders.json was generated from the reference shader (checked
     against the file when the reference is present, i.e. in the build container)."""
