@@ -129,8 +129,6 @@ def test_rank_lut_is_a_bit_permutation(ort):
     and skip mask s, which holds because each LUT row maps octant bits to rank bits one for one."""
     import ctypes as C
 
-    import numpy as np
-
     from octreeraytracer_amd import _lib as L
     lib = L.lib()
     c = np.arange(256)[:, None]
