@@ -106,6 +106,10 @@ def parse(argv=None):
                     help="testing only, no GPU: every rank renders its tile with the host build of the kernel's "
                     "per-pixel code and the bands are gathered with gloo (exercises the launcher, partition and "
                     "gather on CPU; never a measurement)")
+    ap.add_argument("--moving-steps", type=int, default=20,
+                    help="also time this many frames with the camera turning --yaw-step degrees per frame (reported "
+                    "as moving_camera, after the main timed region; 0 = skip)")
+    ap.add_argument("--yaw-step", type=float, default=0.5, help="moving_camera: degrees of yaw per frame")
     ap.add_argument("--single-steps", type=int, default=10,
                     help="N > 1 with frames in flight: also time this many frames with one frame in flight "
                     "(reported as single_frame, after the main timed region; 0 = skip)")
@@ -172,23 +176,56 @@ def lib_sha() -> str:
     return hashlib.sha256(p.read_bytes()).hexdigest()[:16] if p.exists() else ""
 
 
-def device_sha() -> str:
-    """SHA-256 (16 hex) of libort.so's .hip_fatbin section: the gfx950 code objects only, so a
-    PMC record stays valid across host-only rebuilds and goes stale with any kernel change."""
+def _elf_sections(b: bytes) -> dict:
+    """{name: bytes} of an ELF64 image (SHT_NOBITS sections empty)."""
     import struct
-    p = ROOT / "octreeraytracer_amd" / "lib" / "libort.so"
-    if not p.exists():
-        return ""
-    b = p.read_bytes()
     shoff = struct.unpack_from("<Q", b, 0x28)[0]
     shentsize, shnum, shstrndx = struct.unpack_from("<HHH", b, 0x3A)
     hdr = [struct.unpack_from("<IIQQQQIIQQ", b, shoff + i * shentsize) for i in range(shnum)]
     names = hdr[shstrndx][4]
+    out = {}
     for h in hdr:
-        name = b[names + h[0]:b.index(b"\0", names + h[0])]
-        if name == b".hip_fatbin":
-            return hashlib.sha256(b[h[4]:h[4] + h[5]]).hexdigest()[:16]
-    return ""
+        name = b[names + h[0]:b.index(b"\0", names + h[0])].decode()
+        out[name] = b"" if h[1] == 8 else b[h[4]:h[4] + h[5]]
+    return out
+
+
+def gfx950_code_objects(b: bytes) -> list:
+    """The gfx950 code objects of a host ELF's .hip_fatbin: one clang offload bundle per HIP
+    translation unit, in link order."""
+    import struct
+    sec = _elf_sections(b).get(".hip_fatbin", b"")
+    out, i = [], 0
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    while (j := sec.find(magic, i)) >= 0:
+        n = struct.unpack_from("<Q", sec, j + len(magic))[0]
+        q = j + len(magic) + 8
+        for _ in range(n):
+            off, size, tl = struct.unpack_from("<QQQ", sec, q)
+            triple = sec[q + 24:q + 24 + tl]
+            q += 24 + tl
+            if triple.endswith(b"gfx950"):
+                out.append(sec[j + off:j + off + size])
+        i = j + len(magic)
+    return out
+
+
+def device_sha(path=None) -> str:
+    """SHA-256 (16 hex) of the device code of libort.so: per gfx950 code object (link order) its
+    .text (the instructions) and .rodata (the kernel descriptors: registers, LDS, scratch).  A
+    PMC record therefore stays valid across host-only rebuilds and rebuilds in another directory
+    (the compilation-unit id, derived from the source path, only reaches the code objects'
+    symbol strings), and goes stale with any kernel change."""
+    p = Path(path) if path else ROOT / "octreeraytracer_amd" / "lib" / "libort.so"
+    if not p.exists():
+        return ""
+    h = hashlib.sha256()
+    cos = gfx950_code_objects(p.read_bytes())
+    for co in cos:
+        sec = _elf_sections(co)
+        for name in (".text", ".rodata"):
+            h.update(name.encode() + len(sec.get(name, b"")).to_bytes(8, "little") + sec.get(name, b""))
+    return h.hexdigest()[:16] if cos else ""
 
 
 def load_pmc(args, tile_rows) -> dict | None:
@@ -334,7 +371,7 @@ def main():
                     fin.record(gstream)  # the frame is assembled (rank 0) / its tile sent
         return frame
 
-    def step(k, ev=None):
+    def step(k, ev=None, params=None):
         slot, j = k % nslot, k % inflight
         st = streams[j]
         drain(nslot - 1)  # the previous use of this slot's tile has been gathered
@@ -343,7 +380,7 @@ def main():
         torch.cuda.set_stream(st)  # frame k's gather (submit) waits on this stream
         if ev is not None:
             ev[0].record(st)
-        rs[j].render(p, tile, out=outs[slot], stream=st.cuda_stream)
+        rs[j].render(params or p, tile, out=outs[slot], stream=st.cuda_stream)
         if ev is not None:
             ev[1].record(st)
             if world == 1:  # no gather: the frame is complete when its render is
@@ -419,6 +456,43 @@ def main():
         ftrace_iso = r.frame_trace_times_ms(n_single)
         trace_ms_in_flight, trace_ms = trace_ms, [m for m, _ in ftrace_iso]
 
+    # moving camera: the cost order and heavy-first lists deal work by the previous frame's walk
+    # steps, which a static camera makes exact; an interactive caller turns the camera
+    # (src/main.cpp:120-163).  The same pipeline, the camera turning yaw_step degrees per frame
+    # from the static pose, so every frame's hints are one frame stale (after the main timed
+    # region, not part of `value`)
+    moving = None
+    if args.moving_steps > 0:
+        from octreeraytracer_amd.scene import DEFAULT_YAW
+        poses = [ort.FrameParams.default_camera(W, H, num_samples=NS, max_depth=MAXD,
+                                                yaw=DEFAULT_YAW + args.yaw_step * (k + 1))
+                 for k in range(args.moving_steps)]
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        for k in range(args.moving_steps):
+            step(args.warmup + args.steps + k, params=poses[k])
+        drain(0)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t_mov = torch.tensor([time.perf_counter() - t2], dtype=torch.float64, device="cuda")
+        if world > 1:
+            dist.all_reduce(t_mov, op=dist.ReduceOp.MAX)
+        # traced rays of those frames: W*H*spp per frame for primary rays, else counted per pose
+        # (the counting kernels, untimed)
+        if NS * MAXD == 1:
+            mov_rays = None
+        else:
+            mov_rays = torch.tensor([sum(r.count_traffic(q, tile)["traversals"] for q in poses)],
+                                    dtype=torch.float64, device="cuda")
+            if world > 1:
+                dist.all_reduce(mov_rays)
+        moving = (float(t_mov.item()), None if mov_rays is None else float(mov_rays.item()))
+
     # algorithmic traffic of this rank's launch (counting variant, untimed); the traced rays
     # of a step = traversals summed over the ranks (W*H*spp for primary-only configs)
     counts = r.count_traffic(p, tile)
@@ -469,6 +543,15 @@ def main():
                 "frame_latency_ms_avg": round(float(np.mean(single[1])), 4),
                 "note": "one frame in flight (render, gather, assembly, then the next); `value` above keeps "
                         "frames_in_flight frames in flight"},
+            "moving_camera": None if moving is None else {
+                "value": round((moving[1] if moving[1] is not None else rays_per_frame * args.moving_steps)
+                               / moving[0] / 1e6, 2),
+                "yaw_step_deg": args.yaw_step, "steps": args.moving_steps,
+                "ms_per_step": round(moving[0] / args.moving_steps * 1e3, 4),
+                "frames_in_flight": inflight,
+                "note": "the camera turns yaw_step_deg per frame (the interactive case): the per-slot walk-cost "
+                        "hints that order work are one frame stale; `value` above is the static camera of the "
+                        "reference's saveStats runs"},
             "trace_kernels_ms_avg": round(float(np.mean(trace_ms)), 4),
             # with frames in flight: trace_kernels_ms_avg and the first-trace figures are taken over
             # the one-frame-in-flight phase (kernels alone on the GPU); this is the main loop's
@@ -511,7 +594,10 @@ def group_bench(args):
     a single-context ort_render of the same scene, bit for bit."""
     W, H, NSPH, DEPTH, MPN, NS, MAXD = CONFIGS[args.config]
     N = args.gpus
-    inflight = args.inflight or default_inflight(args.config, N)
+    # frame slots: the RCCL transport with several slots (their communicators' gathers running
+    # concurrently) has not run between distinct devices yet, so it is opt-in (--inflight);
+    # the copy-transport rehearsal takes the per-config default
+    inflight = args.inflight or (default_inflight(args.config, N) if args.rehearse_one_gpu or N == 1 else 1)
     if inflight > 1:  # as main(): frame slots overlap only on distinct hardware queues
         os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, max(8, 4 * inflight)))
     import torch
@@ -667,8 +753,35 @@ def emulate(args, world, rank):
         dist.destroy_process_group()
 
 
+def sample_rows(height: int, n: int):
+    """A row sample of about n rows spread evenly over the whole frame height, as the oracle's
+    band arguments: (y0, rows, band_height, band_stride) -- tile row j is frame row
+    y0 + (j // band_height) * band_stride + j % band_height.  Up to half the height: single rows
+    every height // n rows.  Beyond: bands of bh rows every bs rows (bs <= 16) with bh / bs
+    closest to n / height, across the whole height (an integer stride would collapse to 1 there
+    and sample the first n rows only)."""
+    n = max(1, min(int(n), height))
+    if 2 * n <= height:
+        stride = height // n
+        return stride // 2, n, 1, stride
+    if n == height:
+        return 0, height, 1, 1
+    best = None
+    for bs in range(2, 17):
+        for bh in range(1, bs):
+            err = abs(bh / bs - n / height)
+            if best is None or err < best[0] - 1e-12:
+                best = (err, bh, bs)
+    _, bh, bs = best
+    rows = bh * (height // bs) + min(bh, height % bs)
+    return 0, rows, bh, bs
+
+
 def cpu_baseline(spheres, tree, p, budget_s, threads=0):
-    """Oracle on the host cores over evenly spaced full rows, sized to ~budget_s of wall time."""
+    """Oracle on the host cores over a row sample spread evenly over the frame (sample_rows),
+    sized to ~budget_s of wall time.  `value` counts traced rays (octree traversals, every
+    bounce, from the oracle's own counters) per second, the unit of the GPU line's `value`;
+    camera rays per second are reported beside it."""
     from oracle import oracle
     ci = cpu_info()
     # the job's CPU share: a cgroup quota (the GPU box grants 16 CPUs of a 256-thread host) caps
@@ -676,31 +789,36 @@ def cpu_baseline(spheres, tree, p, budget_s, threads=0):
     # on a 16-CPU quota ran the oracle 2.3x slower than 16)
     threads = threads or (max(1, int(ci["cgroup_cpu_quota"])) if ci["cgroup_cpu_quota"] else ci["affinity"])
 
-    def run(n):
-        stride = max(1, p.height // n)
+    def run(n, nthreads):
+        y0, rows, bh, bs = sample_rows(p.height, n)
         t0 = time.perf_counter()
-        oracle.render(spheres, tree, p, 0, stride // 2, p.width, n, band_height=1, band_stride=stride, threads=threads)
-        return time.perf_counter() - t0, stride
+        _, c = oracle.render(spheres, tree, p, 0, y0, p.width, rows, band_height=bh, band_stride=bs, counts=True,
+                             threads=nthreads)
+        return time.perf_counter() - t0, rows, (y0, bh, bs), c
+
+    def where(rows, geo):
+        y0, bh, bs = geo
+        last = y0 + ((rows - 1) // bh) * bs + (rows - 1) % bh
+        return (f"{rows} of {p.height} rows (every {bs}th from row {y0})" if bh == 1 else
+                f"{rows} of {p.height} rows ({bh} of every {bs}, rows {y0}..{last})")
 
     n = 2 * threads
-    dt, _ = run(min(n, p.height))  # calibration sample
+    dt, _, _, _ = run(min(n, p.height), threads)  # calibration sample
     n = int(max(min(n, p.height), min(p.height, n * budget_s / max(dt, 1e-3))))
-    dt, stride = run(n)
-    rays = n * p.width * p.num_samples
+    dt, rows, geo, c = run(n, threads)
+    cam = rows * p.width * p.num_samples
     # one core (report all cores and 1 core), a smaller row sample
-    n1 = max(2, min(p.height, int(n * 0.25 * budget_s / max(dt * threads, 1e-3))))
-    stride1 = max(1, p.height // n1)
-    t0 = time.perf_counter()
-    oracle.render(spheres, tree, p, 0, stride1 // 2, p.width, n1, band_height=1, band_stride=stride1, threads=1)
-    dt1 = time.perf_counter() - t0
-    rays1 = n1 * p.width * p.num_samples
-    return {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": f"{n} of {p.height} rows (every {stride}th), {rays} camera rays, {dt:.1f} s wall; "
+    n1 = max(2, min(p.height, int(rows * 0.25 * budget_s / max(dt * threads, 1e-3))))
+    dt1, rows1, geo1, c1 = run(n1, 1)
+    return {"value": round(c["traversals"] / dt / 1e6, 3), "unit": "Mrays/s (traced rays: octree traversals, every bounce)",
+            "cores": threads, "kind": "port",
+            "sample": f"{where(rows, geo)}, {c['traversals']} traversals of {cam} camera rays, {dt:.1f} s wall; "
                       f"oracle/ort_oracle.c -O3, OpenMP dynamic over rows, {threads} threads",
+            "camera_rays_per_s_M": round(cam / dt / 1e6, 3),
             "cpu_model": ci["model"], "nproc": ci["nproc"], "affinity_cpus": ci["affinity"],
             "cgroup_cpu_quota": ci["cgroup_cpu_quota"],
-            "value_1core": round(rays1 / dt1 / 1e6, 3),
-            "sample_1core": f"{n1} rows (every {stride1}th), {rays1} camera rays, {dt1:.1f} s wall, 1 thread"}
+            "value_1core": round(c1["traversals"] / dt1 / 1e6, 3),
+            "sample_1core": f"{where(rows1, geo1)}, {c1['traversals']} traversals, {dt1:.1f} s wall, 1 thread"}
 
 
 if __name__ == "__main__":

@@ -84,10 +84,12 @@ typedef struct ort_scene_info {
 #define ORT_OPT_FORCE_LAYOUT 1     /* -1 auto (default), or ORT_LAYOUT_* */
 #define ORT_OPT_EXACT_TRAVERSAL 2  /* 1: disable the sign-specialised fast walk (A/B testing; same pixels) */
 #define ORT_OPT_REFILL 3           /* persistent trace: refill a wave when >= value of its 64 lanes idle (16) */
-#define ORT_OPT_PERSISTENT 4       /* persistent trace kernel with per-lane ray refill: 0 off, 1 every
-                                      trace, 2 (default) bounce >= 1 traces only: their incoherent
-                                      rays gain from refilling idle lanes (C5 -4.5 %) */
-#define ORT_OPT_PACKET 5           /* 1: wave-level walk for camera rays; 0 (default): per-lane walk (same pixels) */
+#define ORT_OPT_PERSISTENT 4       /* persistent trace kernel with per-lane ray refill: 0 off, 2 (default)
+                                      bounce >= 1 traces only: their incoherent rays gain from
+                                      refilling idle lanes (C5 -4.5 %); 1 (every trace) was removed in
+                                      round 4 (C5 -19 %): ORT_ERR_UNSUPPORTED */
+#define ORT_OPT_PACKET 5           /* removed in round 4 (the wave-level walk was SALU-bound, 1.2-1.35x
+                                      slower): ORT_ERR_UNSUPPORTED */
 #define ORT_OPT_SORT_PATHS 6       /* order of the alive paths between bounces (coherence; same pixels):
                                       2 (default) radix-sort the compacted list by direction octant +
                                       origin cell + direction; the list's length stays on the device
@@ -95,8 +97,8 @@ typedef struct ort_scene_info {
                                       frame of the same shape + 1/64 + 1024, read back asynchronously;
                                       a longer list goes on unsorted): no host wait; 1 sort every
                                       slot's key; 0 slot order */
-#define ORT_OPT_WAVE_QUEUE 7       /* 1: resident workgroups whose waves take 64-slot blocks from a queue;
-                                      0 (default): one workgroup per 16x16 tile (same pixels) */
+#define ORT_OPT_WAVE_QUEUE 7       /* removed in round 4 (the wave-level block queue traced a 1/8 band in
+                                      0.83 vs 0.61 ms): ORT_ERR_UNSUPPORTED */
 #define ORT_OPT_XCD_SWIZZLE 8      /* workgroup -> tile order (same pixels): 2 (default) each XCD renders
                                       runs of consecutive raster tiles (about 1/15 of a tile row, a power
                                       of two: 16 at 3840 px); 1: each XCD renders 128x128-pixel
@@ -266,17 +268,21 @@ int ort_group_build_scene(ort_group* group, const float* sphere_center_radius, c
  * memory (pinned for a fully asynchronous copy), or (out_is_device != 0) device memory on
  * devices[0] -- and return at once with its ticket (0, 1, 2, ...).  Every rank's render is
  * enqueued before any of them runs (no host wait inside); the only wait is for the frame that
- * last used this frame's slot, frames_in_flight frames earlier.  rgb_out must stay untouched
- * until ort_group_wait(ticket) returns. */
+ * last used this frame's slot, frames_in_flight frames earlier.  The bands are received (and
+ * then de-interleaved) on a gather stream of devices[0], each as soon as its rank has rendered
+ * it, while rank 0 may still be rendering.  rgb_out must stay untouched until
+ * ort_group_wait(ticket) returns.  With the RCCL transport, frames_in_flight > 1 runs several
+ * slots' communicators concurrently: not yet measured between distinct devices. */
 int ort_group_submit(ort_group* group, const ort_params* params, float* rgb_out, int32_t out_is_device,
                      int64_t* ticket);
 /* Wait until frame `ticket` is in rgb_out (gathered, assembled and, for host output, copied). */
 int ort_group_wait(ort_group* group, int64_t ticket);
 /* submit + wait for it and every earlier frame: synchronous. */
 int ort_group_render(ort_group* group, const ort_params* params, float* rgb_out, int32_t out_is_device);
-/* Device time, on devices[0], of the last frame ort_group_wait / ort_group_render saw complete:
- * from its submission on devices[0]'s stream to its assembly (renders, gather, de-interleave;
- * HIP events) -- the frame's latency, not its share of a pipelined throughput. */
+/* Device time, on devices[0], of the frame the last ort_group_wait / ort_group_render waited
+ * for: from its submission on devices[0]'s stream to its assembly (renders, gather,
+ * de-interleave; HIP events), taken when that frame completed -- the frame's latency, not its
+ * share of a pipelined throughput. */
 int ort_group_last_frame_ms(ort_group* group, float* ms);
 
 /* ---- host scene-build stage (kept reference API, src/raytracer.cpp + src/octree.cpp) -- */

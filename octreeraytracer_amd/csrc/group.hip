@@ -107,6 +107,11 @@ struct GroupSlot {
     float* frame = nullptr;            // devices[0]: the assembled frame (host output path)
     size_t frame_floats = 0;
     std::vector<hipEvent_t> done;      // per rank: its tile has been copied (copy transport)
+    // devices[0]: the gather's stream -- the receives (RCCL) or the waits for the copies, then
+    // the de-interleave -- so that the bands of ranks 1..N-1 land while rank 0 still renders
+    // (posted behind rank 0's render on stream[0], no band was received before it finished)
+    hipStream_t gstream = nullptr;
+    hipEvent_t rendered0 = nullptr;    // devices[0]: rank 0's band tile is rendered
     hipEvent_t assembled = nullptr;    // devices[0]: the de-interleave has read recv[]
     hipEvent_t finished = nullptr;     // devices[0]: the frame (and its host copy) is complete
     hipEvent_t t0 = nullptr, t1 = nullptr;
@@ -120,8 +125,17 @@ struct ort_group {
     std::vector<int> dev;
     std::vector<GroupSlot> slot;
     long long next_ticket = 0;
-    int last_slot = -1;                // slot of the frame ort_group_wait saw complete last
+    // device time of each completed frame, taken when its slot's completion is first seen
+    // (wait_slot: by ort_group_wait, or by the submit that reuses the slot) -- a later
+    // submission on that slot cannot overwrite it
+    static constexpr int kMsRing = 64;
+    long long ms_ticket[kMsRing];
+    float ms_value[kMsRing];
+    float last_ms = -1.0f;             // of the frame ort_group_wait / ort_group_render saw complete last
     std::string err;
+    ort_group() {
+        for (int i = 0; i < kMsRing; ++i) ms_ticket[i] = -1;
+    }
 };
 
 namespace {
@@ -199,6 +213,13 @@ int wait_slot(ort_group* g, GroupSlot& S) {
     if (S.ticket < 0) return ORT_OK;
     GCHK(g, hipSetDevice(g->dev[0]));
     GCHK(g, hipEventSynchronize(S.finished));
+    const int i = (int)(S.ticket % ort_group::kMsRing);
+    if (g->ms_ticket[i] != S.ticket) {  // first time this frame is seen complete: keep its time
+        float ms = 0.0f;
+        GCHK(g, hipEventElapsedTime(&ms, S.t0, S.t1));
+        g->ms_ticket[i] = S.ticket;
+        g->ms_value[i] = ms;
+    }
     return ORT_OK;
 }
 
@@ -255,6 +276,8 @@ int ort_group_create_pipelined(const int32_t* devices, int32_t n_devices, int32_
         }
         if (hipSetDevice(devices[0]) != hipSuccess || hipEventCreate(&S.t0) != hipSuccess ||
             hipEventCreate(&S.t1) != hipSuccess ||
+            hipStreamCreateWithFlags(&S.gstream, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&S.rendered0, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&S.assembled, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&S.finished, hipEventDisableTiming) != hipSuccess)
             return bail(gfail(g, ORT_ERR_HIP, "ort_group_create: timing events"));
@@ -280,12 +303,17 @@ int ort_group_create(const int32_t* devices, int32_t n_devices, int32_t transpor
 
 int ort_group_destroy(ort_group* g) {
     if (!g) return ORT_OK;
-    for (GroupSlot& S : g->slot)
+    for (GroupSlot& S : g->slot) {
         for (int r = 0; r < g->n; ++r)
             if (S.ctx[r]) {
                 (void)hipSetDevice(g->dev[r]);
                 (void)hipStreamSynchronize(S.stream[r]);
             }
+        if (S.gstream) {
+            (void)hipSetDevice(g->dev[0]);
+            (void)hipStreamSynchronize(S.gstream);
+        }
+    }
     for (GroupSlot& S : g->slot) {
         if (!S.comm.empty()) {
             std::string why;
@@ -302,8 +330,9 @@ int ort_group_destroy(ort_group* g) {
             if (S.ctx[r]) ort_destroy(S.ctx[r]);
         }
         if (!g->dev.empty()) (void)hipSetDevice(g->dev[0]);
-        for (hipEvent_t e : {S.t0, S.t1, S.assembled, S.finished})
+        for (hipEvent_t e : {S.t0, S.t1, S.rendered0, S.assembled, S.finished})
             if (e) (void)hipEventDestroy(e);
+        if (S.gstream) (void)hipStreamDestroy(S.gstream);
     }
     delete g;
     return ORT_OK;
@@ -366,7 +395,11 @@ int ort_group_submit(ort_group* g, const ort_params* p, float* rgb_out, int32_t 
         const ort_tile t = ort::group_tile(W, H, r, N);
         if ((rc = each(g, S.ctx[r], ort_render(S.ctx[r], p, &t, S.tile[r], 1, S.stream[r]), r))) return rc;
     }
-    // 2. the one exchange: bands of ranks 1..N-1 to devices[0]
+    GCHK(g, hipSetDevice(g->dev[0]));
+    GCHK(g, hipEventRecord(S.rendered0, S.stream[0]));
+    // 2. the one exchange: bands of ranks 1..N-1 to devices[0], received on the gather stream
+    //    (each band as soon as its rank is done, also while rank 0 still renders); the slot's
+    //    previous assembly ran on that stream too, so recv[] is free when they land
     if (N > 1) {
         if (g->transport == ORT_GROUP_TRANSPORT_RCCL) {
             std::string why;
@@ -374,7 +407,7 @@ int ort_group_submit(ort_group* g, const ort_params* p, float* rgb_out, int32_t 
             ncclResult_t e = R.groupStart();
             for (int r = 1; r < N && e == ncclSuccess; ++r) {
                 e = R.send(S.tile[r], tile_floats, ncclFloat32, 0, S.comm[r], S.stream[r]);
-                if (e == ncclSuccess) e = R.recv(S.recv[r], tile_floats, ncclFloat32, r, S.comm[0], S.stream[0]);
+                if (e == ncclSuccess) e = R.recv(S.recv[r], tile_floats, ncclFloat32, r, S.comm[0], S.gstream);
             }
             const ncclResult_t e2 = R.groupEnd();
             if (e != ncclSuccess || e2 != ncclSuccess)
@@ -388,24 +421,25 @@ int ort_group_submit(ort_group* g, const ort_params* p, float* rgb_out, int32_t 
                                            S.stream[r]));
                 GCHK(g, hipEventRecord(S.done[r], S.stream[r]));
                 GCHK(g, hipSetDevice(g->dev[0]));
-                GCHK(g, hipStreamWaitEvent(S.stream[0], S.done[r], 0));
+                GCHK(g, hipStreamWaitEvent(S.gstream, S.done[r], 0));
             }
         }
     }
-    // 3. de-interleave on devices[0]
+    // 3. de-interleave on devices[0], once rank 0's own tile is rendered too
     GCHK(g, hipSetDevice(g->dev[0]));
+    GCHK(g, hipStreamWaitEvent(S.gstream, S.rendered0, 0));
     SrcTable src{};
     src.tile[0] = S.tile[0];
     for (int r = 1; r < N; ++r) src.tile[r] = S.recv[r];
     float* dst = out_is_device ? rgb_out : S.frame;
-    hipLaunchKernelGGL(k_assemble, dim3((unsigned)H), dim3(256), 0, S.stream[0], src, N, W, H, dst);
+    hipLaunchKernelGGL(k_assemble, dim3((unsigned)H), dim3(256), 0, S.gstream, src, N, W, H, dst);
     GCHK(g, hipGetLastError());
-    GCHK(g, hipEventRecord(S.assembled, S.stream[0]));
+    GCHK(g, hipEventRecord(S.assembled, S.gstream));
     S.assembled_once = true;
-    GCHK(g, hipEventRecord(S.t1, S.stream[0]));
+    GCHK(g, hipEventRecord(S.t1, S.gstream));
     if (!out_is_device)  // pageable rgb_out: the runtime may stage this copy synchronously
-        GCHK(g, hipMemcpyAsync(rgb_out, S.frame, frame_floats * sizeof(float), hipMemcpyDeviceToHost, S.stream[0]));
-    GCHK(g, hipEventRecord(S.finished, S.stream[0]));
+        GCHK(g, hipMemcpyAsync(rgb_out, S.frame, frame_floats * sizeof(float), hipMemcpyDeviceToHost, S.gstream));
+    GCHK(g, hipEventRecord(S.finished, S.gstream));
     S.ticket = tk;
     g->next_ticket = tk + 1;
     if (ticket) *ticket = tk;
@@ -417,10 +451,12 @@ int ort_group_wait(ort_group* g, int64_t ticket) {
     if (ticket < 0 || ticket >= g->next_ticket) return gfail(g, ORT_ERR_INVALID_ARG, "ort_group_wait: no such frame");
     const int si = (int)(ticket % (long long)g->slot.size());
     GroupSlot& S = g->slot[(size_t)si];
-    if (S.ticket != ticket) return ORT_OK;  // the slot took a later frame, so this one completed
-    int rc;
-    if ((rc = wait_slot(g, S))) return rc;
-    g->last_slot = si;
+    if (S.ticket == ticket) {  // else the slot took a later frame, so this one has completed
+        const int rc = wait_slot(g, S);
+        if (rc) return rc;
+    }
+    const int i = (int)(ticket % ort_group::kMsRing);
+    if (g->ms_ticket[i] == ticket) g->last_ms = g->ms_value[i];
     return ORT_OK;
 }
 
@@ -436,11 +472,8 @@ int ort_group_render(ort_group* g, const ort_params* p, float* rgb_out, int32_t 
 
 int ort_group_last_frame_ms(ort_group* g, float* ms) {
     if (!g || !ms) return gfail(g, ORT_ERR_INVALID_ARG, "ort_group_last_frame_ms: null argument");
-    if (g->last_slot < 0) return gfail(g, ORT_ERR_NO_SCENE, "no frame completed yet (ort_group_wait)");
-    GroupSlot& S = g->slot[(size_t)g->last_slot];
-    GCHK(g, hipSetDevice(g->dev[0]));
-    GCHK(g, hipEventSynchronize(S.t1));
-    GCHK(g, hipEventElapsedTime(ms, S.t0, S.t1));
+    if (g->last_ms < 0.0f) return gfail(g, ORT_ERR_NO_SCENE, "no frame completed yet (ort_group_wait)");
+    *ms = g->last_ms;  // taken when that frame completed (wait_slot): later submissions do not move it
     return ORT_OK;
 }
 

@@ -33,8 +33,6 @@ int ort_debug_group_emulate(const float* sphere_center_radius, const float* sphe
 // rows (rank_lut_entry) for every child mask: lut256[cmask] (checked against the shader's
 // tables, tests/golden/traversal_orders.json).
 int ort_debug_fast_order(int32_t m, int32_t* order8, uint8_t* lut256);
-// ANALYSIS-ONLY: deferred bounce rays per trace launch (ort_kernel.hip ort_debug_defer_probe).
-int ort_debug_defer_probe(ort_ctx* ctx, void* dev, int32_t cap);
 // TEST-ONLY: per ray (origin.xyz, direction.xyz in rays[6 i]) the fast walk where the kernels
 // would take it (fast_prepare) and the exact walk (traverse_compact, literal GLSL min/max);
 // out[5 i] = {fast taken, fast entry, fast t bits, exact entry, exact t bits}.  bounce != 0:

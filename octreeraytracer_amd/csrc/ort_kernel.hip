@@ -8,6 +8,7 @@
 //                       record; one path per lane, a wave = 8x8 pixels, a workgroup = 16x16.
 //                       Only the sign-specialised fast walk is compiled in, so it runs at
 //                       8 waves/SIMD; rays it cannot take are appended to a defer list.
+//   ort_trace_persistent  bounces >= 1: the sorted alive-path list, lanes refilled from a queue.
 //   ort_trace_exact     the exact walk for the (rare) deferred rays, persistent grid.
 //   ort_shade_kernel    BSDF / sky, path state or (1 spp, 1 bounce) the final pixel.
 //   ort_finalize_kernel average + gamma for the multi-sample / multi-bounce case.
@@ -53,9 +54,7 @@ struct PipeArgs {
     int nobounce;     // maxDepth <= 0: radiance() returns (1,1,1) without tracing
     int exact_only;   // ORT_OPT_EXACT_TRAVERSAL: every compact ray takes the exact walk
     int refill;       // persistent trace: refill a wave when at least this many lanes idle
-    int rays_stored;  // bounce-0 rays were written by ort_raygen_kernel (persistent pipeline)
     int final_out;    // a path that ends in the last sample writes its final pixel (no finalize pass)
-    const uint8_t* lut;  // global copy of the rank LUT (ort::rank_lut_entry), 8 x 256 bytes
     const int* qlist;    // bounce >= 1: the alive path slots (compacted, increasing), or null = all
     const int* qcount;   // their number (device)
     int* qnext;          // shade kernels: append the paths that go on here (next bounce's list), or null
@@ -77,7 +76,7 @@ struct PipeArgs {
     uint16_t* bcost_w;        // ORT_OPT_HEAVY_FIRST: the persistent bounce trace records each walk's steps here
     const uint16_t* bcost_r;  // ... the kernels appending the next bounce's list read that bounce's last-frame steps
     int heavy;                // ... walks of at least this many steps are heavy: they sort first
-    ulonglong4* wclock;  // analysis only (ort_debug_wave_clock): per queue block {t0, t1, hw ids, 0}
+    ulonglong4* wclock;  // analysis builds only (ORT_PERSIST_CLOCK, ort_debug_wave_clock): per wave a timeline record
     int wclock_n;
 };
 
@@ -243,30 +242,6 @@ __device__ inline ort::Ray load_ray(const PipeArgs& A, int k, bool& alive) {
     r.d = ort::mk(d.x, d.y, d.z);
     alive = d.w != 0.0f;
     return r;
-}
-
-// Sample-s camera rays (main() up to radiance()'s first line): path state for bounce 0.
-__global__ void __launch_bounds__(kBlock) ort_raygen_kernel(PipeArgs A) {
-    const int k = blockIdx.x * kBlock + threadIdx.x;
-    int col, row;
-    const bool in = slot_coords<true>(A, k, col, row);
-    const int y = in ? tile_row_to_y(A.tm, row) : 0;
-    if (!in || y >= A.pp.H) {
-        A.pd[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // hole
-        return;
-    }
-    ort_rng st;
-    if (A.sample == 0) {
-        ort::pixel_rng_init(A.pp, A.tm.x0 + col, y, st);
-    } else {
-        const float2 v = A.prng[k];
-        st.x = v.x;
-        st.y = v.y;
-    }
-    const ort::Ray ray = ort::primary_ray(A.pp, A.tm.x0 + col, y, A.sample, st);
-    A.po[k] = make_float4(ray.o.x, ray.o.y, ray.o.z, 1.0f);
-    A.pd[k] = make_float4(ray.d.x, ray.d.y, ray.d.z, 1.0f);
-    A.prng[k] = make_float2(st.x, st.y);
 }
 
 // Persistent trace over the compact layout: every lane keeps one ray's FastState; the
@@ -570,7 +545,10 @@ __device__ inline void append_slots(bool go, int k, uint32_t key, int* list, uin
 #ifndef ORT_HEAVY_RATIO_LOG2
 #define ORT_HEAVY_RATIO_LOG2 1  // class thresholds T, 2T, 4T
 #endif
+static_assert(ORT_HEAVY_LEVELS >= 1 && ORT_HEAVY_LEVELS <= 7, "ORT_HEAVY_LEVELS: 1..7 classes above the lightest");
 constexpr int kHeavyKeyBits = ORT_HEAVY_LEVELS > 3 ? 3 : (ORT_HEAVY_LEVELS > 1 ? 2 : 1);
+// the class sits above the path key's bits in a 32-bit radix key (sortListBounded's end bit)
+static_assert(ort::kPathKeyBits + kHeavyKeyBits <= 32, "heavy-first class bits + path key bits exceed 32");
 __device__ __forceinline__ uint32_t light_bit(const uint16_t* bcost_r, int heavy, int k) {
     if (!bcost_r) return 0u;
     const int c = bcost_r[k];
@@ -723,6 +701,7 @@ __device__ __forceinline__ void trace_compact_body(PipeArgs& A, unsigned char* s
     ort::Counters cnt;
     for (int q = 0; q < 6; ++q) cnt.v[q] = 0;
     const bool go = trace_slot<COUNT, PRIMARY, DEEP, FUSE>(A, L, k, cnt);
+    (void)go;
     if constexpr (FUSE == 2) {  // the paths that go on join the next bounce's list
 #if defined(__HIP_DEVICE_COMPILE__)
         typedef __attribute__((address_space(4))) const PipeArgs KernArgs;
@@ -732,47 +711,6 @@ __device__ __forceinline__ void trace_compact_body(PipeArgs& A, unsigned char* s
             key = ort::path_key(kp->po[k], kp->pd[k], kp->mp, kp->key_spread) | light_bit(kp->bcost_r, kp->heavy, k);
         append_slots(go, k, key, kp->qnext, kp->qnext_keys, kp->qnext_count);
 #endif
-    }
-    flush_counts<COUNT>(cnt, A.counters);
-}
-
-// Wave queue (ORT_OPT_WAVE_QUEUE): resident workgroups whose waves each take the next 64-slot
-// block (an 8x8 pixel block, or 64 entries of a bounce list) with one atomic, as soon as
-// their previous block is done -- no workgroup-level wait and one LDS setup per resident
-// group.  Balances the tail when a GPU has few blocks (a 1/8 band tile of an 8-GPU frame).
-template <bool COUNT, bool PRIMARY, bool DEEP, int FUSE>
-__device__ __forceinline__ void trace_queue_body(PipeArgs& A, unsigned char* smem) {
-    (void)setup_lds<true>(smem, A.S);
-    const int lane = threadIdx.x & 63;
-    const int items = (!PRIMARY && A.qlist) ? *A.qcount : A.total;
-    const int nblk = (items + 63) >> 6;
-    int* cursor = A.sync + 1;
-    ort::Counters cnt;
-    for (int q = 0; q < 6; ++q) cnt.v[q] = 0;
-    for (;;) {
-        int w = 0;
-        if (lane == 0) w = atomicAdd(cursor, 1);
-        w = __shfl(w, 0);
-        if (w >= nblk) break;
-        int k = w * 64 + lane;
-        // kernel arguments re-read per block through a laundered pointer: hoisted out of the
-        // loop they would stay live across the walk and spill
-#if defined(__HIP_DEVICE_COMPILE__)
-        typedef __attribute__((address_space(4))) const PipeArgs KernArgs;
-        KernArgs* kp = (KernArgs*)__builtin_amdgcn_kernarg_segment_ptr();
-        asm volatile("" : "+s"(kp));
-        PipeArgs A1 = *kp;
-#else
-        PipeArgs& A1 = A;
-#endif
-        LdsView L = lds_view<true>(smem, A1.S.depth);
-        const unsigned long long t0 = A1.wclock ? __builtin_amdgcn_s_memrealtime() : 0;
-        if (PRIMARY || list_slot(A1, k)) trace_slot<COUNT, PRIMARY, DEEP, FUSE>(A1, L, k, cnt);
-        if (A1.wclock && lane == 0 && w < A1.wclock_n) {
-            const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);     // HW_ID: wave, simd, cu, se
-            const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);   // XCC_ID
-            A1.wclock[w] = make_ulonglong4(t0, __builtin_amdgcn_s_memrealtime(), hw, xcc);
-        }
     }
     flush_counts<COUNT>(cnt, A.counters);
 }
@@ -789,221 +727,6 @@ ort_trace_compact_deep(PipeArgs A) {
     extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];  // plane tables: 1 KiB-aligned
     trace_compact_body<COUNT, PRIMARY, true, FUSE>(A, smem);
 }
-template <bool COUNT, bool PRIMARY, bool FUSE>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ORT_TRACE_WAVES))) ort_trace_compact_q(PipeArgs A) {
-    extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];  // plane tables: 1 KiB-aligned
-    trace_queue_body<COUNT, PRIMARY, false, FUSE>(A, smem);
-}
-template <bool COUNT, bool PRIMARY, bool FUSE>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ORT_TRACE_WAVES_DEEP)))
-ort_trace_compact_deep_q(PipeArgs A) {
-    extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];  // plane tables: 1 KiB-aligned
-    trace_queue_body<COUNT, PRIMARY, true, FUSE>(A, smem);
-}
-
-// Wave-wide OR of v (every lane of the wave must be executing): DPP prefix-OR inside each
-// row of 16 lanes, then the row broadcasts; lane 63 ends up with the OR of all 64.
-__device__ inline uint32_t wave_or(uint32_t v) {
-    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);   // row_shr:1
-    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);   // row_shr:2
-    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);   // row_shr:4
-    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true);   // row_shr:8
-    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
-    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
-    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
-}
-
-// Camera rays, wave-level ("packet") walk of the compact layout.
-//
-// A wave is an 8x8 pixel block; when all its fast-path rays share the sign vector (hence the
-// traversal order), the wave walks the tree ONCE, in that order, visiting the union of the
-// nodes its rays visit.  Each lane keeps its own rank-reversed level masks (the children ITS
-// walk pushed) and is active at a node iff that node is in its own set, so every lane sees
-// exactly its own node sequence (a DFS in a fixed child order, restricted to an
-// ancestor-closed subset, is that subset's DFS) and stops after its first hitting leaf, as
-// the per-lane walk does.  What moves to the scalar side: the node record, split planes and
-// leaf spheres are wave-uniform loads (s_load), the union masks and the cell/level
-// bookkeeping live in SGPRs, and the per-level children offsets in one VGPR indexed by level
-// (v_writelane/v_readlane).  The per-lane work per visit is the slab math of the active
-// lanes only.  Waves whose rays do not share one order take the per-lane walk.
-//
-// tools/wave_stats.py prices it: at C3 the union visits 1.41x the internal nodes of one ray,
-// while the per-lane loop ran a ~46-VALU pop for every lane every iteration.
-template <bool COUNT, bool DEEP>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ORT_TRACE_WAVES))) ort_trace_packet(PipeArgs A) {
-    extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];  // plane tables: 1 KiB-aligned
-    using Masks = typename std::conditional<DEEP, ort::Masks96, ort::Masks64>::type;
-    const ort::KScene& S = A.S;
-    // planes and rank LUT in LDS: wave-uniform reads are LDS broadcasts addressed by one VALU
-    // op, instead of scalar loads whose 64-bit address arithmetic saturated the scalar unit
-    LdsView LV = setup_lds<true>(smem, A.S);
-    const int k = blockIdx.x * kBlock + threadIdx.x;
-    bool alive;
-    const ort::Ray ray = slot_ray<true>(A, k, alive);
-    const ort::V3 inv = ort::mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
-    const bool fast = alive && !A.exact_only && ort::fast_path_ok(ray, inv, 0.001f, ORT_MAXFLOAT);
-    ort::Counters cnt;
-    for (int q = 0; q < 6; ++q) cnt.v[q] = 0;
-    if (COUNT && fast) cnt.v[5] += 1;
-    const uint32_t mL = ((uint32_t)(ray.d.z < 0.0f) << 2) | ((uint32_t)(ray.d.x < 0.0f) << 1) | (uint32_t)(ray.d.y < 0.0f);
-    const uint64_t fastMask = __ballot(fast);
-    int entry = -1;
-    float tHit = 0.0f;
-    bool hit = false;
-    if (fastMask) {
-        const int lead = __builtin_ctzll(fastMask);
-        const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)mL, lead);
-        if (__ballot(fast && mL != m) == 0) {
-            // ---- packet walk: every lane of the wave executes this block ----
-            const int D = S.depth;
-            const int top = 1 << D;
-            const bool swap = (m >> 1) & 1u;
-            const uint32_t gA = swap ? (m & 1u) : ((m >> 1) & 1u), gB = swap ? ((m >> 1) & 1u) : (m & 1u),
-                           gC = (m >> 2) & 1u;
-            const int S1 = ort::fast_axis_floats(D);  // forward tables at a * S1 (fill_fast_planes)
-            const float* pA = LV.planes + (swap ? S1 : 0) + (gA ? top : 0);
-            const float* pB = LV.planes + (swap ? 0 : S1) + (gB ? top : 0);
-            const float* pC = LV.planes + 2 * S1 + (gC ? top : 0);
-            const int sA = gA ? -1 : 1, sB = gB ? -1 : 1, sC = gC ? -1 : 1;
-            uint32_t otab = 0;
-            for (uint32_t r = 0; r < 8; ++r) otab |= ort::rank_perm(r, m) << (4 * r);
-            const uint8_t* lutRow = LV.lut + m * 256u;
-            const float oA = swap ? ray.o.y : ray.o.x, oB = swap ? ray.o.x : ray.o.y, oC = ray.o.z;
-            const float iA = swap ? inv.y : inv.x, iB = swap ? inv.x : inv.y, iC = inv.z;
-            const float a = ort::dot(ray.d, ray.d);
-            const float ya = 1.0f / a;
-            const float tmin0 = 0.001f, tmax0 = ORT_MAXFLOAT;
-            float closest = tmax0;
-            // root (glsl:296-311): lanes whose ray hits the root box start active
-            bool active;
-            {
-                const float tNA = iA * (pA[0] - oA), tFA = iA * (pA[sA * top] - oA);
-                const float tNB = iB * (pB[0] - oB), tFB = iB * (pB[sB * top] - oB);
-                const float tNC = iC * (pC[0] - oC), tFC = iC * (pC[sC * top] - oC);
-                active = fast && ort::fmin3(tFA, tFB, tFC) >= ort::fmax3(tNA, tNB, tNC);
-            }
-            Masks lm;     // this lane's pending children (rank-reversed level bytes)
-            lm.clear();
-            Masks um;     // wave union of lm (uniform)
-            um.clear();
-            int coLanes = 0;  // lane L holds the children offset of the walk's level-L ancestor
-            const int laneId = (int)(threadIdx.x & 63u);
-            int node = 0, depth = 0, cA = 0, cB = 0, cC = 0, w = top;  // uniform
-            bool more = __ballot(active) != 0;
-            while (more) {
-                // (readfirstlane: keeps the compiler's uniformity analysis from losing these)
-                node = __builtin_amdgcn_readfirstlane(node);
-                depth = __builtin_amdgcn_readfirstlane(depth);
-                cA = __builtin_amdgcn_readfirstlane(cA);
-                cB = __builtin_amdgcn_readfirstlane(cB);
-                cC = __builtin_amdgcn_readfirstlane(cC);
-                w = __builtin_amdgcn_readfirstlane(w);
-                um.uniform();
-                const uint2 rec = S.node[node];  // uniform: s_load
-                const float pnA = pA[sA * cA], pfA = pA[sA * (cA + w)];
-                const float pnB = pB[sB * cB], pfB = pB[sB * (cB + w)];
-                const float pnC = pC[sC * cC], pfC = pC[sC * (cC + w)];
-                // the wave-uniform node-type branch must not share its join with a divergent
-                // branch (or the compiler treats everything merged there as divergent)
-                const bool internal = (rec.y & ORT_INTERNAL_FLAG) != 0;
-                if (internal) {
-                    const int co = (int)rec.x;
-                    const int h = w >> 1;
-                    const float pmA = pA[sA * (cA + h)], pmB = pB[sB * (cB + h)], pmC = pC[sC * (cC + h)];
-                    const uint32_t rcm = lutRow[rec.y & 0xffu];
-                    uint32_t rm = 0;
-                    if (active) {
-                        if (COUNT) {
-                            cnt.v[0] += 1;
-                            const long long rem = (long long)S.n_nodes - (long long)co;
-                            cnt.v[1] += (unsigned long long)(rem >= 8 ? 8 : (rem > 0 ? rem : 0));
-                        }
-                        const float tNA = iA * (pnA - oA), tFA = iA * (pfA - oA), tMA = iA * (pmA - oA);
-                        const float tNB = iB * (pnB - oB), tFB = iB * (pfB - oB), tMB = iB * (pmB - oB);
-                        const float tNC = iC * (pnC - oC), tFC = iC * (pfC - oC), tMC = iC * (pmC - oC);
-                        const float e00 = ort::fmax2(tNA, tNB), e01 = ort::fmax2(tNA, tMB);
-                        const float e10 = ort::fmax2(tMA, tNB), e11 = ort::fmax2(tMA, tMB);
-                        const float x00 = ort::fmin2(tMA, tMB), x01 = ort::fmin2(tMA, tFB);
-                        const float x10 = ort::fmin2(tFA, tMB), x11 = ort::fmin2(tFA, tFB);
-                        const float nN = ort::fmax2(tNC, tmin0), nF = ort::fmax2(tMC, tmin0);
-                        const float cN = ort::fmin2(tMC, tmax0), cF = ort::fmin2(tFC, tmax0);
-                        uint32_t drop = 0;
-#define ORT_CHILD(EAB, XAB, EC, XC) drop = (drop << 1) | (ort::f2u(ort::fmin2(XAB, XC) - ort::fmax2(EAB, EC)) >> 31);
-                        ORT_CHILD(e00, x00, nN, cN)
-                        ORT_CHILD(e01, x01, nN, cN)
-                        ORT_CHILD(e10, x10, nN, cN)
-                        ORT_CHILD(e11, x11, nN, cN)
-                        ORT_CHILD(e00, x00, nF, cF)
-                        ORT_CHILD(e01, x01, nF, cF)
-                        ORT_CHILD(e10, x10, nF, cF)
-                        ORT_CHILD(e11, x11, nF, cF)
-#undef ORT_CHILD
-                        rm = rcm & ~drop;
-                        lm.put(depth, rm);
-                    }
-                    um.put(depth, wave_or(rm));
-                    coLanes = (laneId == depth) ? co : coLanes;  // v_writelane without the builtin
-                }
-                if (!internal && active) {
-                    if (COUNT) cnt.v[0] += 1;
-                    const int off = (int)rec.x;
-                    const int n = (int)rec.y;
-                    const float tNA = iA * (pnA - oA), tNB = iB * (pnB - oB), tNC = iC * (pnC - oC);
-                    const float ntmin = depth == 0 ? tmin0 : ort::fmax2(ort::fmax3(tNA, tNB, tNC), tmin0);
-                    for (int i = 0; i < n; ++i) {
-                        const float4 sp = S.leaf_sph[off + i];  // uniform: s_load
-                        if (COUNT) cnt.v[2] += 1;
-                        float t;
-                        if (ort::sphere_hit_fast(ray, a, ya, sp, ntmin, closest, t)) {
-                            hit = true;
-                            closest = t;
-                            entry = off + i;
-                            if (COUNT) cnt.v[3] += 1;
-                        }
-                    }
-                    if (hit) lm.clear();  // glsl:336: this lane's walk ends after this leaf
-                }
-                // next node: deepest level, lowest rank that some lane still wants
-                int hb = -1;
-                active = false;
-                um.uniform();
-                while (!um.empty()) {
-                    const int c = um.pop();
-                    active = lm.take(c);
-                    if (__ballot(active)) {
-                        hb = c;
-                        break;
-                    }
-                }
-                more = hb >= 0;
-                if (more) {
-                    const int L = hb >> 3;
-                    const uint32_t rk = (uint32_t)(~hb) & 7u;
-                    const int wc = 1 << (D - 1 - L);
-                    const int keep = -2 * wc;
-                    cA = (cA & keep) | (((rk >> 1) & 1u) ? wc : 0);
-                    cB = (cB & keep) | ((rk & 1u) ? wc : 0);
-                    cC = (cC & keep) | (((rk >> 2) & 1u) ? wc : 0);
-                    w = wc;
-                    depth = L + 1;
-                    node = __builtin_amdgcn_readlane(coLanes, L) + (int)((otab >> (4 * rk)) & 15u);
-                }
-            }
-            tHit = hit ? closest : 0.0f;
-        } else if (fast) {
-            // ---- mixed orders: per-lane walk ----
-            hit = ort::traverse_fast_t<COUNT, Masks>(S, LV.planes, LV.lut, ray, inv, 0.001f, ORT_MAXFLOAT, entry, tHit,
-                                                     LV.fr, cnt);
-        }
-    }
-    if (alive && !fast) {
-        A.defer_list[atomicAdd(A.sync, 1)] = k;
-    } else if (alive) {
-        A.hit[k] = make_int2(hit ? entry : -1, __float_as_int(tHit));
-    }
-    flush_counts<COUNT>(cnt, A.counters);
-}
-
 // One-ray-per-lane trace for the explicit layout (MODE 1) and brute force (MODE 2).
 template <int MODE, bool COUNT, bool PRIMARY>
 __global__ void __launch_bounds__(kBlock) ort_trace_kernel(PipeArgs A) {
@@ -1084,7 +807,7 @@ __device__ __forceinline__ bool shade_slot(const PipeArgs& A, int k) {
     bool alive = true;
     ort::Ray ray;
     ort_rng st;
-    if (FIRST && !A.rays_stored) {
+    if (FIRST) {
         if (A.sample == 0) {
             ort::pixel_rng_init(A.pp, A.tm.x0 + col, y, st);
         } else {
@@ -1171,15 +894,11 @@ struct ort_ctx {
     int force_layout = -1;
     int exact_only = 0;
     int refill = 16;  // ORT_OPT_REFILL: C5 (64-item chunks) 16 > 12 (-0.6 %) > 8 (-1.2 %); tools/ab_stream.py
-    int persistent = 2;  // ORT_OPT_PERSISTENT: 0 off, 1 every trace, 2 bounce >= 1 traces (default)
-    void* wclock = nullptr;  // ort_debug_wave_clock
-    float4* dprobe = nullptr;  // ort_debug_defer_probe: per trace launch, the deferred rays
-    int dprobe_cap = 0;
+    int persistent = 2;  // ORT_OPT_PERSISTENT: 0 off, 2 bounce >= 1 traces (default)
+    void* wclock = nullptr;  // ort_debug_wave_clock (ORT_PERSIST_CLOCK analysis builds)
     long long wclock_n = 0;
     int xcd_swizzle = 2;  // ORT_OPT_XCD_SWIZZLE: workgroup -> tile order (block_tile)
     int kid_skip = 1;     // ORT_OPT_KID_SKIP: rejected-sphere skip of one-sphere leaf children (2: without nk)
-    int wave_queue = 0;  // ORT_OPT_WAVE_QUEUE: per-lane walk from a wave-level block queue (opt-in)
-    int packet = 0;     // ORT_OPT_PACKET: wave-level walk for camera rays (SALU-bound so far: off)
     // ORT_OPT_SORT_PATHS: order of the alive paths between bounces.  2 (default): the list the
     // shade kernel appended, radix-sorted by the coherence key after reading its length back --
     // C5 bounce traces 33.8 -> 31.2 ms, frame 55.5 -> 54.9 ms (A/B).  1 (every slot's key sorted,
@@ -1190,9 +909,16 @@ struct ort_ctx {
     // The list sort without a host wait (sortListBounded): its size is a host-side bound, the
     // list's length from the same bounce of an earlier frame (read back asynchronously into
     // pinned memory: alive_host[sample * bounces + bounce]) plus a margin; a longer list goes
-    // on unsorted (same pixels).  hint_sig: the frame shape the hints belong to.
+    // on unsorted (same pixels).  hint_sig: the frame shape the hints belong to.  The hints live
+    // in one of kHintBanks banks: a new shape takes a bank that no copy is still headed for (the
+    // event after the bank's last copy has completed), so a copy of the old shape's frames
+    // still in flight cannot land in the new shape's hints.
     static constexpr int kHints = 64;
-    int* alive_host = nullptr;
+    static constexpr int kHintBanks = 4;
+    int* alive_host = nullptr;         // kHintBanks x kHints
+    int hint_bank = 0;
+    hipEvent_t hint_ev[kHintBanks] = {};
+    bool hint_ev_used[kHintBanks] = {};
     unsigned long long hint_sig = 0;
     int sort_bound = 0;  // ORT_OPT_SORT_BOUND (testing): > 0 forces this bound
     // ORT_OPT_COST_ORDER (cost_order_slot): per slot the walk steps of its last camera ray,
@@ -1207,7 +933,6 @@ struct ort_ctx {
     DevBuf bcost;
     unsigned long long bcost_sig = 0;
     float root_lo[3] = {0, 0, 0}, root_hi[3] = {0, 0, 0};  // root box (coherence-sort key)
-    DevBuf lut;         // rank LUT (global copy, for the packet kernel)
     ort::GpuTree tree;  // reference-layout tree of the last ort_build_scene(keep_tree)
     float build_ms = 0.0f;
     bool has_scene = false;
@@ -1286,19 +1011,6 @@ int build_lds_image(ort_ctx* ctx) {
         HIPCHK(ctx, hipGetLastError());
     }
     return ORT_OK;
-}
-
-// ANALYSIS-ONLY (ort_debug_defer_probe): record {count, 0, 0, 0} and the first cap deferred
-// rays {origin, direction} of one trace launch (bounce >= 1: the rays are the path state)
-__global__ void k_defer_dump(const int* list, const int* count, const float4* po, const float4* pd, float4* out,
-                             int cap) {
-    const int n = *count;
-    if (threadIdx.x == 0) out[0] = make_float4(__int_as_float(n), 0.0f, 0.0f, 0.0f);
-    for (int i = threadIdx.x; i < n && i < cap; i += blockDim.x) {
-        const int k = list[i];
-        out[1 + 2 * i] = po[k];
-        out[2 + 2 * i] = pd[k];
-    }
 }
 
 __global__ void __launch_bounds__(kBlock) k_interleave_nk(const uint2* node, const uint2* kid, uint4* nk, int64_t n) {
@@ -1559,27 +1271,12 @@ int ensure(ort_ctx* ctx, DevBuf& b, size_t bytes) {
 }
 
 template <bool COUNT, bool PRIMARY>
-hipError_t launch_trace_p(int mode, const PipeArgs& a, int blocks, int pblocks, size_t lds, hipStream_t s, bool packet,
-                          int fuse, int qblocks) {
+hipError_t launch_trace_p(int mode, const PipeArgs& a, int blocks, int pblocks, size_t lds, hipStream_t s, int fuse) {
     if (mode == 0 && pblocks > 0) {
         if (a.S.depth > 8)
             hipLaunchKernelGGL((ort_trace_persistent<COUNT, true>), dim3(pblocks), dim3(kPersistDeepBlock),
                                lds_bytes(0, a.S.depth, false, kRevBounce, kPersistDeepBlock), s, a);
         else hipLaunchKernelGGL((ort_trace_persistent<COUNT, false>), dim3(pblocks), dim3(kBlock), lds, s, a);
-    }
-    else if (mode == 0 && qblocks > 0 && !(PRIMARY && packet)) {
-        const dim3 g(qblocks), t(kBlock);
-        if (a.S.depth > 8) {
-            if (fuse == 1) hipLaunchKernelGGL((ort_trace_compact_deep_q<COUNT, PRIMARY, true>), g, t, lds, s, a);
-            else hipLaunchKernelGGL((ort_trace_compact_deep_q<COUNT, PRIMARY, false>), g, t, lds, s, a);
-        } else {
-            if (fuse == 1) hipLaunchKernelGGL((ort_trace_compact_q<COUNT, PRIMARY, true>), g, t, lds, s, a);
-            else hipLaunchKernelGGL((ort_trace_compact_q<COUNT, PRIMARY, false>), g, t, lds, s, a);
-        }
-    }
-    else if (mode == 0 && PRIMARY && packet) {
-        if (a.S.depth > 8) hipLaunchKernelGGL((ort_trace_packet<COUNT, true>), dim3(blocks), dim3(kBlock), lds, s, a);
-        else hipLaunchKernelGGL((ort_trace_packet<COUNT, false>), dim3(blocks), dim3(kBlock), lds, s, a);
     }
     else if (mode == 0 && a.S.depth > 8)
     {
@@ -1599,9 +1296,9 @@ hipError_t launch_trace_p(int mode, const PipeArgs& a, int blocks, int pblocks, 
 
 template <bool COUNT>
 hipError_t launch_trace(int mode, bool primary, const PipeArgs& a, int blocks, int pblocks, size_t lds, hipStream_t s,
-                        bool packet, int fuse, int qblocks) {
-    return primary ? launch_trace_p<COUNT, true>(mode, a, blocks, pblocks, lds, s, packet, fuse, qblocks)
-                   : launch_trace_p<COUNT, false>(mode, a, blocks, pblocks, lds, s, packet, 0, qblocks);
+                        int fuse) {
+    return primary ? launch_trace_p<COUNT, true>(mode, a, blocks, pblocks, lds, s, fuse)
+                   : launch_trace_p<COUNT, false>(mode, a, blocks, pblocks, lds, s, 0);
 }
 
 template <int MODE>
@@ -1616,21 +1313,6 @@ hipError_t launch_shade(int mode, bool first, bool direct, const PipeArgs& a, in
     if (mode == 0) return launch_shade_mode<0>(first, direct, a, blocks, s);
     if (mode == 1) return launch_shade_mode<1>(first, direct, a, blocks, s);
     return launch_shade_mode<2>(first, direct, a, blocks, s);
-}
-
-// Resident workgroups of the wave-queue trace kernels.
-int queue_blocks(ort_ctx* ctx, bool count, size_t lds, long long needed) {
-    int per_cu = 0, cus = 0;
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device);
-    const bool deep = ctx->depth > 8;
-    if (count)
-        (void)(deep ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ort_trace_compact_deep_q<true, true, false>, kBlock, lds)
-                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ort_trace_compact_q<true, true, false>, kBlock, lds));
-    else
-        (void)(deep ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ort_trace_compact_deep_q<false, true, true>, kBlock, lds)
-                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ort_trace_compact_q<false, true, true>, kBlock, lds));
-    const long long b = (long long)std::max(per_cu, 1) * std::max(cus, 1);
-    return (int)std::max(1LL, std::min(b, needed));
 }
 
 // Resident workgroups of the persistent trace kernel (a plain launch: extra groups just
@@ -1693,16 +1375,15 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
             (rc = ensure(ctx, ctx->pcol, 16 * slots)))
             return rc;
     }
-    const bool pers_all = ctx->persistent == 1;     // every trace persistent (rays stored by raygen)
     const bool pers_bounce = ctx->persistent == 2;  // persistent only for the bounce >= 1 lists
-    const bool compact = !direct && !pers_all && p->max_depth > 1;
+    const bool compact = !direct && p->max_depth > 1;
     // primary-ray mode (1 sample, 1 bounce) on the compact layout: the trace kernels shade
-    const bool fuse = direct && mode == 0 && !pers_all && !ctx->packet;
+    const bool fuse = direct && mode == 0;
     const bool sorted = compact && ctx->sort_paths == 1;   // radix sort of every slot's key
     const bool listsort = compact && ctx->sort_paths == 2; // sort of the appended list (its length read back)
     // bounce 0 of a multi-bounce frame: the trace kernels shade their camera rays into the path
     // state and append the paths that go on (no hit records, no shade launch: C5 -0.7 ms)
-    const bool fuse_first = compact && !sorted && mode == 0 && !ctx->packet && !ctx->wave_queue && !dcounters;
+    const bool fuse_first = compact && !sorted && mode == 0 && !dcounters;
     size_t qtemp_bytes = 0;
     if (compact) {
         qtemp_bytes = (sorted || listsort) ? ort::sortAliveTempBytes((int)slots) : 0;
@@ -1719,7 +1400,17 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
         if (listsort) {  // the list-length hints belong to one frame shape and scene
             const unsigned long long sig = frame_sig(ctx, p, t);
             if (sig != ctx->hint_sig) {
-                for (int i = 0; i < ort_ctx::kHints; ++i) ctx->alive_host[i] = -1;
+                int bank = -1;
+                for (int i = 1; i <= ort_ctx::kHintBanks && bank < 0; ++i) {
+                    const int c = (ctx->hint_bank + i) % ort_ctx::kHintBanks;
+                    if (!ctx->hint_ev_used[c] || hipEventQuery(ctx->hint_ev[c]) == hipSuccess) bank = c;
+                }
+                if (bank < 0) {  // every bank still awaits copies (several shape changes in flight)
+                    bank = (ctx->hint_bank + 1) % ort_ctx::kHintBanks;
+                    HIPCHK(ctx, hipEventSynchronize(ctx->hint_ev[bank]));
+                }
+                ctx->hint_bank = bank;
+                for (int i = 0; i < ort_ctx::kHints; ++i) ctx->alive_host[bank * ort_ctx::kHints + i] = -1;
                 ctx->hint_sig = sig;
             }
         }
@@ -1747,7 +1438,6 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     a.total = (int)slots;
     a.exact_only = ctx->exact_only || !ctx->ordered;
     a.refill = ctx->refill;
-    a.lut = (const uint8_t*)ctx->lut.p;
     a.hit = (int2*)ctx->hit.p;
     a.defer_list = (int*)ctx->defer_list.p;
     a.sync = (int*)ctx->defer_count.p;
@@ -1766,7 +1456,7 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     a.final_out = fuse_first ? 1 : 0;
     a.key_spread = (const uint32_t*)ctx->key_spread.p;
     // the cost order: the per-workgroup camera-ray kernels (ort_trace_compact[_deep]) only
-    if (mode == 0 && ctx->cost_order && !ctx->wave_queue && !ctx->packet && !pers_all && ctx->depth >= 2) {
+    if (mode == 0 && ctx->cost_order && ctx->depth >= 2) {
         if ((rc = ensure(ctx, ctx->pcost, 2 * slots))) return rc;
         const unsigned long long sig = frame_sig(ctx, p, t);
         if (sig != ctx->cost_sig) {  // a new shape: tile order for the first frame
@@ -1793,15 +1483,12 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     const size_t lds_exact = lds_bytes(mode, ctx->depth, true);
     const int pblocks = (mode == 0 && ctx->persistent) ? persistent_blocks(ctx->device, dcounters != nullptr, ctx->depth > 8, ctx->depth, lds, blocks) : 0;
     const int exact_blocks = 1024;
-    // wave queue: as many workgroups as are resident (never more than the frame has)
-    const int qblocks = (mode == 0 && ctx->wave_queue) ? queue_blocks(ctx, dcounters != nullptr, lds, blocks) : 0;
     hipError_t e;
     HIPCHK(ctx, hipEventRecord(ctx->ev0, s));
     const int fslot = (int)(ctx->frames % ort_ctx::kRing);  // this frame's timing slot
     ctx->tseg[fslot] = 0;
     for (int smp = 0; smp < ns; ++smp) {
         a.sample = smp;
-        a.rays_stored = pers_all && pblocks > 0;
         a.qlist = nullptr;  // bounce 0: every slot
         a.qcount = nullptr;
         // the alive paths of the current bounce in append order, and the buffer the next
@@ -1809,15 +1496,11 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
         int* qbuf[2] = {(int*)ctx->qlist.p, (int*)ctx->qlist2.p};
         int* qcnt[2] = {(int*)ctx->qcount.p, (int*)ctx->qcount.p + 4};
         int cur = 1;  // bounce 0 appends to qbuf[0]
-        if (a.rays_stored) {  // the persistent kernel refills lanes from stored rays
-            hipLaunchKernelGGL(ort_raygen_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, s, a);
-            if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "ort_raygen_kernel launch");
-        }
         const int bounces = maxd > 0 ? maxd : 1;
         a.nobounce = maxd <= 0;
         for (int b = 0; b < bounces; ++b) {
             a.last = (b == bounces - 1);
-            const int fmode = fuse ? 1 : ((b == 0 && fuse_first && !a.rays_stored) ? 2 : 0);
+            const int fmode = fuse ? 1 : ((b == 0 && fuse_first) ? 2 : 0);
             if (!a.nobounce) {
                 HIPCHK(ctx, hipMemsetAsync(ctx->defer_count.p, 0, 64, s));
                 const int slot = fslot;
@@ -1828,8 +1511,8 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                     HIPCHK(ctx, hipEventCreate(&ctx->tr1[slot][seg]));
                 }
                 if (timed) HIPCHK(ctx, hipEventRecord(ctx->tr0[slot][seg], s));
-                const bool prim = (b == 0) && !a.rays_stored;
-                const int pb = (pers_all || (pers_bounce && b > 0)) ? pblocks : 0;
+                const bool prim = b == 0;
+                const int pb = (pers_bounce && b > 0) ? pblocks : 0;
                 PipeArgs at = a;
                 if (pb > 0 && a.wclock) {  // analysis (ORT_PERSIST_CLOCK): a record range per launch
                     const long long nw = (long long)pb * (ctx->depth > 8 ? kPersistDeepBlock : kBlock) / 64;
@@ -1847,15 +1530,15 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                     if (bcost && pb > 0 && b > 0 && hi < nbc) at.bcost_w = bcost + (size_t)hi * slots;
                     if (bcost && fmode == 2 && hi + 1 < nbc && b + 1 < bounces) at.bcost_r = bcost + (size_t)(hi + 1) * slots;
                 }
-                e = dcounters ? launch_trace<true>(mode, prim, at, (int)blocks, pb, lds, s, ctx->packet != 0, fmode, qblocks)
-                              : launch_trace<false>(mode, prim, at, (int)blocks, pb, lds, s, ctx->packet != 0, fmode, qblocks);
+                e = dcounters ? launch_trace<true>(mode, prim, at, (int)blocks, pb, lds, s, fmode)
+                              : launch_trace<false>(mode, prim, at, (int)blocks, pb, lds, s, fmode);
                 if (e != hipSuccess) return hip_fail(ctx, e, "trace kernel launch");
                 if (timed) {
                     HIPCHK(ctx, hipEventRecord(ctx->tr1[slot][seg], s));
                     ctx->tseg[slot] = seg + 1;
                 }
                 if (mode == 0) {
-                    const bool prim = (b == 0) && !a.rays_stored;
+                    const bool prim = b == 0;
                     const dim3 g(exact_blocks), t(kBlock);
                     if (dcounters && fuse) hipLaunchKernelGGL((ort_trace_exact<true, true, 1>), g, t, lds_exact, s, at);
                     else if (dcounters && prim) hipLaunchKernelGGL((ort_trace_exact<true, true, 0>), g, t, lds_exact, s, at);
@@ -1865,12 +1548,6 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                     else if (prim) hipLaunchKernelGGL((ort_trace_exact<false, true, 0>), g, t, lds_exact, s, at);
                     else hipLaunchKernelGGL((ort_trace_exact<false, false, 0>), g, t, lds_exact, s, at);
                     if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "ort_trace_exact launch");
-                    if (ctx->dprobe && seg < ort_ctx::kSeg && !prim) {
-                        float4* o = ctx->dprobe + (size_t)seg * (1 + 2 * (size_t)ctx->dprobe_cap);
-                        hipLaunchKernelGGL(k_defer_dump, dim3(1), dim3(256), 0, s, (const int*)ctx->defer_list.p,
-                                           (const int*)ctx->defer_count.p, (const float4*)ctx->po.p,
-                                           (const float4*)ctx->pd.p, o, ctx->dprobe_cap);
-                    }
                 }
             }
             if (!fuse && fmode != 2) {
@@ -1921,7 +1598,7 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                         long long bound = (long long)slots;
                         if (ctx->sort_bound > 0) bound = ctx->sort_bound;
                         else if (hi < ort_ctx::kHints) {
-                            const int h = ((volatile int*)ctx->alive_host)[hi];
+                            const int h = ((volatile int*)ctx->alive_host)[ctx->hint_bank * ort_ctx::kHints + hi];
                             if (h >= 0) bound = (long long)h + (h >> 6) + 1024;
                         }
                         bound = std::min<long long>(bound, (long long)slots);
@@ -1931,7 +1608,7 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                         e = ort::sortListBounded(ctx->qtemp.p, qtemp_bytes, (int)bound, qcnt[cur], sb, s, key_bits);
                         if (e != hipSuccess) return hip_fail(ctx, e, "path list sort");
                         if (hi < ort_ctx::kHints)  // the next frame's bound (pinned: no host wait)
-                            HIPCHK(ctx, hipMemcpyAsync(ctx->alive_host + hi, qcnt[cur], sizeof(int),
+                            HIPCHK(ctx, hipMemcpyAsync(ctx->alive_host + ctx->hint_bank * ort_ctx::kHints + hi, qcnt[cur], sizeof(int),
                                                        hipMemcpyDeviceToHost, s));
                     }
                     a.qlist = listsort ? (const int*)ctx->svals.p : qbuf[cur];
@@ -1941,6 +1618,10 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
         }
     }
     if (ctx->tseg[fslot] > 0) ctx->frames += 1;
+    if (listsort) {  // after this frame's hint copies: the bank is free once this completes
+        HIPCHK(ctx, hipEventRecord(ctx->hint_ev[ctx->hint_bank], s));
+        ctx->hint_ev_used[ctx->hint_bank] = true;
+    }
     if (!direct && !a.final_out) {
         hipLaunchKernelGGL(ort_finalize_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, s, a);
         if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "ort_finalize_kernel launch");
@@ -1985,25 +1666,20 @@ int ort_create(int device, ort_ctx** out) {
             return rc;
         }
     }
-    if ((e = hipHostMalloc((void**)&c->alive_host, sizeof(int) * ort_ctx::kHints, hipHostMallocDefault)) != hipSuccess) {
+    if ((e = hipHostMalloc((void**)&c->alive_host, sizeof(int) * ort_ctx::kHints * ort_ctx::kHintBanks,
+                           hipHostMallocDefault)) != hipSuccess) {
         c->alive_host = nullptr;
         const int rc = hip_fail(nullptr, e, "ort_create: pinned hint buffer");
         ort_destroy(c);
         return rc;
     }
-    for (int i = 0; i < ort_ctx::kHints; ++i) c->alive_host[i] = -1;
-    {
-        std::vector<uint8_t> lut(kRankLutBytes);
-        for (size_t i = 0; i < lut.size(); ++i) lut[i] = ort::rank_lut_entry((uint32_t)i >> 8, (uint32_t)i & 255u);
-        const int rc = upload(c, c->lut, lut.data(), lut.size());
-        if (rc == ORT_OK) e = hipStreamSynchronize(c->stream);
-        if (rc != ORT_OK || e != hipSuccess) {
-            const int rc2 = rc != ORT_OK ? rc : hip_fail(nullptr, e, "ort_create: lut");
-            ort::set_thread_error(c->err);
+    for (int i = 0; i < ort_ctx::kHints * ort_ctx::kHintBanks; ++i) c->alive_host[i] = -1;
+    for (int i = 0; i < ort_ctx::kHintBanks; ++i)
+        if ((e = hipEventCreateWithFlags(&c->hint_ev[i], hipEventDisableTiming)) != hipSuccess) {
+            const int rc = hip_fail(nullptr, e, "ort_create: hint events");
             ort_destroy(c);
-            return rc2;
+            return rc;
         }
-    }
     *out = c;
     return ORT_OK;
 }
@@ -2015,7 +1691,6 @@ int ort_destroy(ort_ctx* ctx) {
     free_scene(ctx);
     free_buf(ctx->scratch_out);
     free_buf(ctx->counters);
-    free_buf(ctx->lut);
     DevBuf* pipe[] = {&ctx->hit, &ctx->defer_list, &ctx->defer_count, &ctx->po, &ctx->pd, &ctx->pc, &ctx->prng, &ctx->pcol,
                       &ctx->qlist, &ctx->qlist2, &ctx->qcount, &ctx->qtemp, &ctx->skeys, &ctx->skeys2, &ctx->svals, &ctx->key_spread,
                       &ctx->pcost, &ctx->bcost};
@@ -2029,6 +1704,8 @@ int ort_destroy(ort_ctx* ctx) {
         }
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->alive_host) (void)hipHostFree(ctx->alive_host);
+    for (hipEvent_t ev : ctx->hint_ev)
+        if (ev) (void)hipEventDestroy(ev);
     delete ctx;
     return ORT_OK;
 }
@@ -2043,14 +1720,14 @@ int ort_set_option(ort_ctx* ctx, int option, int value) {
         return ORT_OK;
     }
     if (option == ORT_OPT_PERSISTENT) {
-        if (value < 0 || value > 2) return fail(ctx, ORT_ERR_INVALID_ARG, "persistent must be 0, 1 or 2");
+        if (value == 1)  // removed in round 4
+            return fail(ctx, ORT_ERR_UNSUPPORTED, "ORT_OPT_PERSISTENT 1 (every trace persistent) was removed (C5 -19 %)");
+        if (value != 0 && value != 2) return fail(ctx, ORT_ERR_INVALID_ARG, "persistent must be 0 or 2");
         ctx->persistent = value;
         return ORT_OK;
     }
-    if (option == ORT_OPT_PACKET) {
-        ctx->packet = value ? 1 : 0;
-        return ORT_OK;
-    }
+    if (option == ORT_OPT_PACKET || option == ORT_OPT_WAVE_QUEUE)  // removed in round 4
+        return fail(ctx, ORT_ERR_UNSUPPORTED, "ORT_OPT_PACKET / ORT_OPT_WAVE_QUEUE were removed (measured slower: DESIGN.md 4)");
     if (option == ORT_OPT_KID_SKIP) {
         if (value < 0 || value > 2) return fail(ctx, ORT_ERR_INVALID_ARG, "ORT_OPT_KID_SKIP: 0, 1 or 2");
         ctx->kid_skip = value;
@@ -2059,10 +1736,6 @@ int ort_set_option(ort_ctx* ctx, int option, int value) {
     if (option == ORT_OPT_XCD_SWIZZLE) {
         if (value < 0 || value > 2) return fail(ctx, ORT_ERR_INVALID_ARG, "xcd swizzle must be 0, 1 or 2");
         ctx->xcd_swizzle = value;
-        return ORT_OK;
-    }
-    if (option == ORT_OPT_WAVE_QUEUE) {
-        ctx->wave_queue = value ? 1 : 0;
         return ORT_OK;
     }
     if (option == ORT_OPT_SORT_PATHS) {
@@ -2463,22 +2136,9 @@ int ort_debug_emulate_render(const float* cr, const float* ma, const float* fr, 
 }
 
 
-// ANALYSIS-ONLY (tools/wave_stats.py): walks sampled 8x8 pixel blocks (one wave each) of
-// the primary-ray frame with the kernel's fast walk on the host and reports how the lanes'
-// visited-node sets overlap, to price wave-level (packet) traversal against the per-lane
-// loop.  stats: see tools/wave_stats.py for the field order.
-// Analysis only: the wave-queue trace kernels record, per 64-slot block, {start, end}
-// (s_memrealtime, 100 MHz), HW_ID and XCC_ID into dev (n records of 4 x u64); null = off.
-// ANALYSIS-ONLY: after each bounce >= 1 trace launch of the next renders, k_defer_dump writes
-// that launch's deferred-ray count and its first `cap` rays to dev + launch * (1 + 2 cap)
-// float4s (launch = the frame's trace-launch index, < 16).  dev = NULL turns it off.
-int ort_debug_defer_probe(ort_ctx* ctx, void* dev, int32_t cap) {
-    if (!ctx || cap < 0) return ORT_ERR_INVALID_ARG;
-    ctx->dprobe = (float4*)dev;
-    ctx->dprobe_cap = dev ? cap : 0;
-    return ORT_OK;
-}
-
+// Analysis builds only (ORT_PERSIST_CLOCK, tools/persist_clock.py): the persistent bounce
+// kernel records a per-wave timeline {start, queue drained, end, XCC id | items << 8} into dev
+// (n records of 4 x u64, one range per launch of a frame); null = off.
 int ort_debug_wave_clock(ort_ctx* ctx, void* dev, int64_t n) {
     if (!ctx) return ORT_ERR_INVALID_ARG;
     ctx->wclock = dev;
@@ -2486,6 +2146,10 @@ int ort_debug_wave_clock(ort_ctx* ctx, void* dev, int64_t n) {
     return ORT_OK;
 }
 
+// ANALYSIS-ONLY (tools/wave_stats.py): walks sampled 8x8 pixel blocks (one wave each) of
+// the primary-ray frame with the kernel's fast walk on the host and reports how the lanes'
+// visited-node sets overlap, to price wave-level (packet) traversal against the per-lane
+// loop.  stats: see tools/wave_stats.py for the field order.
 int ort_debug_wave_stats(const float* cr, const float* ma, const float* fr, int32_t n_spheres,
                          const float* node_min, const float* node_max, const int32_t* co, const int32_t* oo,
                          const int32_t* cnt, int32_t n_nodes, const int32_t* idx, int64_t n_indices,

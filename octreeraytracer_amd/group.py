@@ -30,6 +30,10 @@ class RenderGroup:
             raise L.OrtError(rc, self._lib.ort_group_last_error(None).decode())
         self.devices = list(devices)
         self.inflight = int(inflight)
+        # outputs of submitted frames, kept alive until their frame is known complete (the ABI
+        # writes them asynchronously; a dropped torch tensor could otherwise be reallocated
+        # while the de-interleave kernel still writes it)
+        self._pending = {}
 
     def _check(self, rc):
         if rc != L.ORT_OK:
@@ -37,8 +41,9 @@ class RenderGroup:
 
     def close(self):
         if self._g:
-            self._lib.ort_group_destroy(self._g)
+            self._lib.ort_group_destroy(self._g)  # synchronizes every stream first
             self._g = C.c_void_p()
+        self._pending = {}
 
     def __enter__(self):
         return self
@@ -95,17 +100,28 @@ class RenderGroup:
         return out
 
     def submit(self, params: FrameParams, out) -> int:
-        """Enqueue a frame into `out` (as render(); keep it untouched until wait(ticket)) and
-        return its ticket at once (ort_group_submit)."""
+        """Enqueue a frame into `out` -- a numpy array or a float32 torch tensor on devices[0],
+        required: the frame is written asynchronously -- and return its ticket at once
+        (ort_group_submit).  Keep `out` untouched until wait(ticket); the group holds a
+        reference to it until then."""
+        if out is None:
+            raise ValueError("submit: out is required (the frame is written after submit returns; read it "
+                             "after wait(ticket))")
         p = params.to_c()
-        _, ptr, dev = self._out(params, out)
+        out, ptr, dev = self._out(params, out)
         tk = C.c_int64(-1)
         self._check(self._lib.ort_group_submit(self._g, C.byref(p), ptr, dev, C.byref(tk)))
+        self._pending[tk.value] = out
+        # submitting frame k waited for the frame that last used its slot (k - inflight) and
+        # every frame before it on that slot: those outputs are complete
+        for t in [t for t in self._pending if t <= tk.value - self.inflight]:
+            del self._pending[t]
         return tk.value
 
     def wait(self, ticket: int):
         """Block until frame `ticket` is complete in its output (ort_group_wait)."""
         self._check(self._lib.ort_group_wait(self._g, C.c_int64(int(ticket))))
+        self._pending.pop(int(ticket), None)
 
     def context(self, rank: int):
         """Rank `rank`'s context of frame slot 0 (owned by the group)."""

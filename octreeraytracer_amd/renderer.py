@@ -114,14 +114,6 @@ class Renderer:
         """Disable (True) / enable the sign-specialised fast walk; pixels are identical either way."""
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_EXACT_TRAVERSAL, int(bool(on))))
 
-    def set_packet(self, on: bool):
-        """Wave-level (packet) walk for camera rays (default off: SALU-bound); same pixels."""
-        self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_PACKET, int(bool(on))))
-
-    def set_wave_queue(self, on: bool):
-        """Wave-level block queue for the per-lane trace kernels (default off); same pixels."""
-        self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_WAVE_QUEUE, int(bool(on))))
-
     def set_xcd_swizzle(self, mode: int):
         """Workgroup -> tile order (ORT_OPT_XCD_SWIZZLE): 2 (default) runs of 8 raster tiles per
         XCD, 1 128x128-pixel super-tiles per XCD, 0 raster; same pixels."""
@@ -135,8 +127,8 @@ class Renderer:
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_SORT_PATHS, int(mode)))
 
     def set_persistent(self, on):
-        """Persistent trace kernel with lane refill: False/0 off, True/1 every trace, 2 bounce >= 1
-        traces only (same pixels)."""
+        """Persistent trace kernel with lane refill for the bounce >= 1 traces: 2 (default) on, 0 off
+        (same pixels).  1 (every trace persistent) was removed: OrtError."""
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_PERSISTENT, int(on)))
 
     def set_kid_skip(self, mode: int):

@@ -154,22 +154,16 @@ def test_errors(ort, renderer, scene_c1):
     fresh.close()
 
 
-@pytest.mark.parametrize("persistent,exact,refill,packet,queue", [
-    (False, False, 16, True, False), (False, False, 16, False, False), (False, True, 16, True, False),
-    (True, False, 1, False, False), (True, False, 16, False, False), (True, True, 64, False, False),
-    (2, False, 8, False, False), (2, True, 32, False, False), (False, False, 16, False, True),
-    (2, False, 16, False, True), (2, True, 16, False, True)])
-def test_kernel_variants_identical(ort, oracle, renderer, scene_c2, persistent, exact, refill, packet, queue):
-    """Every trace-kernel variant (packet walk / one ray per lane / persistent with refill /
-    wave queue, fast / exact walk) produces the oracle's pixels, also with several samples
-    and bounces."""
+@pytest.mark.parametrize("persistent,exact,refill", [
+    (0, False, 16), (0, True, 16), (2, False, 1), (2, False, 8), (2, True, 32), (2, False, 64)])
+def test_kernel_variants_identical(ort, oracle, renderer, scene_c2, persistent, exact, refill):
+    """Every trace-kernel variant (one ray per lane / persistent bounce walks with refill, fast
+    / exact walk) produces the oracle's pixels, also with several samples and bounces."""
     s, t = scene_c2
     renderer.upload(s, t)
     renderer.set_persistent(persistent)
     renderer.set_exact_traversal(exact)
     renderer.set_refill(refill)
-    renderer.set_packet(packet)
-    renderer.set_wave_queue(queue)
     try:
         p = ort.FrameParams.default_camera(1920, 1080, num_samples=2, max_depth=3)
         tile = ort.Tile(700, 200, 300, 120)
@@ -182,8 +176,15 @@ def test_kernel_variants_identical(ort, oracle, renderer, scene_c2, persistent, 
         renderer.set_persistent(2)  # the default
         renderer.set_exact_traversal(False)
         renderer.set_refill(16)  # the default
-        renderer.set_packet(False)
-        renderer.set_wave_queue(False)
+
+
+def test_removed_options_are_refused(ort, renderer):
+    """The variants removed in round 4 (packet walk, wave queue, every-trace persistent) fail
+    loudly instead of silently rendering another way."""
+    from octreeraytracer_amd import _lib as L
+    for opt, val in ((L.ORT_OPT_PACKET, 1), (L.ORT_OPT_WAVE_QUEUE, 1), (L.ORT_OPT_PERSISTENT, 1)):
+        with pytest.raises(ort.OrtError):
+            renderer._check(renderer._lib.ort_set_option(renderer._ctx, opt, val))
 
 
 @pytest.mark.parametrize("kid_skip", [1, 2, 0])
@@ -248,12 +249,6 @@ def test_c3_full_frame_bit_exact(ort, oracle, renderer, scene_c3):
     from octreeraytracer_amd.distributed import assemble, rank_tile
     parts = [renderer.render(p, rank_tile(3840, 2160, r, 8)) for r in range(8)]
     assert np.array_equal(assemble(np.stack(parts), 2160, 8), img)
-    # the wave-level (packet) walk gives the same frame
-    renderer.set_packet(True)
-    try:
-        assert_same(renderer.render(p), img, "C3 packet walk")
-    finally:
-        renderer.set_packet(False)
 
 
 def test_c3_counters_match_oracle_on_rows(ort, oracle, renderer, scene_c3):

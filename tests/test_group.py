@@ -108,9 +108,18 @@ def test_group_pipelined_frames(ort, oracle, scene_c2, inflight):
         host = np.empty((H, W, 3), np.float32)
         tickets = [g.submit(p, o) for p, o in zip(shots, outs)]
         assert tickets == list(range(len(shots)))
+        g.wait(tickets[-1])
+        ms_last = g.last_frame_ms()
+        # frame 0's slot has been reused since: its time was kept when it completed (not the
+        # time of the slot's later frame)
+        g.wait(tickets[0])
+        ms_first = g.last_frame_ms()
+        assert ms_last > 0 and ms_first > 0
         for tk in tickets:
             g.wait(tk)
         assert g.last_frame_ms() > 0
+        with pytest.raises(ValueError):
+            g.submit(shots[0], None)  # the frame is written after submit returns: out is required
         for k, (o, w) in enumerate(zip(outs, want)):
             assert np.array_equal(o.cpu().numpy().view(np.uint32), w.view(np.uint32)), k
         tk = g.submit(shots[2], host)  # host output through a slot
@@ -120,3 +129,14 @@ def test_group_pipelined_frames(ort, oracle, scene_c2, inflight):
         assert np.array_equal(outs[0].cpu().numpy()[500:540].view(np.uint32), ref.view(np.uint32))
         with pytest.raises(ort.OrtError):
             g.wait(99)
+
+
+def test_group_submit_requires_out(ort):
+    """submit() writes its frame asynchronously, so a missing output is refused before the ABI
+    (no GPU needed: the check runs first)."""
+    from octreeraytracer_amd.group import RenderGroup
+    g = object.__new__(RenderGroup)
+    g._g = None
+    g._pending = {}
+    with pytest.raises(ValueError):
+        g.submit(ort.FrameParams.default_camera(64, 32), None)

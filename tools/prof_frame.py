@@ -21,7 +21,6 @@ ap.add_argument("--warm", type=int, default=1,
                 help="frames rendered first and left out of the PMC sums (the cost order's first frame "
                      "has no previous-frame costs; bench.py's timed frames all do)")
 ap.add_argument("--layout", type=int, default=-1)
-ap.add_argument("--both", action="store_true", help="render with the packet walk on, then off")
 ap.add_argument("--meta", default="", help="write frames / traversals / build id here (JSON)")
 a = ap.parse_args()
 W, H, N, D, M, NS, MD = bench.CONFIGS[a.config]
@@ -31,23 +30,14 @@ r.set_layout(a.layout)
 r.build_scene(s, D, M)  # GPU octree builder (same tree as the host builder)
 p = ort.FrameParams.default_camera(W, H, num_samples=NS, max_depth=MD)
 out = np.empty((H, W, 3), np.float32)
-if a.both:
-    r.set_packet(True)  # first the wave-level walk, then (below) the per-lane walk
 ms = []
 for _ in range(a.warm + a.frames):
     r.render(p, out=out)
     ms.append(r.last_kernel_ms())
 print(f"{a.config} layout={r.info()['layout']} kernel ms: {['%.3f' % m for m in ms]}", flush=True)
-if a.both:
-    r.set_packet(False)
-    ms = []
-    for _ in range(a.frames):
-        r.render(p, out=out)
-        ms.append(r.last_kernel_ms())
-    print(f"{a.config} per-lane walk kernel ms: {['%.3f' % m for m in ms]}", flush=True)
 if a.meta:
     counts = r.count_traffic(p)  # COUNT=true kernel instances: excluded from the PMC sums by name
-    Path(a.meta).write_text(json.dumps({"config": a.config, "frames": a.frames * (2 if a.both else 1),
+    Path(a.meta).write_text(json.dumps({"config": a.config, "frames": a.frames,
                                         "warm_frames": a.warm,
                                         "traversals_per_frame": counts["traversals"], "counts": counts,
                                         "lib_sha": bench.lib_sha(), "device_sha": bench.device_sha(), "tile_rows": H}))

@@ -4,8 +4,8 @@ PMC record bench.py reads (profiles/pmc_<config>.json).
 usage: python tools/summarize_profile.py gpurun_out/<tag> profiles/<name> <config> [--no-record]
 
 Trace kernels = the production (COUNT=false) instances of the walk kernels that
-ort_frame_trace_times_ms times: ort_trace_compact[_deep][_q], ort_trace_persistent,
-ort_trace_packet, ort_trace_kernel.  Per-frame figures = the sum over a frame's launches."""
+ort_frame_trace_times_ms times: ort_trace_compact[_deep], ort_trace_persistent,
+ort_trace_kernel.  Per-frame figures = the sum over a frame's launches."""
 import csv
 import json
 import re
@@ -16,7 +16,7 @@ from pathlib import Path
 args = [a for a in sys.argv[1:] if not a.startswith("--")]
 src, dst, cfg = Path(args[0]), Path(args[1]), args[2]
 record = "--no-record" not in sys.argv
-TRACE_RE = re.compile(r"ort_trace_(compact_deep_q|compact_q|compact_deep|compact|persistent|packet|kernel)<(false|0)")
+TRACE_RE = re.compile(r"ort_trace_(compact_deep|compact|persistent|kernel)<(false|0)")
 
 
 def short(name):
