@@ -404,6 +404,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    # the static camera's frame (the later phases reuse the frame buffer)
+    saved = frame.cpu().numpy() if (args.save and rank == 0 and frame is not None) else None
     kern_ms = [a.elapsed_time(b) for a, b, _ in evs]       # whole per-frame pipeline (trace+shade+sort)
     latency_ms = [a.elapsed_time(c) for a, _, c in evs]    # render start -> frame gathered and assembled
     nframes0 = min(-(-args.steps // inflight), 64)          # context 0's timed frames
@@ -573,7 +575,7 @@ def main():
                 setup["host_octree_build_s"] = round(time.time() - t0, 3)
             result["cpu_baseline"] = cpu_baseline(spheres, tree, p, args.cpu_seconds, args.cpu_threads)
         if args.save:
-            img = frame.cpu().numpy()
+            img = saved
             from octreeraytracer_amd import image
             (image.write_png if args.save.endswith(".png") else image.write_pfm)(args.save, img)
     for x in rs:

@@ -2248,6 +2248,24 @@ int ort_debug_wave_stats(const float* cr, const float* ma, const float* fr, int3
                 stats[13] += act;         // lane-iterations
             }
             stats[14] += (double)maxlen;
+            if (n_stats >= 18) {
+                // wave-uniform iterations: every lane still walking pops the same node -- the
+                // leading run of them (the shared descent) and all of them
+                bool lead = true;
+                for (size_t k = 0; k < maxlen; ++k) {
+                    int nd = -1;
+                    bool uni = true;
+                    for (int l = 0; l < 64 && uni; ++l) {
+                        if (k >= seq[l].size()) continue;
+                        if (nd < 0) nd = seq[l][k];
+                        else if (seq[l][k] != nd) uni = false;
+                    }
+                    lead = lead && uni;
+                    stats[15] += lead ? 1 : 0;
+                    stats[16] += uni ? 1 : 0;
+                }
+                stats[17] += 1;
+            }
         }
         return ORT_OK;
     } catch (const std::exception& ex) {

@@ -24,14 +24,14 @@ p = ort.FrameParams.default_camera(W, H, num_samples=NS, max_depth=MD)
 lib = L.lib()
 f = lib.ort_debug_wave_stats
 f.restype = C.c_int
-st = np.zeros(16, np.float64)
+st = np.zeros(18, np.float64)
 fp = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
 arr = [np.ascontiguousarray(x) for x in (s.center_radius, s.mat_albedo, s.fuzz_ri)]
 tt = [np.ascontiguousarray(x) for x in (t.node_min, t.node_max, t.children_offset, t.objects_offset,
                                          t.object_count, t.object_indices)]
 rc = f(fp(arr[0]), fp(arr[1]), fp(arr[2]), C.c_int32(s.n), fp(tt[0]), fp(tt[1]), fp(tt[2]), fp(tt[3]),
        fp(tt[4]), C.c_int32(len(t.children_offset)), fp(tt[5]), C.c_int64(len(t.object_indices)),
-       C.byref(p.to_c()), C.c_int32(step), fp(st), C.c_int32(16))
+       C.byref(p.to_c()), C.c_int32(step), fp(st), C.c_int32(18))
 L.check(rc)
 waves, mixed, lanes, iI, iL, iS, uI, uL, uS, it, itI, itL, trips, laneit, maxlen = st[:15]
 print(f"{cfg}: {int(waves)} sampled waves (every {step}th 8x8 block), {int(mixed)} mixed-order, "
@@ -44,3 +44,5 @@ print(f"union / mean-ray: internal {uI / (iI / lanes * waves):.2f}x leaf {uL / (
 print(f"lockstep loop per wave: {it / waves:.1f} iterations ({itI / waves:.1f} with internal block, "
       f"{itL / waves:.1f} with leaf block, {trips / waves:.1f} sphere trips), "
       f"lane occupancy {laneit / (it * 64):.2f}")
+print(f"wave-uniform iterations (every walking lane pops the same node): leading {st[15] / waves:.1f}, "
+      f"all {st[16] / waves:.1f} of {it / waves:.1f}")
