@@ -122,6 +122,18 @@ typedef struct ort_scene_info {
                                       >= T, the rest, each class in coherence order -- so the longest
                                       walks start early rather than in the launch's drain tail (same
                                       pixels); 0: coherence order only */
+#define ORT_OPT_HEAVY_PRIO 13      /* T > 0: a wave of the camera-ray trace (cost order on) that holds a ray
+                                      whose walk took >= T steps in the previous frame of the same shape
+                                      runs at raised issue priority (s_setprio), so the frame's longest
+                                      walks do not set its end; 0: off.  Same pixels */
+#define ORT_OPT_SPLIT_HEAVY 14     /* T > 0 (1 sample, 1 bounce, cost order on): the camera rays whose walk
+                                      took >= T steps in the previous frame of the same shape (up to 4096
+                                      a frame) are each walked by 8 lanes that deal the walk's subtrees of
+                                      level ORT_OPT_SPLIT_LEVEL round robin (the first hit = the hit of the
+                                      lowest such subtree in the walk's order), on a second stream beside
+                                      the per-tile kernel: a small tile's frame no longer waits for its
+                                      longest walks.  0: off.  Same pixels */
+#define ORT_OPT_SPLIT_LEVEL 15     /* the level of those subtrees: 0 (default) = tree depth - 5 (at least 1) */
 
 /* Traffic counters (ort_count_traffic), in the REFERENCE layout's terms. */
 #define ORT_COUNT_NODES_POPPED 0

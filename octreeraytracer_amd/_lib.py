@@ -34,6 +34,9 @@ ORT_OPT_KID_SKIP = 9
 ORT_OPT_SORT_BOUND = 10
 ORT_OPT_COST_ORDER = 11
 ORT_OPT_HEAVY_FIRST = 12
+ORT_OPT_HEAVY_PRIO = 13
+ORT_OPT_SPLIT_HEAVY = 14
+ORT_OPT_SPLIT_LEVEL = 15
 ORT_LAYOUT_COMPACT_EXACT_EMULATION = 2
 ORT_COUNT_N = 6
 COUNT_NAMES = ("nodes_popped", "child_records", "leaf_objects", "accepted_hits", "pixels", "traversals")
@@ -143,6 +146,8 @@ def _declare(lib, strict: bool = True):
         "ort_debug_fast_order": (C.c_int, [C.c_int32, _ip, C.POINTER(C.c_uint8)]),
         "ort_debug_trace_rays": (C.c_int, [_fp, C.c_int32, _fp, _fp, _ip, _ip, _ip, C.c_int32, _ip, C.c_int64, _fp,
                                            C.c_int32, C.c_int32, _ip]),
+        "ort_debug_split_rays": (C.c_int, [_fp, C.c_int32, _fp, _fp, _ip, _ip, _ip, C.c_int32, _ip, C.c_int64, _fp,
+                                           C.c_int32, C.c_int32, C.c_int32, _ip]),
         "ort_debug_emulate_render": (C.c_int, [_fp, _fp, _fp, C.c_int32, _fp, _fp, _ip, _ip, _ip, C.c_int32, _ip,
                                                C.c_int64, C.c_int32, C.POINTER(OrtParams), C.POINTER(OrtTile),
                                                _fp, _u64p]),

@@ -33,6 +33,14 @@ int ort_debug_group_emulate(const float* sphere_center_radius, const float* sphe
 // rows (rank_lut_entry) for every child mask: lut256[cmask] (checked against the shader's
 // tables, tests/golden/traversal_orders.json).
 int ort_debug_fast_order(int32_t m, int32_t* order8, uint8_t* lut256);
+// TEST-ONLY: the split walk (render_core.h traverse_split, the walk of ort_trace_split) of each
+// ray run by `lanes` lanes one after another, level-`level` subtrees dealt round robin, merged by
+// the lowest DFS position; out[4 i] = {hit entry (-1 none), t bits, position, summed steps}.
+int ort_debug_split_rays(const float* sphere_center_radius, int32_t n_spheres, const float* node_min,
+                         const float* node_max, const int32_t* children_offset, const int32_t* objects_offset,
+                         const int32_t* object_count, int32_t n_nodes, const int32_t* object_indices,
+                         int64_t n_indices, const float* rays, int32_t n_rays, int32_t level, int32_t lanes,
+                         int32_t* out);
 // TEST-ONLY: per ray (origin.xyz, direction.xyz in rays[6 i]) the fast walk where the kernels
 // would take it (fast_prepare) and the exact walk (traverse_compact, literal GLSL min/max);
 // out[5 i] = {fast taken, fast entry, fast t bits, exact entry, exact t bits}.  bounce != 0:

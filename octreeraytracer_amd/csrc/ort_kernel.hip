@@ -76,6 +76,17 @@ struct PipeArgs {
     uint16_t* bcost_w;        // ORT_OPT_HEAVY_FIRST: the persistent bounce trace records each walk's steps here
     const uint16_t* bcost_r;  // ... the kernels appending the next bounce's list read that bounce's last-frame steps
     int heavy;                // ... walks of at least this many steps are heavy: they sort first
+    int prio_steps;   // ORT_OPT_HEAVY_PRIO: a camera-ray wave holding a ray whose last walk took >= this many
+                      // steps runs at raised issue priority (0: off)
+    // ORT_OPT_SPLIT_HEAVY (1 sample, 1 bounce): the camera rays whose walk took >= split steps in the
+    // previous frame, listed by k_heavy_scan, are walked by ort_trace_split (their walk dealt over 8
+    // lanes by level-split_level subtrees) on the context's second stream; the per-tile kernel
+    // passes over the slots hbits marks
+    const uint32_t* hbits;
+    const int* hlist;
+    int* hsync;       // [0] heavy rays found (the list holds the first hcap), [1] ort_trace_split's cursor
+    int hcap;
+    int split_level;
     ulonglong4* wclock;  // analysis builds only (ORT_PERSIST_CLOCK, ort_debug_wave_clock): per wave a timeline record
     int wclock_n;
 };
@@ -580,6 +591,9 @@ __device__ __forceinline__ bool trace_slot(PipeArgs& A, LdsView& L, int k, ort::
     ort::V3 inv = ort::mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
     // camera rays (jittered: practically never a zero component) keep the plain check, which
     // costs the hot kernel less (C3 +0.7 %); bounce rays take zero components fast too
+    if constexpr (PRIMARY && !COUNT && FUSE == 1) {
+        if (A.hbits && ((A.hbits[k >> 5] >> (k & 31)) & 1u)) return false;  // ort_trace_split walks and shades it
+    }
     if (A.exact_only || !(PRIMARY ? ort::fast_path_ok(ray, inv, 0.001f, ORT_MAXFLOAT) : ort::fast_prepare(A.S, ray, inv))) {
         A.defer_list[atomicAdd(A.sync, 1)] = k;  // ort_trace_exact walks (and, FUSE, shades) it
         if (PRIMARY && !COUNT && A.pcost) A.pcost[k] = 0;
@@ -691,12 +705,28 @@ __device__ __forceinline__ int cost_order_slot(const uint16_t* pcost, int* sc, i
 #endif
 }
 
+// Analysis builds only (-DORT_TILE_CLOCK=1, tools/tile_clock.py): the per-tile camera-ray
+// kernels record per wave {start, end, XCC id, the longest walk of its lanes} into wclock.
+#ifndef ORT_TILE_CLOCK
+#define ORT_TILE_CLOCK 0
+#endif
 template <bool COUNT, bool PRIMARY, bool DEEP, int FUSE>
 __device__ __forceinline__ void trace_compact_body(PipeArgs& A, unsigned char* smem) {
     if (!PRIMARY && A.qlist && (int)(blockIdx.x * kBlock) >= *A.qcount) return;  // whole block past the list
+#if ORT_TILE_CLOCK && defined(__HIP_DEVICE_COMPILE__)
+    const unsigned long long tclk0 = __builtin_amdgcn_s_memrealtime();
+#endif
     LdsView L = setup_lds<true>(smem, A.S);
     int k = blockIdx.x * kBlock + threadIdx.x;
-    if (PRIMARY && !COUNT && A.pcost) k = cost_order_slot<DEEP ? ORT_COST_SHIFT_DEEP : ORT_COST_SHIFT>(A.pcost, L.fr.co, k);  // (the counting pass: tile order)
+    if (PRIMARY && !COUNT && A.pcost) {  // (the counting pass: tile order)
+        k = cost_order_slot<DEEP ? ORT_COST_SHIFT_DEEP : ORT_COST_SHIFT>(A.pcost, L.fr.co, k);
+#if defined(__HIP_DEVICE_COMPILE__)
+        // heavy priority: the few waves holding the frame's longest walks start with the first
+        // workgroups but, sharing their SIMD with 7 others, finish long after the rest of a small
+        // tile (tools/tile_clock.py); they get the SIMD's issue slots first
+        if (A.prio_steps > 0 && __ballot((int)A.pcost[k] >= A.prio_steps)) __builtin_amdgcn_s_setprio(3);
+#endif
+    }
     if (!PRIMARY && !list_slot(A, k)) return;
     ort::Counters cnt;
     for (int q = 0; q < 6; ++q) cnt.v[q] = 0;
@@ -713,6 +743,19 @@ __device__ __forceinline__ void trace_compact_body(PipeArgs& A, unsigned char* s
 #endif
     }
     flush_counts<COUNT>(cnt, A.counters);
+#if ORT_TILE_CLOCK && defined(__HIP_DEVICE_COMPILE__)
+    if (PRIMARY && !COUNT) {
+        typedef __attribute__((address_space(4))) const PipeArgs KernArgs;
+        KernArgs* kp = (KernArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+        int st = kp->pcost ? (int)kp->pcost[k] : 0;
+        for (int o = 32; o >= 1; o >>= 1) st = max(st, __shfl_xor(st, o));
+        const int gw = (int)(blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6));
+        if (kp->wclock && (threadIdx.x & 63) == 0 && gw < kp->wclock_n) {
+            const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);  // XCC_ID
+            kp->wclock[gw] = make_ulonglong4(tclk0, __builtin_amdgcn_s_memrealtime(), xcc & 15u, (unsigned long long)st);
+        }
+    }
+#endif
 }
 
 // FUSE: 1 sample, 1 bounce -- the kernel also shades (shade_direct), no hit records.
@@ -727,6 +770,89 @@ ort_trace_compact_deep(PipeArgs A) {
     extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];  // plane tables: 1 KiB-aligned
     trace_compact_body<COUNT, PRIMARY, true, FUSE>(A, smem);
 }
+// Heavy camera rays (ORT_OPT_SPLIT_HEAVY): the slots whose walk took >= T steps in the previous
+// frame (pcost), listed (the first `cap` of them) and marked in a bitmap the per-tile kernel
+// reads.  A wave's slots are listed in slot order after one atomic.
+__global__ void __launch_bounds__(kBlock) k_heavy_scan(const uint16_t* pcost, int n, int T, int cap, uint32_t* bits,
+                                                       int* list, int* count) {
+    const int k = blockIdx.x * kBlock + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const bool h0 = k < n && (int)pcost[k] >= T;
+    const unsigned long long m = __ballot(h0);
+    int base = 0;
+    if (lane == 0 && m) base = atomicAdd(count, __popcll(m));
+    base = __shfl(base, 0);
+    const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const int pos = base + __popcll(m & below);
+    const bool h = h0 && pos < cap;  // past the cap the per-tile kernel walks them itself
+    if (h) list[pos] = k;
+    const unsigned long long mh = __ballot(h);
+    if (k < n && (lane & 31) == 0) bits[k >> 5] = (uint32_t)(mh >> (lane & 32));
+}
+
+// The heavy camera rays of k_heavy_scan's list, each walked by a group of 8 lanes that deal its
+// walk's level-split_level subtrees round robin (traverse_split), then shaded like the per-tile
+// kernel shades (FUSE 1: shade_direct).  Runs on the context's second stream beside the per-tile
+// kernel and ahead of it in the GPU's dispatch, at raised issue priority: the frame's longest
+// walks, run by one lane each, are what a small tile's frame waits for (tools/tile_clock.py).
+constexpr int kSplitLanes = 8;
+template <bool DEEP>
+__global__ void __launch_bounds__(kBlock) ort_trace_split(PipeArgs A) {
+    extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];  // plane tables: 1 KiB-aligned
+#if defined(__HIP_DEVICE_COMPILE__)
+    __builtin_amdgcn_s_setprio(3);
+#endif
+    const int count = min(A.hsync[0], A.hcap);
+    if (count == 0) return;
+    LdsView L = setup_lds<true>(smem, A.S);
+    using Masks = typename std::conditional<DEEP, ort::Masks96Split, ort::Masks64Split>::type;
+    const int lane = threadIdx.x & 63, g = lane / kSplitLanes, j = lane % kSplitLanes;
+    constexpr int kNoHit = 0x7fffffff;
+    for (;;) {
+        int base = 0;
+        if (lane == 0) base = atomicAdd(A.hsync + 1, 64 / kSplitLanes);
+        base = __shfl(base, 0);
+        if (base >= count) break;
+        const int idx = base + g;
+        const int k = idx < count ? A.hlist[idx] : -1;
+        int pos = kNoHit, entry = -1, steps = 0;
+        float t = 0.0f;
+        bool walked = false;
+        ort_rng rng0;
+        ort::Ray ray;
+        ray.o = ray.d = ort::mk(0.0f, 0.0f, 0.0f);
+        if (k >= 0) {
+            bool alive;
+            ray = slot_ray<true>(A, k, alive, &rng0);
+            const ort::V3 inv = ort::mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
+            if (alive && !A.exact_only && ort::fast_path_ok(ray, inv, 0.001f, ORT_MAXFLOAT)) {
+                walked = true;
+                ort::traverse_split<Masks>(A.S, L.planes, L.lut, ray, inv, A.split_level, kSplitLanes, j, pos, entry, t,
+                                           L.fr, steps);
+            } else if (alive && j == 0) {  // (a moved camera: rare) the exact kernel walks and shades it
+                A.defer_list[atomicAdd(A.sync, 1)] = k;
+                if (A.pcost) A.pcost[k] = 0;
+            }
+        }
+        // the group's result: the hit with the lowest DFS position
+        for (int o = 1; o < kSplitLanes; o <<= 1) {
+            const int op = __shfl_xor(pos, o, kSplitLanes);
+            const int oe = __shfl_xor(entry, o, kSplitLanes);
+            const float ot = __shfl_xor(t, o, kSplitLanes);
+            if (op < pos) {
+                pos = op;
+                entry = oe;
+                t = ot;
+            }
+            steps += __shfl_xor(steps, o, kSplitLanes);
+        }
+        if (walked && j == 0) {
+            if (A.pcost) A.pcost[k] = (uint16_t)min(steps, 65535);
+            shade_direct(A, k, ray, rng0, pos != kNoHit, entry, t);
+        }
+    }
+}
+
 // One-ray-per-lane trace for the explicit layout (MODE 1) and brute force (MODE 2).
 template <int MODE, bool COUNT, bool PRIMARY>
 __global__ void __launch_bounds__(kBlock) ort_trace_kernel(PipeArgs A) {
@@ -930,6 +1056,15 @@ struct ort_ctx {
     // first kCostBounces of a frame, every slot's last walk steps (cleared with cost_sig)
     static constexpr int kCostBounces = 8;
     int heavy_first = ORT_HEAVY_STEPS;
+    int heavy_prio = 0;  // ORT_OPT_HEAVY_PRIO (steps; 0 off)
+    // ORT_OPT_SPLIT_HEAVY (steps; 0 off) / ORT_OPT_SPLIT_LEVEL (0: auto): the heavy camera rays of a
+    // 1-sample 1-bounce frame walked by ort_trace_split on aux_stream (k_heavy_scan lists them)
+    int split_steps = 0;
+    int split_level = 0;
+    static constexpr int kSplitCap = 4096;  // heavy rays listed per frame at most
+    hipStream_t aux_stream = nullptr;
+    hipEvent_t ev_scan = nullptr, ev_split = nullptr;
+    DevBuf hbits, hlist, hsync;
     DevBuf bcost;
     unsigned long long bcost_sig = 0;
     float root_lo[3] = {0, 0, 0}, root_hi[3] = {0, 0, 0};  // root box (coherence-sort key)
@@ -1464,6 +1599,19 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
             ctx->cost_sig = sig;
         }
         a.pcost = (uint16_t*)ctx->pcost.p;
+        a.prio_steps = ctx->heavy_prio;
+    }
+    // split walks of the heavy camera rays (1 sample, 1 bounce; the production kernels)
+    const bool split = fuse && a.pcost && ctx->split_steps > 0 && !dcounters && ns == 1;
+    if (split) {
+        if ((rc = ensure(ctx, ctx->hbits, 4 * (slots / 32 + 1))) || (rc = ensure(ctx, ctx->hlist, 4 * (size_t)ort_ctx::kSplitCap)) ||
+            (rc = ensure(ctx, ctx->hsync, 64)))
+            return rc;
+        a.hsync = (int*)ctx->hsync.p;
+        a.hlist = (const int*)ctx->hlist.p;
+        a.hcap = ort_ctx::kSplitCap;
+        // the subtrees dealt to the lanes: ~5 levels above the leaves (a depth-8 tree: level 3)
+        a.split_level = ctx->split_level > 0 ? ctx->split_level : std::max(1, ctx->depth - 5);
     }
     // heavy first: the bounce >= 1 lists of the persistent trace (sorted, default path)
     const int nbc = std::min(ns * (maxd > 0 ? maxd : 1), ort_ctx::kCostBounces);  // recorded bounce indices
@@ -1530,9 +1678,28 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                     if (bcost && pb > 0 && b > 0 && hi < nbc) at.bcost_w = bcost + (size_t)hi * slots;
                     if (bcost && fmode == 2 && hi + 1 < nbc && b + 1 < bounces) at.bcost_r = bcost + (size_t)(hi + 1) * slots;
                 }
+                const bool do_split = split && fmode == 1;
+                if (do_split) {
+                    // the heavy rays of this frame (last frame's steps), then their split walks on the
+                    // second stream beside the per-tile kernel (which passes over them)
+                    HIPCHK(ctx, hipMemsetAsync(ctx->hsync.p, 0, 8, s));
+                    hipLaunchKernelGGL(k_heavy_scan, dim3((unsigned)blocks), dim3(kBlock), 0, s, (const uint16_t*)a.pcost,
+                                       (int)slots, ctx->split_steps, ort_ctx::kSplitCap, (uint32_t*)ctx->hbits.p,
+                                       (int*)ctx->hlist.p, (int*)ctx->hsync.p);
+                    HIPCHK(ctx, hipGetLastError());
+                    HIPCHK(ctx, hipEventRecord(ctx->ev_scan, s));
+                    HIPCHK(ctx, hipStreamWaitEvent(ctx->aux_stream, ctx->ev_scan, 0));
+                    const int hblocks = 32;  // 1024 heavy rays in flight; more loop
+                    if (ctx->depth > 8) hipLaunchKernelGGL(ort_trace_split<true>, dim3(hblocks), dim3(kBlock), lds, ctx->aux_stream, at);
+                    else hipLaunchKernelGGL(ort_trace_split<false>, dim3(hblocks), dim3(kBlock), lds, ctx->aux_stream, at);
+                    HIPCHK(ctx, hipGetLastError());
+                    HIPCHK(ctx, hipEventRecord(ctx->ev_split, ctx->aux_stream));
+                    at.hbits = (const uint32_t*)ctx->hbits.p;
+                }
                 e = dcounters ? launch_trace<true>(mode, prim, at, (int)blocks, pb, lds, s, fmode)
                               : launch_trace<false>(mode, prim, at, (int)blocks, pb, lds, s, fmode);
                 if (e != hipSuccess) return hip_fail(ctx, e, "trace kernel launch");
+                if (do_split) HIPCHK(ctx, hipStreamWaitEvent(s, ctx->ev_split, 0));  // joined before the exact kernel
                 if (timed) {
                     HIPCHK(ctx, hipEventRecord(ctx->tr1[slot][seg], s));
                     ctx->tseg[slot] = seg + 1;
@@ -1680,6 +1847,13 @@ int ort_create(int device, ort_ctx** out) {
             ort_destroy(c);
             return rc;
         }
+    if ((e = hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&c->ev_scan, hipEventDisableTiming)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&c->ev_split, hipEventDisableTiming)) != hipSuccess) {
+        const int rc = hip_fail(nullptr, e, "ort_create: second stream");
+        ort_destroy(c);
+        return rc;
+    }
     *out = c;
     return ORT_OK;
 }
@@ -1693,7 +1867,7 @@ int ort_destroy(ort_ctx* ctx) {
     free_buf(ctx->counters);
     DevBuf* pipe[] = {&ctx->hit, &ctx->defer_list, &ctx->defer_count, &ctx->po, &ctx->pd, &ctx->pc, &ctx->prng, &ctx->pcol,
                       &ctx->qlist, &ctx->qlist2, &ctx->qcount, &ctx->qtemp, &ctx->skeys, &ctx->skeys2, &ctx->svals, &ctx->key_spread,
-                      &ctx->pcost, &ctx->bcost};
+                      &ctx->pcost, &ctx->bcost, &ctx->hbits, &ctx->hlist, &ctx->hsync};
     for (DevBuf* b : pipe) free_buf(*b);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
@@ -1706,6 +1880,12 @@ int ort_destroy(ort_ctx* ctx) {
     if (ctx->alive_host) (void)hipHostFree(ctx->alive_host);
     for (hipEvent_t ev : ctx->hint_ev)
         if (ev) (void)hipEventDestroy(ev);
+    if (ctx->aux_stream) {
+        (void)hipStreamSynchronize(ctx->aux_stream);
+        (void)hipStreamDestroy(ctx->aux_stream);
+    }
+    if (ctx->ev_scan) (void)hipEventDestroy(ctx->ev_scan);
+    if (ctx->ev_split) (void)hipEventDestroy(ctx->ev_split);
     delete ctx;
     return ORT_OK;
 }
@@ -1746,6 +1926,21 @@ int ort_set_option(ort_ctx* ctx, int option, int value) {
     if (option == ORT_OPT_HEAVY_FIRST) {
         if (value < 0 || value > 65535) return fail(ctx, ORT_ERR_INVALID_ARG, "ORT_OPT_HEAVY_FIRST: 0 (off) .. 65535 steps");
         ctx->heavy_first = value;
+        return ORT_OK;
+    }
+    if (option == ORT_OPT_SPLIT_HEAVY) {
+        if (value < 0 || value > 65535) return fail(ctx, ORT_ERR_INVALID_ARG, "ORT_OPT_SPLIT_HEAVY: 0 (off) .. 65535 steps");
+        ctx->split_steps = value;
+        return ORT_OK;
+    }
+    if (option == ORT_OPT_SPLIT_LEVEL) {
+        if (value < 0 || value > ORT_COMPACT_MAX_DEPTH) return fail(ctx, ORT_ERR_INVALID_ARG, "ORT_OPT_SPLIT_LEVEL: 0 (auto) .. 10");
+        ctx->split_level = value;
+        return ORT_OK;
+    }
+    if (option == ORT_OPT_HEAVY_PRIO) {
+        if (value < 0 || value > 65535) return fail(ctx, ORT_ERR_INVALID_ARG, "ORT_OPT_HEAVY_PRIO: 0 (off) .. 65535 steps");
+        ctx->heavy_prio = value;
         return ORT_OK;
     }
     if (option == ORT_OPT_COST_ORDER) {
@@ -2008,6 +2203,74 @@ int ort_debug_trace_rays(const float* cr, int32_t n_spheres, const float* node_m
             o[2] = (int32_t)ort::f2u(tf);
             o[3] = ex;
             o[4] = (int32_t)ort::f2u(tx);
+        }
+        return ORT_OK;
+    } catch (const std::exception& ex) {
+        return fail(nullptr, ORT_ERR_INTERNAL, ex.what());
+    }
+}
+
+int ort_debug_split_rays(const float* cr, int32_t n_spheres, const float* node_min, const float* node_max,
+                         const int32_t* co, const int32_t* oo, const int32_t* cnt, int32_t n_nodes, const int32_t* idx,
+                         int64_t n_indices, const float* rays, int32_t n_rays, int32_t level, int32_t lanes, int32_t* out) {
+    try {
+        if (lanes < 1 || level < 1) return fail(nullptr, ORT_ERR_INVALID_ARG, "ort_debug_split_rays: lanes, level >= 1");
+        std::vector<float> ma((size_t)n_spheres * 4, 0.0f), fr((size_t)n_spheres * 4, 0.0f);
+        ort::SceneInput in{cr, ma.data(), fr.data(), n_spheres, node_min, node_max, co, oo, cnt, n_nodes, idx, n_indices};
+        const std::string vbad = ort::validateScene(in);
+        if (!vbad.empty()) return fail(nullptr, ORT_ERR_INVALID_ARG, vbad);
+        ort::CompactLayout cl;
+        std::string why;
+        if (!ort::buildCompactLayout(in, ORT_COMPACT_MAX_DEPTH, cl, why)) return fail(nullptr, ORT_ERR_UNSUPPORTED, why);
+        if (!cl.ordered) return fail(nullptr, ORT_ERR_UNSUPPORTED, "unordered tree");
+        ort::KScene S;
+        std::memset(&S, 0, sizeof(S));
+        S.n_spheres = n_spheres;
+        S.n_nodes = n_nodes;
+        S.node = (const uint2*)cl.node.data();
+        S.kid = (const uint2*)cl.kid.data();
+        S.tail_base = (uint32_t)in.n_indices;
+        S.leaf_sph = (const float4*)cl.leaf_sph.data();
+        S.leaf_idx = cl.leaf_idx.data();
+        S.planes = cl.planes.data();
+        S.depth = cl.depth;
+        std::vector<float> fplanes(ort::fast_plane_floats(cl.depth));  // the default image's layout
+        ort::fill_fast_planes(cl.planes.data(), fplanes.data(), cl.depth);
+        std::vector<uint8_t> lut(kRankLutBytes);
+        for (size_t i = 0; i < lut.size(); ++i) lut[i] = ort::rank_lut_entry((uint32_t)i >> 8, (uint32_t)i & 255u);
+        ort::LocalFrames lf;
+        for (int32_t i = 0; i < n_rays; ++i) {
+            ort::Ray r;
+            r.o = ort::mk(rays[6 * (size_t)i], rays[6 * (size_t)i + 1], rays[6 * (size_t)i + 2]);
+            r.d = ort::mk(rays[6 * (size_t)i + 3], rays[6 * (size_t)i + 4], rays[6 * (size_t)i + 5]);
+            const ort::V3 inv = ort::mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+            int32_t* o = out + 4 * (size_t)i;
+            o[0] = -1;
+            o[1] = 0;
+            o[2] = 0x7fffffff;
+            o[3] = 0;
+            if (!ort::fast_path_ok(r, inv, 0.001f, ORT_MAXFLOAT)) continue;
+            // the lanes of one group one after another; the lowest DFS position wins
+            int best = 0x7fffffff, be = -1, steps = 0;
+            float bt = 0.0f;
+            for (int j = 0; j < lanes; ++j) {
+                int pos = 0x7fffffff, e = -1, st = 0;
+                float t = 0.0f;
+                if (S.depth > 8)
+                    ort::traverse_split<ort::Masks96Split>(S, fplanes.data(), lut.data(), r, inv, level, lanes, j, pos, e, t, lf, st);
+                else
+                    ort::traverse_split<ort::Masks64Split>(S, fplanes.data(), lut.data(), r, inv, level, lanes, j, pos, e, t, lf, st);
+                steps += st;
+                if (pos < best) {
+                    best = pos;
+                    be = e;
+                    bt = t;
+                }
+            }
+            o[0] = be;
+            o[1] = (int32_t)ort::f2u(bt);
+            o[2] = best;
+            o[3] = steps;
         }
         return ORT_OK;
     } catch (const std::exception& ex) {

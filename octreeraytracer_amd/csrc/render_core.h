@@ -915,6 +915,19 @@ struct Masks64Plain : Masks64 {
     static constexpr bool kKidSkip = true;
 };
 
+// The split walk's level masks (traverse_split): no leaf children tested inline (the lanes
+// must pop every level-`level` node themselves, to count it) and no rejected-sphere skip (each
+// lane's skip state depends on the subtrees it walked, and a skipped level-`level` leaf would
+// shift that lane's subtree count against the others').
+struct Masks64Split : Masks64Plain {
+    static constexpr bool kKidSkip = false;
+};
+struct Masks96Split : Masks96 {
+    static constexpr bool kInlineLeaves = false;
+    static constexpr bool kLeadLeaves = false;
+    static constexpr bool kKidSkip = false;
+};
+
 // Node i's record into st.rec and, with kid (the rejected-sphere skip), its kid entry into
 // st.kd: both from the interleaved copy S.nk in one 16-byte load when the context built it
 // (ORT_NODE_KID), else from the two arrays.
@@ -1116,10 +1129,10 @@ ORT_FN bool leaf_kids(const KScene& S, FastStateT<Masks>& st, int co, uint32_t k
     return st.hit();
 }
 
-// One node of the walk: visit st.node (push its surviving children, or test its spheres),
-// then pop the next node.  Returns true when the walk is over (hit found, or stack empty).
+// Visit st.node: push its surviving children, or test its spheres.  Returns true when a hit
+// ends the walk (glsl:336).
 template <bool COUNT, class Masks, class Frames>
-ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks>& st, Frames& fr, Counters& cnt) {
+ORT_FN bool fast_visit(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks>& st, Frames& fr, Counters& cnt) {
     const int D = S.depth;
     const uint2 rec = st.rec;
     if (COUNT) cnt.v[0] += 1;
@@ -1204,6 +1217,19 @@ ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks
         const float ntmin = st.depth == 0 ? kFastTMin : fmax_tmin(fmax3(st.tNA, st.tNB, st.tNC));
         if (leaf_tests<COUNT>(S, st, (int)rec.x, (int)rec.y, ntmin, cnt)) return true;  // glsl:336
     }
+    return false;
+}
+
+// Pop the next node -- the lowest remaining rank of the deepest level with one left (the masks
+// must not be empty) -- and load its record and box planes.
+template <bool COUNT, class Masks, class Frames>
+ORT_FN void fast_pop(const KScene& S, FastStateT<Masks>& st, Frames& fr);
+
+// One node of the walk: visit st.node (push its surviving children, or test its spheres),
+// then pop the next node.  Returns true when the walk is over (hit found, or stack empty).
+template <bool COUNT, class Masks, class Frames>
+ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks>& st, Frames& fr, Counters& cnt) {
+    if (fast_visit<COUNT>(S, rank_lut, st, fr, cnt)) return true;
     if (st.masks.empty()) return true;
 #if defined(__HIP_DEVICE_COMPILE__) && defined(ORT_PAD_VALU)
     {   // issue-sensitivity experiment only (tools): ORT_PAD_VALU extra VALU per step
@@ -1217,6 +1243,13 @@ ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks
         for (int q = 0; q < ORT_PAD_SALU; ++q) asm volatile("s_mov_b32 %0, %0" : "+s"(ps));
     }
 #endif
+    fast_pop<COUNT>(S, st, fr);
+    return false;
+}
+
+template <bool COUNT, class Masks, class Frames>
+ORT_FN void fast_pop(const KScene& S, FastStateT<Masks>& st, Frames& fr) {
+    const int D = S.depth;
     // next node: lowest remaining rank of the deepest level with one left
     const int hb = st.masks.pop();
     const int L = hb >> 3;
@@ -1276,7 +1309,6 @@ ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks
             st.tMC = st.iC * (*st.at(nC, st.sC, w >> 1) - st.oC);
         }
     }
-    return false;
 }
 
 template <bool COUNT, class Masks, class Frames>
@@ -1297,6 +1329,50 @@ ORT_FN bool traverse_fast_t(const KScene& S, const float* planes, const uint8_t*
     hitEntry = st.hitEntry;
     hitT = st.closest;
     return st.hit();
+}
+
+// Split walk (the heavy camera rays of ort_trace_split): ONE ray's walk dealt over G lanes by
+// its level-`level` subtrees.  The reference DFS (glsl:312-479) walks the subtree of a node
+// completely before its next sibling, so the nodes of the walk's level-`level` subtrees are
+// contiguous, in DFS order, and a hit ends the walk (glsl:336): the walk's result is the first
+// hit of the lowest-ordered subtree holding one, unless a leaf above that level, visited before
+// it, holds one.  Lane j walks the nodes above the level and the subtrees i with i % G == j,
+// popping the others without visiting them, and stops at its first hit; `pos` orders the lanes'
+// hits by their place in the DFS -- 2i + 1 for a hit inside subtree i, 2c for a hit in a leaf
+// above the level visited after c subtrees -- and the lowest `pos` of the G lanes is the result
+// of the whole walk (bit-identical: each lane's visits are the reference walk's own).
+// Returns whether this lane found a hit; steps = the nodes it visited.
+template <class Masks, class Frames>
+ORT_FN bool traverse_split(const KScene& S, const float* planes, const uint8_t* rank_lut, const Ray& r, V3 inv,
+                           int level, int G, int j, int& pos, int& hitEntry, float& hitT, Frames& fr, int& steps) {
+    FastStateT<Masks> st;
+    Counters cnt;  // (COUNT = false: untouched)
+    steps = 0;
+    if (!fast_begin(S, planes, rank_lut, r, inv, kFastTMin, ORT_MAXFLOAT, st)) return false;
+    int sub = -1, seen = 0;  // the level-`level` subtree the walk is in; how many were popped
+    for (;;) {
+        ++steps;
+        if (fast_visit<false>(S, rank_lut, st, fr, cnt)) {
+            pos = st.depth >= level ? 2 * sub + 1 : 2 * seen;
+            hitEntry = st.hitEntry;
+            hitT = st.closest;
+            return true;
+        }
+        bool more = false;
+        while (!st.masks.empty()) {  // the next node, passing over other lanes' subtrees
+            fast_pop<false>(S, st, fr);
+            if (st.depth != level) {
+                more = true;
+                break;
+            }
+            sub = seen++;
+            if (sub % G == j) {
+                more = true;
+                break;
+            }
+        }
+        if (!more) return false;
+    }
 }
 
 template <bool COUNT, class Frames>

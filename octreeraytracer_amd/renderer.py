@@ -146,6 +146,20 @@ class Renderer:
         >= T (T = steps, default 64), the rest last; 0 off (coherence order only).  Same pixels."""
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_HEAVY_FIRST, int(steps)))
 
+    def set_heavy_prio(self, steps: int):
+        """ORT_OPT_HEAVY_PRIO: camera-ray waves holding a walk of >= steps (last frame) run at raised
+        issue priority; 0 off.  Same pixels."""
+        self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_HEAVY_PRIO, int(steps)))
+
+    def set_split_heavy(self, steps: int):
+        """ORT_OPT_SPLIT_HEAVY: camera rays whose walk took >= steps (last frame) are walked by 8 lanes
+        each, their subtrees dealt round robin, beside the per-tile kernel; 0 off.  Same pixels."""
+        self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_SPLIT_HEAVY, int(steps)))
+
+    def set_split_level(self, level: int):
+        """ORT_OPT_SPLIT_LEVEL: the level of the subtrees a split walk deals (0: depth - 5)."""
+        self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_SPLIT_LEVEL, int(level)))
+
     def set_cost_order(self, on: int):
         """ORT_OPT_COST_ORDER: 1 (default) camera rays dealt to waves by last frame's walk cost; 0 fixed blocks."""
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_COST_ORDER, int(on)))

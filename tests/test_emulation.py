@@ -235,3 +235,56 @@ def test_ordinary_rays_fast_equals_exact(ort):
     out = _trace_rays(ort, s, t, np.concatenate([o, dirs], axis=1), 0)
     assert (out[:, 0] == 1).all()
     assert (out[:, 1] == out[:, 3]).all() and (out[out[:, 1] >= 0, 2] == out[out[:, 1] >= 0, 4]).all()
+
+
+def _split_rays(ort, s, t, rays, level, lanes):
+    from octreeraytracer_amd import _lib as L
+    lib = L.lib()
+    arr = [np.ascontiguousarray(a, d) for a, d in (
+        (s.center_radius, np.float32), (t.node_min, np.float32), (t.node_max, np.float32),
+        (t.children_offset, np.int32), (t.objects_offset, np.int32), (t.object_count, np.int32),
+        (t.object_indices, np.int32))]
+    rays = np.ascontiguousarray(rays, np.float32)
+    out = np.zeros((len(rays), 4), np.int32)
+    L.check(lib.ort_debug_split_rays(L.fptr(arr[0]), s.n, L.fptr(arr[1]), L.fptr(arr[2]), L.iptr(arr[3]),
+                                     L.iptr(arr[4]), L.iptr(arr[5]), t.n_nodes, L.iptr(arr[6]), t.n_indices,
+                                     L.fptr(rays), len(rays), int(level), int(lanes), L.iptr(out)))
+    return out
+
+
+@pytest.mark.parametrize("n,d,m", [(2000, 5, 0), (10_000, 8, 0), (2000, 8, 1), (3000, 10, 1)])
+def test_split_walk_equals_the_walk(ort, oracle, n, d, m):
+    """The split walk of ort_trace_split (render_core.h traverse_split): one ray's walk dealt over
+    several lanes by its level-L subtrees, the lanes' first hits merged by DFS position, finds the
+    walk's own hit (entry and t bits) -- for every split level, lane count, camera rays (with the
+    field's longest, grazing walks) and random rays from inside the scene."""
+    s = ort.random_spheres(n, 11)
+    t = ort.build_octree(s, d, m)
+    rng = np.random.default_rng(n + d + m)
+    p = ort.FrameParams.default_camera(320, 180)
+    cam = oracle.camera(p)[:12].astype(np.float64).reshape(4, 3)  # origin, lower-left, horizontal, vertical
+    u, v = rng.uniform(0, 1, (2, 1500))
+    org = np.broadcast_to(cam[0], (1500, 3))
+    dirs = cam[1] + u[:, None] * cam[2] + v[:, None] * cam[3] - cam[0]
+    lo, hi = t.node_min[0].astype(np.float64), t.node_max[0].astype(np.float64)
+    o2 = lo + (hi - lo) * rng.uniform(0, 1, (1500, 3))
+    d2 = rng.normal(size=(1500, 3))
+    rays = np.concatenate([np.concatenate([org, dirs], 1), np.concatenate([o2, d2], 1)]).astype(np.float32)
+    rays[:, 3:] /= np.linalg.norm(rays[:, 3:], axis=1, keepdims=True)
+    want = _trace_rays(ort, s, t, rays, 0)
+    fast = want[:, 0] == 1
+    assert fast.mean() > 0.99
+    for level in range(1, d + 1):
+        for lanes in (1, 3, 8):
+            got = _split_rays(ort, s, t, rays, level, lanes)
+            assert np.array_equal(got[fast, 0], want[fast, 1]), (level, lanes)
+            hit = want[fast, 1] >= 0
+            assert np.array_equal(got[fast, 1][hit], want[fast, 2][hit]), (level, lanes)
+    # and the oracle's traverseOctree on a sample
+    ref = oracle.trace_rays(s, t, rays[:400])
+    got = _split_rays(ort, s, t, rays[:400], max(1, d - 5), 8)
+    sel = fast[:400]
+    assert np.array_equal((got[sel, 0] >= 0).astype(np.int32), ref[sel, 0])
+    hit = ref[sel, 0] == 1
+    assert np.array_equal(got[sel, 1][hit], ref[sel, 1][hit])
+    assert hit.mean() > 0.05

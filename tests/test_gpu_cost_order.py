@@ -104,3 +104,52 @@ def test_heavy_first_option_range(ort):
             r.set_heavy_first(70000)
         r.set_heavy_first(0)
         r.set_heavy_first(384)
+
+
+@pytest.mark.parametrize("split,level,prio", [(40, 0, 150), (20, 1, 0), (60, 2, 60), (30, 5, 0)])
+def test_split_heavy_frames_match(ort, oracle, scene_c2, split, level, prio):
+    """Split walks of the heavy camera rays (ORT_OPT_SPLIT_HEAVY: 8 lanes per ray on the second
+    stream, subtrees of one level dealt round robin) and heavy-wave priority (ORT_OPT_HEAVY_PRIO):
+    low thresholds make many rays heavy (up to the 4096-ray cap, the rest walked by the tiles).
+    Static camera, moved camera (last frame's costs), a band tile, every split level: bit-exact
+    vs the plain per-tile kernel and the oracle."""
+    from octreeraytracer_amd.scene import DEFAULT_YAW
+    s, t = scene_c2
+    W, H = 960, 540
+    p0 = ort.FrameParams.default_camera(W, H)
+    p1 = ort.FrameParams.default_camera(W, H, yaw=DEFAULT_YAW + 3.0)
+    full = ort.Tile(0, W, 0, H)
+    band = ort.Tile(0, W, 0, 136, band_height=16, band_stride=128)
+    params = [p0, p0, p1, p1, p0, p0, p0]
+    tiles = [full, full, full, full, band, band, full]
+    with ort.Renderer(0) as r:
+        r.upload(s, t)
+        want = _frames(ort, r, s, t, params, tiles)
+    with ort.Renderer(0) as r:
+        r.upload(s, t)
+        r.set_split_heavy(split)
+        r.set_split_level(level)
+        r.set_heavy_prio(prio)
+        got = _frames(ort, r, s, t, params, tiles)
+    for i, (a, b) in enumerate(zip(got, want)):
+        assert_same(a, b, f"frame {i}: split {split} level {level} vs plain")
+    ref = oracle.render(s, t, p1, 0, 300, W, 16)
+    assert_same(got[3][300:316], ref, "moved camera, split walks vs oracle")
+
+
+def test_split_heavy_deep_tree(ort, oracle):
+    """The split walk over 96-bit masks (depth 9): bit-exact vs the plain kernel and the oracle."""
+    s = ort.random_spheres(20000, 42)
+    t = ort.build_octree(s, 9, 1)
+    W, H = 480, 270
+    p = ort.FrameParams.default_camera(W, H)
+    with ort.Renderer(0) as r:
+        r.upload(s, t)
+        want = [r.render(p) for _ in range(2)]
+    with ort.Renderer(0) as r:
+        r.upload(s, t)
+        r.set_split_heavy(30)
+        got = [r.render(p) for _ in range(3)]
+    for g in got:
+        assert_same(g, want[1], "deep split")
+    assert_same(got[2][100:116], oracle.render(s, t, p, 0, 100, W, 16), "deep split vs oracle")
