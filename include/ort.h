@@ -134,6 +134,10 @@ typedef struct ort_scene_info {
                                       the per-tile kernel: a small tile's frame no longer waits for its
                                       longest walks.  0: off.  Same pixels */
 #define ORT_OPT_SPLIT_LEVEL 15     /* the level of those subtrees: 0 (default) = tree depth - 5 (at least 1) */
+#define ORT_OPT_TILE_PAIRS 16      /* 1: a camera-ray workgroup renders two 16x16 tiles side by side, its 512
+                                      pixels dealt to 8 blocks of 64 by last frame's walk steps and each
+                                      wave walking a heavy and a light block (a workgroup keeps its LDS
+                                      until its slowest wave ends); 0: a tile per workgroup.  Same pixels */
 
 /* Traffic counters (ort_count_traffic), in the REFERENCE layout's terms. */
 #define ORT_COUNT_NODES_POPPED 0

@@ -45,7 +45,8 @@ struct PipeArgs {
     ort::PixelParams pp;
     ort::KScene S;
     TileMap tm;
-    int tilesX, tilesY;
+    int tilesX, tilesY;  // the dispatch grid: tiles, or (pair) tile pairs across x tiles
+    int pair;         // ORT_OPT_TILE_PAIRS: a camera-ray workgroup renders two tiles side by side (trace_pair_body)
     int swizzle;      // ORT_OPT_XCD_SWIZZLE (block_tile)
     int xrun_log2;    // swizzle 2: log2 of the tiles per XCD run (xcd_run_log2)
     int total;        // path slots = workgroups x 256 (tile-block order, some are holes)
@@ -192,7 +193,7 @@ inline int xcd_run_log2(int tilesX) {
     while (lr < 6 && (2 << lr) * 15 <= tilesX) ++lr;
     return lr;
 }
-__host__ __device__ inline void block_tile(const PipeArgs& A, int blk, int& bx, int& by) {
+__host__ __device__ inline void block_tile_grid(const PipeArgs& A, int blk, int& bx, int& by) {
     if (!A.swizzle) {
         bx = blk % A.tilesX;
         by = blk / A.tilesX;
@@ -219,21 +220,37 @@ __host__ __device__ inline void block_tile(const PipeArgs& A, int blk, int& bx, 
     bx = sc * 8 + r2 % cols;
     by = srow * 8 + r2 / cols;
 }
+// Tile pairs (ORT_OPT_TILE_PAIRS): slot blocks 2b and 2b+1 are the two tiles of pair b, which the
+// swizzle places on the pair grid (x-adjacent tiles; a last odd column's second tile is a hole).
+__host__ __device__ inline void block_tile(const PipeArgs& A, int blk, int& bx, int& by) {
+    if (!A.pair) {
+        block_tile_grid(A, blk, bx, by);
+        return;
+    }
+    block_tile_grid(A, blk >> 1, bx, by);
+    bx = 2 * bx + (blk & 1);
+}
 
 // Path slot k (tile-block order: 256 slots = one 16x16 tile, 64 = one 8x8 wave block)
 // -> tile column/row.  Returns false for slots outside the tile.  UNI: every lane of the wave
 // holds a slot of the same 256-slot block (the per-tile kernels), so the tile lookup -- two
-// integer divisions by the tile-grid width -- runs once per wave on the scalar unit.
-template <bool UNI = false>
+// integer divisions by the tile-grid width -- runs once per wave on the scalar unit.  UNI 2:
+// every lane holds a slot of the same tile PAIR (tile pairs, cost_order_pair), so the pair's
+// place is looked up once per wave and each lane picks its tile of the two.
+template <int UNI = 0>
 __host__ __device__ inline bool slot_coords(const PipeArgs& A, int k, int& col, int& row) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    const int blk = UNI ? __builtin_amdgcn_readfirstlane(k >> 8) : k >> 8;
-#else
-    const int blk = k >> 8;
-#endif
     const int tid = k & 255, wave = tid >> 6, lane = tid & 63;
     int bx, by;
-    block_tile(A, blk, bx, by);
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (UNI == 2) {
+        block_tile_grid(A, __builtin_amdgcn_readfirstlane(k >> 9), bx, by);
+        bx = 2 * bx + ((k >> 8) & 1);
+    } else {
+        block_tile(A, UNI ? __builtin_amdgcn_readfirstlane(k >> 8) : k >> 8, bx, by);
+    }
+#else
+    block_tile(A, k >> 8, bx, by);
+#endif
     col = bx * 16 + (wave & 1) * 8 + (lane & 7);  // an 8x8 block per wave (16x4 and 4x16: no faster, §8)
     row = by * 16 + (wave >> 1) * 8 + (lane >> 3);
     return col < A.tm.tw && row < A.tm.th;
@@ -407,7 +424,7 @@ __device__ inline bool list_slot(const PipeArgs& A, int& k) {
 // Path-slot ray for the trace kernels: bounce 0 generates the sample's camera ray here
 // (main() up to radiance()'s first line; the shade kernel regenerates it identically),
 // later bounces read the ray the previous shade kernel stored.
-template <bool PRIMARY, bool UNI = false>
+template <bool PRIMARY, int UNI = 0>
 __device__ inline ort::Ray slot_ray(const PipeArgs& A, int k, bool& alive, ort_rng* st_out = nullptr) {
     if constexpr (PRIMARY) {
         int col, row;
@@ -436,7 +453,7 @@ __device__ inline ort::Ray slot_ray(const PipeArgs& A, int k, bool& alive, ort_r
 
 // 1 sample, 1 bounce (the primary-ray benchmark mode): the trace kernels shade their own
 // rays -- exactly ort_shade_kernel<0, true, true> -- instead of writing hit records for it.
-template <bool UNI = false>
+template <int UNI = 0>
 __device__ inline void shade_direct(const PipeArgs& A, int k, ort::Ray ray, ort_rng st, bool hit, int entry, float t) {
     int col, row;
     (void)slot_coords<UNI>(A, k, col, row);
@@ -454,9 +471,10 @@ __device__ inline void shade_direct(const PipeArgs& A, int k, ort::Ray ray, ort_
     o[2] = v.z;
 }
 // Tile rows past the frame (band padding) are written as zeros, as the shade kernel does.
+template <int UNI = 1>
 __device__ inline void shade_direct_padding(const PipeArgs& A, int k) {
     int col, row;
-    if (!slot_coords<true>(A, k, col, row) || tile_row_to_y(A.tm, row) < A.pp.H) return;
+    if (!slot_coords<UNI>(A, k, col, row) || tile_row_to_y(A.tm, row) < A.pp.H) return;
     float* o = A.out + 3 * ((size_t)row * A.tm.tw + col);
     o[0] = 0.0f;
     o[1] = 0.0f;
@@ -575,23 +593,24 @@ __device__ __forceinline__ uint32_t light_bit(const uint16_t* bcost_r, int heavy
 // FUSE: 0 the walk's hit record is stored (shaded by ort_shade_kernel); 1 (1 sample, 1 bounce)
 // the kernel shades its ray into the final pixel; 2 (bounce 0 of a multi-bounce frame) the
 // kernel shades its ray into the path state and returns whether the path goes on.
-template <bool COUNT, bool PRIMARY, bool DEEP, int FUSE>
+// UNI: every lane of the wave holds a slot of the same tile (slot_coords); tile pairs: of either.
+template <bool COUNT, bool PRIMARY, bool DEEP, int FUSE, int UNI = 1>
 __device__ __forceinline__ bool trace_slot(PipeArgs& A, LdsView& L, int k, ort::Counters& cnt) {
     bool alive;
     ort_rng rng0;  // FUSE: the camera ray's RNG state, kept for the shading after the walk
-    const ort::Ray ray = slot_ray<PRIMARY, true>(A, k, alive, FUSE ? &rng0 : nullptr);
+    const ort::Ray ray = slot_ray<PRIMARY, UNI>(A, k, alive, FUSE ? &rng0 : nullptr);
     if (!alive) {
-        if (FUSE == 1) shade_direct_padding(A, k);
+        if (FUSE == 1) shade_direct_padding<UNI>(A, k);
         if (FUSE == 2) {
             A.pd[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // never alive (ort_shade_kernel's hole)
-            if (A.final_out && A.sample == A.pp.ns - 1) shade_direct_padding(A, k);  // band padding rows
+            if (A.final_out && A.sample == A.pp.ns - 1) shade_direct_padding<UNI>(A, k);  // band padding rows
         }
         return false;
     }
     ort::V3 inv = ort::mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
     // camera rays (jittered: practically never a zero component) keep the plain check, which
     // costs the hot kernel less (C3 +0.7 %); bounce rays take zero components fast too
-    if constexpr (PRIMARY && !COUNT && FUSE == 1) {
+    if constexpr (PRIMARY && !COUNT && FUSE != 0) {
         if (A.hbits && ((A.hbits[k >> 5] >> (k & 31)) & 1u)) return false;  // ort_trace_split walks and shades it
     }
     if (A.exact_only || !(PRIMARY ? ort::fast_path_ok(ray, inv, 0.001f, ORT_MAXFLOAT) : ort::fast_prepare(A.S, ray, inv))) {
@@ -635,10 +654,10 @@ __device__ __forceinline__ bool trace_slot(PipeArgs& A, LdsView& L, int k, ort::
         const PipeArgs& A2 = A;
 #endif
         if constexpr (FUSE == 1) {
-            shade_direct<true>(A2, k2, walked, rng0, hit, entry, t);
+            shade_direct<UNI>(A2, k2, walked, rng0, hit, entry, t);
         } else {
             int col, row;
-            (void)slot_coords<true>(A2, k2, col, row);
+            (void)slot_coords<UNI>(A2, k2, col, row);
             return shade_state<0, true, false>(A2, k2, (size_t)row * A2.tm.tw + col, walked, rng0, hit ? entry : -1, t);
         }
     } else {
@@ -705,10 +724,87 @@ __device__ __forceinline__ int cost_order_slot(const uint16_t* pcost, int* sc, i
 #endif
 }
 
+// Cost order over a tile pair (ORT_OPT_TILE_PAIRS): the 512 slots of workgroup b (slots 512b ..
+// 512b + 511, two tiles) in eight blocks of 64 by last frame's walk steps (the stable counting
+// sort of cost_order_slot, buckets of 4 steps), and wave w walks block 7 - w and then block w: a
+// workgroup holds its LDS until its slowest wave ends, and with one block per wave the cost
+// order left 12-13 % of the waves' time idle inside the workgroups (tools/tile_clock.py); the
+// longest-processing-time pairs (7,0) (6,1) (5,2) (4,3) even the waves out.  Scratch: the
+// first 1024 ints of the frame columns (free before the walk; lds_bytes >= 4 levels).
+template <int SHIFT>
+__device__ __forceinline__ void cost_order_pair(const uint16_t* pcost, int* sc, int base, int& kk0, int& kk1) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const uint32_t b0 = min((uint32_t)pcost[base + tid] >> SHIFT, 63u);
+    const uint32_t b1 = min((uint32_t)pcost[base + 256 + tid] >> SHIFT, 63u);
+    uint64_t m0 = ~0ull, m1 = ~0ull;  // the lanes of this wave in the same bucket, per item
+    for (int i = 0; i < 6; ++i) {
+        const uint64_t bal0 = __ballot((b0 >> i) & 1u), bal1 = __ballot((b1 >> i) & 1u);
+        m0 &= ((b0 >> i) & 1u) ? bal0 : ~bal0;
+        m1 &= ((b1 >> i) & 1u) ? bal1 : ~bal1;
+    }
+    const int below0 = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m0, 0u));
+    const int below1 = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0u));
+    int* cnt = sc;         // [virtual wave 0..7][bucket]: items, then first position
+    int* perm = sc + 512;  // position -> item (0..511)
+    cnt[tid] = 0;
+    cnt[256 + tid] = 0;
+    __syncthreads();
+    if (below0 == 0) cnt[wave * 64 + b0] = __popcll(m0);
+    if (below1 == 0) cnt[(4 + wave) * 64 + b1] = __popcll(m1);
+    __syncthreads();
+    if (wave == 0) {  // lane = bucket: exclusive scan of the bucket totals, then the virtual waves in order
+        int c[8];
+        int tot = 0;
+        for (int v = 0; v < 8; ++v) {
+            c[v] = cnt[v * 64 + lane];
+            tot += c[v];
+        }
+        int incl = tot;
+        for (int off = 1; off < 64; off <<= 1) {
+            const int x = __shfl_up(incl, off);
+            if (lane >= off) incl += x;
+        }
+        int pos = incl - tot;
+        for (int v = 0; v < 8; ++v) {
+            cnt[v * 64 + lane] = pos;
+            pos += c[v];
+        }
+    }
+    __syncthreads();
+    perm[cnt[wave * 64 + b0] + below0] = tid;
+    perm[cnt[(4 + wave) * 64 + b1] + below1] = 256 + tid;
+    __syncthreads();
+    kk0 = base + perm[64 * (7 - wave) + lane];
+    kk1 = base + perm[64 * wave + lane];
+    __syncthreads();  // the frame columns are the walk's from here
+#else
+    (void)pcost;
+    (void)sc;
+    kk0 = base + (int)threadIdx.x;
+    kk1 = kk0 + 256;
+#endif
+}
+
 // Analysis builds only (-DORT_TILE_CLOCK=1, tools/tile_clock.py): the per-tile camera-ray
 // kernels record per wave {start, end, XCC id, the longest walk of its lanes} into wclock.
 #ifndef ORT_TILE_CLOCK
 #define ORT_TILE_CLOCK 0
+#endif
+#if ORT_TILE_CLOCK && defined(__HIP_DEVICE_COMPILE__)
+template <bool ON>
+__device__ inline void tile_clock_record(int k0, int k1, unsigned long long tclk0) {
+    if (!ON) return;
+    typedef __attribute__((address_space(4))) const PipeArgs KernArgs;
+    KernArgs* kp = (KernArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+    int st = kp->pcost ? max((int)kp->pcost[k0], (int)kp->pcost[k1]) : 0;
+    for (int o = 32; o >= 1; o >>= 1) st = max(st, __shfl_xor(st, o));
+    const int gw = (int)(blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6));
+    if (kp->wclock && (threadIdx.x & 63) == 0 && gw < kp->wclock_n) {
+        const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);  // XCC_ID
+        kp->wclock[gw] = make_ulonglong4(tclk0, __builtin_amdgcn_s_memrealtime(), xcc & 15u, (unsigned long long)st);
+    }
+}
 #endif
 template <bool COUNT, bool PRIMARY, bool DEEP, int FUSE>
 __device__ __forceinline__ void trace_compact_body(PipeArgs& A, unsigned char* smem) {
@@ -744,17 +840,59 @@ __device__ __forceinline__ void trace_compact_body(PipeArgs& A, unsigned char* s
     }
     flush_counts<COUNT>(cnt, A.counters);
 #if ORT_TILE_CLOCK && defined(__HIP_DEVICE_COMPILE__)
-    if (PRIMARY && !COUNT) {
+    tile_clock_record<PRIMARY && !COUNT>(k, k, tclk0);
+#endif
+}
+
+// Tile pairs (ORT_OPT_TILE_PAIRS): a workgroup renders the two tiles of pair blockIdx.x, each
+// wave a heavy and then a light 64-slot block (cost_order_pair).  Between the blocks the kernel
+// arguments are re-read through a laundered pointer (hoisted out of the loop they stay live
+// across the walk and spill) and the second block's slot is kept in one VGPR.
+template <bool COUNT, bool PRIMARY, bool DEEP, int FUSE>
+__device__ __forceinline__ void trace_pair_body(PipeArgs& A, unsigned char* smem) {
+#if ORT_TILE_CLOCK && defined(__HIP_DEVICE_COMPILE__)
+    const unsigned long long tclk0 = __builtin_amdgcn_s_memrealtime();
+#endif
+    LdsView L0 = setup_lds<true>(smem, A.S);
+    const int base = blockIdx.x * (2 * kBlock);
+    int kk0 = base + threadIdx.x, kk1 = kk0 + kBlock;
+    if (!COUNT && A.pcost) cost_order_pair<DEEP ? ORT_COST_SHIFT_DEEP : ORT_COST_SHIFT>(A.pcost, L0.fr.co, base, kk0, kk1);
+    ort::Counters cnt;
+    for (int q = 0; q < 6; ++q) cnt.v[q] = 0;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+#if defined(__HIP_DEVICE_COMPILE__)
         typedef __attribute__((address_space(4))) const PipeArgs KernArgs;
         KernArgs* kp = (KernArgs*)__builtin_amdgcn_kernarg_segment_ptr();
-        int st = kp->pcost ? (int)kp->pcost[k] : 0;
-        for (int o = 32; o >= 1; o >>= 1) st = max(st, __shfl_xor(st, o));
-        const int gw = (int)(blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6));
-        if (kp->wclock && (threadIdx.x & 63) == 0 && gw < kp->wclock_n) {
-            const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);  // XCC_ID
-            kp->wclock[gw] = make_ulonglong4(tclk0, __builtin_amdgcn_s_memrealtime(), xcc & 15u, (unsigned long long)st);
+        asm volatile("" : "+s"(kp));
+        PipeArgs A1 = *kp;
+#else
+        PipeArgs& A1 = A;
+#endif
+        LdsView L = lds_view<true>(smem, A1.S.depth);
+        int k = j ? kk1 : kk0;
+#if defined(__HIP_DEVICE_COMPILE__)
+        asm volatile("" : "+v"(k));
+        if (!COUNT && A1.pcost && A1.prio_steps > 0) {  // heavy priority, per block
+            if (__ballot((int)A1.pcost[k] >= A1.prio_steps)) __builtin_amdgcn_s_setprio(3);
+            else __builtin_amdgcn_s_setprio(0);
+        }
+#endif
+        const bool go = trace_slot<COUNT, PRIMARY, DEEP, FUSE, 2>(A1, L, k, cnt);
+        (void)go;
+        if constexpr (FUSE == 2) {  // the paths that go on join the next bounce's list
+#if defined(__HIP_DEVICE_COMPILE__)
+            KernArgs* kq = (KernArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+            uint32_t key = 0;
+            if (go && kq->qnext_keys)
+                key = ort::path_key(kq->po[k], kq->pd[k], kq->mp, kq->key_spread) | light_bit(kq->bcost_r, kq->heavy, k);
+            append_slots(go, k, key, kq->qnext, kq->qnext_keys, kq->qnext_count);
+#endif
         }
     }
+    flush_counts<COUNT>(cnt, A.counters);
+#if ORT_TILE_CLOCK && defined(__HIP_DEVICE_COMPILE__)
+    tile_clock_record<PRIMARY && !COUNT>(kk0, kk1, tclk0);
 #endif
 }
 
@@ -769,6 +907,18 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ORT
 ort_trace_compact_deep(PipeArgs A) {
     extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];  // plane tables: 1 KiB-aligned
     trace_compact_body<COUNT, PRIMARY, true, FUSE>(A, smem);
+}
+// camera rays, tile pairs (ORT_OPT_TILE_PAIRS)
+template <bool COUNT, int FUSE>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ORT_TRACE_WAVES))) ort_trace_pair(PipeArgs A) {
+    extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];  // plane tables: 1 KiB-aligned
+    trace_pair_body<COUNT, true, false, FUSE>(A, smem);
+}
+template <bool COUNT, int FUSE>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ORT_TRACE_WAVES_DEEP)))
+ort_trace_pair_deep(PipeArgs A) {
+    extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];  // plane tables: 1 KiB-aligned
+    trace_pair_body<COUNT, true, true, FUSE>(A, smem);
 }
 // Heavy camera rays (ORT_OPT_SPLIT_HEAVY): the slots whose walk took >= T steps in the previous
 // frame (pcost), listed (the first `cap` of them) and marked in a bitmap the per-tile kernel
@@ -796,7 +946,7 @@ __global__ void __launch_bounds__(kBlock) k_heavy_scan(const uint16_t* pcost, in
 // kernel and ahead of it in the GPU's dispatch, at raised issue priority: the frame's longest
 // walks, run by one lane each, are what a small tile's frame waits for (tools/tile_clock.py).
 constexpr int kSplitLanes = 8;
-template <bool DEEP>
+template <bool DEEP, int FUSE>
 __global__ void __launch_bounds__(kBlock) ort_trace_split(PipeArgs A) {
     extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];  // plane tables: 1 KiB-aligned
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -848,7 +998,18 @@ __global__ void __launch_bounds__(kBlock) ort_trace_split(PipeArgs A) {
         }
         if (walked && j == 0) {
             if (A.pcost) A.pcost[k] = (uint16_t)min(steps, 65535);
-            shade_direct(A, k, ray, rng0, pos != kNoHit, entry, t);
+            if constexpr (FUSE == 1) {
+                shade_direct(A, k, ray, rng0, pos != kNoHit, entry, t);
+            } else {  // bounce 0 of a multi-bounce frame: path state, and the next bounce's list
+                int col, row;
+                (void)slot_coords(A, k, col, row);
+                if (shade_state<0, true, false>(A, k, (size_t)row * A.tm.tw + col, ray, rng0, pos != kNoHit ? entry : -1, t)) {
+                    const int q = atomicAdd(A.qnext_count, 1);
+                    A.qnext[q] = k;
+                    if (A.qnext_keys)
+                        A.qnext_keys[q] = ort::path_key(A.po[k], A.pd[k], A.mp, A.key_spread) | light_bit(A.bcost_r, A.heavy, k);
+                }
+            }
         }
     }
 }
@@ -1057,6 +1218,7 @@ struct ort_ctx {
     static constexpr int kCostBounces = 8;
     int heavy_first = ORT_HEAVY_STEPS;
     int heavy_prio = 0;  // ORT_OPT_HEAVY_PRIO (steps; 0 off)
+    int tile_pairs = 0;  // ORT_OPT_TILE_PAIRS: camera-ray workgroups of two tiles (cost_order_pair)
     // ORT_OPT_SPLIT_HEAVY (steps; 0 off) / ORT_OPT_SPLIT_LEVEL (0: auto): the heavy camera rays of a
     // 1-sample 1-bounce frame walked by ort_trace_split on aux_stream (k_heavy_scan lists them)
     int split_steps = 0;
@@ -1407,6 +1569,19 @@ int ensure(ort_ctx* ctx, DevBuf& b, size_t bytes) {
 
 template <bool COUNT, bool PRIMARY>
 hipError_t launch_trace_p(int mode, const PipeArgs& a, int blocks, int pblocks, size_t lds, hipStream_t s, int fuse) {
+    if (PRIMARY && mode == 0 && a.pair && pblocks == 0) {  // tile pairs: blocks = workgroups (one per pair)
+        const dim3 g(blocks), t(kBlock);
+        if (a.S.depth > 8) {
+            if (fuse == 1) hipLaunchKernelGGL((ort_trace_pair_deep<COUNT, 1>), g, t, lds, s, a);
+            else if (fuse == 2) hipLaunchKernelGGL((ort_trace_pair_deep<COUNT, 2>), g, t, lds, s, a);
+            else hipLaunchKernelGGL((ort_trace_pair_deep<COUNT, 0>), g, t, lds, s, a);
+        } else {
+            if (fuse == 1) hipLaunchKernelGGL((ort_trace_pair<COUNT, 1>), g, t, lds, s, a);
+            else if (fuse == 2) hipLaunchKernelGGL((ort_trace_pair<COUNT, 2>), g, t, lds, s, a);
+            else hipLaunchKernelGGL((ort_trace_pair<COUNT, 0>), g, t, lds, s, a);
+        }
+        return hipGetLastError();
+    }
     if (mode == 0 && pblocks > 0) {
         if (a.S.depth > 8)
             hipLaunchKernelGGL((ort_trace_persistent<COUNT, true>), dim3(pblocks), dim3(kPersistDeepBlock),
@@ -1471,7 +1646,7 @@ int persistent_blocks(int device, bool count, bool deep, int depth, size_t lds, 
 unsigned long long frame_sig(const ort_ctx* ctx, const ort_params* p, const ort_tile* t) {
     const long long v[] = {p->width, p->height, p->num_samples, p->max_depth, t->x0, t->width, t->y0,
                            t->rows, t->band_height, t->band_stride, ctx->n_nodes, ctx->n_spheres,
-                           (long long)ctx->n_indices, ctx->xcd_swizzle};
+                           (long long)ctx->n_indices, ctx->xcd_swizzle, ctx->tile_pairs};
     unsigned long long sig = 1469598103934665603ull;
     for (long long x : v) sig = (sig ^ (unsigned long long)x) * 1099511628211ull;
     return sig;
@@ -1488,7 +1663,11 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     if (!out && pix > 0) return fail(ctx, ORT_ERR_INVALID_ARG, "ort_render: null output");
     if (pix == 0) return ORT_OK;
     const int tilesX = (t->width + 15) / 16, tilesY = (t->rows + 15) / 16;
-    const long long blocks = (long long)tilesX * tilesY;
+    // tile pairs (ORT_OPT_TILE_PAIRS; the compact layout, trees of 4+ levels: cost_order_pair's
+    // scratch): the slot blocks of a pair are consecutive, a last odd column's second tile a hole
+    const bool pairs = mode == 0 && ctx->tile_pairs && ctx->depth >= 4;
+    const int gridX = pairs ? (tilesX + 1) / 2 : tilesX;
+    const long long blocks = (long long)(pairs ? 2 * gridX : tilesX) * tilesY;
     if (blocks * kBlock > 0x7fffffffLL) return fail(ctx, ORT_ERR_INVALID_ARG, "ort_render: tile too large");
     const size_t slots = (size_t)blocks * kBlock;
     HIPCHK(ctx, hipSetDevice(ctx->device));
@@ -1566,10 +1745,11 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     a.pp = pixel_params(p);
     a.S = device_scene(ctx);
     a.tm = {t->x0, t->width, t->y0, t->rows, t->band_height, t->band_stride};
-    a.tilesX = tilesX;
+    a.tilesX = gridX;
+    a.pair = pairs ? 1 : 0;
     a.tilesY = tilesY;
     a.swizzle = ctx->xcd_swizzle;
-    a.xrun_log2 = xcd_run_log2(tilesX);
+    a.xrun_log2 = xcd_run_log2(gridX);
     a.total = (int)slots;
     a.exact_only = ctx->exact_only || !ctx->ordered;
     a.refill = ctx->refill;
@@ -1601,8 +1781,8 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
         a.pcost = (uint16_t*)ctx->pcost.p;
         a.prio_steps = ctx->heavy_prio;
     }
-    // split walks of the heavy camera rays (1 sample, 1 bounce; the production kernels)
-    const bool split = fuse && a.pcost && ctx->split_steps > 0 && !dcounters && ns == 1;
+    // split walks of the heavy camera rays (1 sample; the production kernels, bounce 0)
+    const bool split = (fuse || fuse_first) && a.pcost && ctx->split_steps > 0 && !dcounters && ns == 1;
     if (split) {
         if ((rc = ensure(ctx, ctx->hbits, 4 * (slots / 32 + 1))) || (rc = ensure(ctx, ctx->hlist, 4 * (size_t)ort_ctx::kSplitCap)) ||
             (rc = ensure(ctx, ctx->hsync, 64)))
@@ -1678,7 +1858,7 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                     if (bcost && pb > 0 && b > 0 && hi < nbc) at.bcost_w = bcost + (size_t)hi * slots;
                     if (bcost && fmode == 2 && hi + 1 < nbc && b + 1 < bounces) at.bcost_r = bcost + (size_t)(hi + 1) * slots;
                 }
-                const bool do_split = split && fmode == 1;
+                const bool do_split = split && (fmode == 1 || fmode == 2);
                 if (do_split) {
                     // the heavy rays of this frame (last frame's steps), then their split walks on the
                     // second stream beside the per-tile kernel (which passes over them)
@@ -1690,14 +1870,18 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                     HIPCHK(ctx, hipEventRecord(ctx->ev_scan, s));
                     HIPCHK(ctx, hipStreamWaitEvent(ctx->aux_stream, ctx->ev_scan, 0));
                     const int hblocks = 32;  // 1024 heavy rays in flight; more loop
-                    if (ctx->depth > 8) hipLaunchKernelGGL(ort_trace_split<true>, dim3(hblocks), dim3(kBlock), lds, ctx->aux_stream, at);
-                    else hipLaunchKernelGGL(ort_trace_split<false>, dim3(hblocks), dim3(kBlock), lds, ctx->aux_stream, at);
+                    const dim3 hg(hblocks), ht(kBlock);
+                    if (ctx->depth > 8 && fmode == 1) hipLaunchKernelGGL((ort_trace_split<true, 1>), hg, ht, lds, ctx->aux_stream, at);
+                    else if (ctx->depth > 8) hipLaunchKernelGGL((ort_trace_split<true, 2>), hg, ht, lds, ctx->aux_stream, at);
+                    else if (fmode == 1) hipLaunchKernelGGL((ort_trace_split<false, 1>), hg, ht, lds, ctx->aux_stream, at);
+                    else hipLaunchKernelGGL((ort_trace_split<false, 2>), hg, ht, lds, ctx->aux_stream, at);
                     HIPCHK(ctx, hipGetLastError());
                     HIPCHK(ctx, hipEventRecord(ctx->ev_split, ctx->aux_stream));
                     at.hbits = (const uint32_t*)ctx->hbits.p;
                 }
-                e = dcounters ? launch_trace<true>(mode, prim, at, (int)blocks, pb, lds, s, fmode)
-                              : launch_trace<false>(mode, prim, at, (int)blocks, pb, lds, s, fmode);
+                const int tblocks = (prim && pairs) ? (int)(blocks / 2) : (int)blocks;  // a workgroup per tile pair
+                e = dcounters ? launch_trace<true>(mode, prim, at, tblocks, pb, lds, s, fmode)
+                              : launch_trace<false>(mode, prim, at, tblocks, pb, lds, s, fmode);
                 if (e != hipSuccess) return hip_fail(ctx, e, "trace kernel launch");
                 if (do_split) HIPCHK(ctx, hipStreamWaitEvent(s, ctx->ev_split, 0));  // joined before the exact kernel
                 if (timed) {
@@ -1926,6 +2110,11 @@ int ort_set_option(ort_ctx* ctx, int option, int value) {
     if (option == ORT_OPT_HEAVY_FIRST) {
         if (value < 0 || value > 65535) return fail(ctx, ORT_ERR_INVALID_ARG, "ORT_OPT_HEAVY_FIRST: 0 (off) .. 65535 steps");
         ctx->heavy_first = value;
+        return ORT_OK;
+    }
+    if (option == ORT_OPT_TILE_PAIRS) {
+        if (value < 0 || value > 1) return fail(ctx, ORT_ERR_INVALID_ARG, "ORT_OPT_TILE_PAIRS: 0 or 1");
+        ctx->tile_pairs = value;
         return ORT_OK;
     }
     if (option == ORT_OPT_SPLIT_HEAVY) {

@@ -160,6 +160,11 @@ class Renderer:
         """ORT_OPT_SPLIT_LEVEL: the level of the subtrees a split walk deals (0: depth - 5)."""
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_SPLIT_LEVEL, int(level)))
 
+    def set_tile_pairs(self, on: int):
+        """ORT_OPT_TILE_PAIRS: camera-ray workgroups of two tiles, each wave a heavy and a light 64-pixel
+        block by last frame's walk steps; 0 a tile per workgroup.  Same pixels."""
+        self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_TILE_PAIRS, int(on)))
+
     def set_cost_order(self, on: int):
         """ORT_OPT_COST_ORDER: 1 (default) camera rays dealt to waves by last frame's walk cost; 0 fixed blocks."""
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_COST_ORDER, int(on)))

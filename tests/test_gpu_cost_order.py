@@ -106,8 +106,9 @@ def test_heavy_first_option_range(ort):
         r.set_heavy_first(384)
 
 
-@pytest.mark.parametrize("split,level,prio", [(40, 0, 150), (20, 1, 0), (60, 2, 60), (30, 5, 0)])
-def test_split_heavy_frames_match(ort, oracle, scene_c2, split, level, prio):
+@pytest.mark.parametrize("split,level,prio,md", [(40, 0, 150, 1), (20, 1, 0, 1), (60, 2, 60, 1), (30, 5, 0, 1),
+                                                 (40, 0, 150, 3), (25, 2, 0, 4)])
+def test_split_heavy_frames_match(ort, oracle, scene_c2, split, level, prio, md):
     """Split walks of the heavy camera rays (ORT_OPT_SPLIT_HEAVY: 8 lanes per ray on the second
     stream, subtrees of one level dealt round robin) and heavy-wave priority (ORT_OPT_HEAVY_PRIO):
     low thresholds make many rays heavy (up to the 4096-ray cap, the rest walked by the tiles).
@@ -116,8 +117,8 @@ def test_split_heavy_frames_match(ort, oracle, scene_c2, split, level, prio):
     from octreeraytracer_amd.scene import DEFAULT_YAW
     s, t = scene_c2
     W, H = 960, 540
-    p0 = ort.FrameParams.default_camera(W, H)
-    p1 = ort.FrameParams.default_camera(W, H, yaw=DEFAULT_YAW + 3.0)
+    p0 = ort.FrameParams.default_camera(W, H, max_depth=md)
+    p1 = ort.FrameParams.default_camera(W, H, yaw=DEFAULT_YAW + 3.0, max_depth=md)
     full = ort.Tile(0, W, 0, H)
     band = ort.Tile(0, W, 0, 136, band_height=16, band_stride=128)
     params = [p0, p0, p1, p1, p0, p0, p0]
@@ -153,3 +154,31 @@ def test_split_heavy_deep_tree(ort, oracle):
     for g in got:
         assert_same(g, want[1], "deep split")
     assert_same(got[2][100:116], oracle.render(s, t, p, 0, 100, W, 16), "deep split vs oracle")
+
+
+@pytest.mark.parametrize("ns,md,depth", [(1, 1, 6), (1, 3, 6), (2, 2, 6), (1, 1, 9), (1, 3, 9)])
+def test_tile_pairs_frames_match(ort, oracle, ns, md, depth):
+    """Tile pairs (ORT_OPT_TILE_PAIRS: a camera-ray workgroup renders two tiles, each wave a heavy
+    and a light 64-pixel block by last frame's steps; every kernel of the frame maps slots to
+    pixels through the pair grid): an odd tile count per row (a hole tile), band tiles, a moved
+    camera, several samples and bounces, depth 6 and 9 -- bit-exact vs one tile per workgroup."""
+    from octreeraytracer_amd.scene import DEFAULT_YAW
+    s = ort.random_spheres(10_000 if depth == 6 else 20_000, 42)
+    t = ort.build_octree(s, depth, 0 if depth == 6 else 1)
+    W, H = 720, 400  # 45 tiles per row: the last pair holds a hole
+    p0 = ort.FrameParams.default_camera(W, H, num_samples=ns, max_depth=md)
+    p1 = ort.FrameParams.default_camera(W, H, num_samples=ns, max_depth=md, yaw=DEFAULT_YAW + 3.0)
+    full = ort.Tile(0, W, 0, H)
+    band = ort.Tile(0, W, 0, 104, band_height=16, band_stride=64)
+    params = [p0, p0, p1, p0, p0]
+    tiles = [full, full, full, band, band]
+    got = {}
+    for on in (1, 0):
+        with ort.Renderer(0) as r:
+            r.upload(s, t)
+            r.set_tile_pairs(on)
+            r.set_heavy_prio(100)
+            got[on] = _frames(ort, r, s, t, params, tiles)
+    for i, (a, b) in enumerate(zip(got[1], got[0])):
+        assert_same(a, b, f"frame {i}: tile pairs vs one tile per workgroup")
+    assert_same(got[1][2][200:216], oracle.render(s, t, p1, 0, 200, W, 16), "tile pairs, moved camera vs oracle")
