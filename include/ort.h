@@ -122,22 +122,26 @@ typedef struct ort_scene_info {
                                       >= T, the rest, each class in coherence order -- so the longest
                                       walks start early rather than in the launch's drain tail (same
                                       pixels); 0: coherence order only */
-#define ORT_OPT_HEAVY_PRIO 13      /* T > 0: a wave of the camera-ray trace (cost order on) that holds a ray
-                                      whose walk took >= T steps in the previous frame of the same shape
-                                      runs at raised issue priority (s_setprio), so the frame's longest
-                                      walks do not set its end; 0: off.  Same pixels */
-#define ORT_OPT_SPLIT_HEAVY 14     /* T > 0 (1 sample, 1 bounce, cost order on): the camera rays whose walk
-                                      took >= T steps in the previous frame of the same shape (up to 4096
-                                      a frame) are each walked by 8 lanes that deal the walk's subtrees of
-                                      level ORT_OPT_SPLIT_LEVEL round robin (the first hit = the hit of the
+#define ORT_OPT_HEAVY_PRIO 13      /* T > 0 (default 150): a wave of the camera-ray trace (cost order on)
+                                      that holds a ray whose walk took >= T steps in the previous frame of
+                                      the same shape runs at raised issue priority (s_setprio), so the
+                                      frame's longest walks do not set its end; 0: off.  Same pixels */
+#define ORT_OPT_SPLIT_HEAVY 14     /* T > 0 (1 sample, cost order on): the camera rays whose walk took >= T
+                                      steps in the previous frame of the same shape (up to 4096 a frame)
+                                      are each walked by 8 lanes that deal the walk's subtrees of level
+                                      ORT_OPT_SPLIT_LEVEL round robin (the first hit = the hit of the
                                       lowest such subtree in the walk's order), on a second stream beside
                                       the per-tile kernel: a small tile's frame no longer waits for its
-                                      longest walks.  0: off.  Same pixels */
+                                      longest walks.  0: off.  -1 (default): T = 200 on tiles of at most
+                                      2^21 pixels, off on larger ones (where the second stream costs more
+                                      than the tail it cuts).  Same pixels */
 #define ORT_OPT_SPLIT_LEVEL 15     /* the level of those subtrees: 0 (default) = tree depth - 5 (at least 1) */
 #define ORT_OPT_TILE_PAIRS 16      /* 1: a camera-ray workgroup renders two 16x16 tiles side by side, its 512
                                       pixels dealt to 8 blocks of 64 by last frame's walk steps and each
                                       wave walking a heavy and a light block (a workgroup keeps its LDS
-                                      until its slowest wave ends); 0: a tile per workgroup.  Same pixels */
+                                      until its slowest wave ends); 0: a tile per workgroup; -1 (default):
+                                      pairs on tiles of at least 2^22 pixels (on small tiles the fewer,
+                                      longer workgroups lengthen the frame's tail).  Same pixels */
 
 /* Traffic counters (ort_count_traffic), in the REFERENCE layout's terms. */
 #define ORT_COUNT_NODES_POPPED 0

@@ -302,6 +302,12 @@ __device__ inline ort::Ray load_ray(const PipeArgs& A, int k, bool& alive) {
 #ifndef ORT_PERSIST_CLOCK
 #define ORT_PERSIST_CLOCK 0
 #endif
+// Analysis builds only (-DORT_PERSIST_STATS=1, tools/persist_stats.py): per wave of the persistent
+// kernel, how its loop iterations went -- refills, steps, and how many lanes stepped an internal
+// node or a leaf (the two blocks of a step run one after the other, each with its own lanes).
+#ifndef ORT_PERSIST_STATS
+#define ORT_PERSIST_STATS 0
+#endif
 #ifndef ORT_CHUNK
 #define ORT_CHUNK 64
 #endif
@@ -348,11 +354,21 @@ ort_trace_persistent(PipeArgs A) {
     unsigned long long clk_drain = 0;
     int n_items = 0;
 #endif
+#if ORT_PERSIST_STATS
+    unsigned long long ps[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // iterations, refills, steps, internal lanes,
+                                                            // leaf lanes, steps with internal / leaf / both
+#endif
     for (;;) {
         const unsigned long long idle = __ballot(k < 0);
         const int n_idle = __popcll(idle);
         if (n_idle == 64 && drained) break;
+#if ORT_PERSIST_STATS
+        ps[0] += 1;
+#endif
         if (!drained && n_idle >= A.refill) {
+#if ORT_PERSIST_STATS
+            ps[1] += 1;
+#endif
             if (next == end) {
                 int base = 0;
                 if (lane == 0) base = atomicAdd(A.sync + 1, chunk);
@@ -393,6 +409,19 @@ ort_trace_persistent(PipeArgs A) {
             next += take;
             continue;
         }
+#if ORT_PERSIST_STATS
+        {
+            const bool in = k >= 0 && (st.rec.y & ORT_INTERNAL_FLAG);
+            const bool lf = k >= 0 && !(st.rec.y & ORT_INTERNAL_FLAG);
+            const int ni = __popcll(__ballot(in)), nl = __popcll(__ballot(lf));
+            ps[2] += 1;
+            ps[3] += ni;
+            ps[4] += nl;
+            ps[5] += ni > 0;
+            ps[6] += nl > 0;
+            ps[7] += (ni > 0 && nl > 0);
+        }
+#endif
         if (k >= 0) {
             ++nst;
             if (ort::fast_step<COUNT>(A.S, lut, st, L.fr, cnt)) {
@@ -408,6 +437,15 @@ ort_trace_persistent(PipeArgs A) {
         const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);  // XCC_ID
         A.wclock[gw] = make_ulonglong4(clk0, clk_drain, __builtin_amdgcn_s_memrealtime(),
                                        (unsigned long long)(xcc & 15u) | ((unsigned long long)n_items << 8));
+    }
+#endif
+#if ORT_PERSIST_STATS
+    {
+        const int gw = (int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+        if (A.wclock && lane == 0 && 2 * gw + 1 < A.wclock_n) {
+            A.wclock[2 * gw] = make_ulonglong4(ps[0], ps[1], ps[2], ps[3]);
+            A.wclock[2 * gw + 1] = make_ulonglong4(ps[4], ps[5], ps[6], ps[7]);
+        }
     }
 #endif
     flush_counts<COUNT>(cnt, A.counters);
@@ -952,6 +990,10 @@ __global__ void __launch_bounds__(kBlock) ort_trace_split(PipeArgs A) {
 #if defined(__HIP_DEVICE_COMPILE__)
     __builtin_amdgcn_s_setprio(3);
 #endif
+#if ORT_TILE_CLOCK && defined(__HIP_DEVICE_COMPILE__)
+    const unsigned long long sclk0 = __builtin_amdgcn_s_memrealtime();
+    int sitems = 0;
+#endif
     const int count = min(A.hsync[0], A.hcap);
     if (count == 0) return;
     LdsView L = setup_lds<true>(smem, A.S);
@@ -965,6 +1007,9 @@ __global__ void __launch_bounds__(kBlock) ort_trace_split(PipeArgs A) {
         if (base >= count) break;
         const int idx = base + g;
         const int k = idx < count ? A.hlist[idx] : -1;
+#if ORT_TILE_CLOCK && defined(__HIP_DEVICE_COMPILE__)
+        sitems += min(64 / kSplitLanes, count - base);
+#endif
         int pos = kNoHit, entry = -1, steps = 0;
         float t = 0.0f;
         bool walked = false;
@@ -1012,6 +1057,14 @@ __global__ void __launch_bounds__(kBlock) ort_trace_split(PipeArgs A) {
             }
         }
     }
+#if ORT_TILE_CLOCK && defined(__HIP_DEVICE_COMPILE__)
+    {   // analysis: per wave {start, end, 1 << 63 (a split-kernel record), rays walked}, from the records' end
+        const int gw = (int)(blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6));
+        if (A.wclock && (threadIdx.x & 63) == 0 && gw < A.wclock_n)
+            A.wclock[A.wclock_n - 1 - gw] =
+                make_ulonglong4(sclk0, __builtin_amdgcn_s_memrealtime(), 1ull << 63, (unsigned long long)sitems);
+    }
+#endif
 }
 
 // One-ray-per-lane trace for the explicit layout (MODE 1) and brute force (MODE 2).
@@ -1167,6 +1220,14 @@ struct DevBuf {
 #ifndef ORT_HEAVY_STEPS
 #define ORT_HEAVY_STEPS 64  // ORT_OPT_HEAVY_FIRST default: classes >= 256, >= 128, >= 64 steps
 #endif
+// Camera-ray defaults, measured with tools/ab_stream.py: a raised issue priority
+// for waves holding a >= 150-step walk (C3 1/8 band +15 %, full frame +-0); split walks of the
+// >= 200-step rays on small tiles only (1/8 band +20 %, full frame -2 %); tile pairs on large
+// tiles only (full frame +2 %, 1/8 band -22 %).
+constexpr int kHeavyPrioSteps = 150;
+constexpr int kSplitAutoSteps = 200;
+constexpr long long kSplitAutoPixels = 1ll << 21;
+constexpr long long kPairsAutoPixels = 1ll << 22;
 struct ort_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -1217,16 +1278,19 @@ struct ort_ctx {
     // first kCostBounces of a frame, every slot's last walk steps (cleared with cost_sig)
     static constexpr int kCostBounces = 8;
     int heavy_first = ORT_HEAVY_STEPS;
-    int heavy_prio = 0;  // ORT_OPT_HEAVY_PRIO (steps; 0 off)
-    int tile_pairs = 0;  // ORT_OPT_TILE_PAIRS: camera-ray workgroups of two tiles (cost_order_pair)
-    // ORT_OPT_SPLIT_HEAVY (steps; 0 off) / ORT_OPT_SPLIT_LEVEL (0: auto): the heavy camera rays of a
-    // 1-sample 1-bounce frame walked by ort_trace_split on aux_stream (k_heavy_scan lists them)
-    int split_steps = 0;
+    int heavy_prio = kHeavyPrioSteps;  // ORT_OPT_HEAVY_PRIO (steps; 0 off)
+    // ORT_OPT_TILE_PAIRS: camera-ray workgroups of two tiles (cost_order_pair); -1 = auto (tiles
+    // of at least kPairsAutoPixels)
+    int tile_pairs = -1;
+    // ORT_OPT_SPLIT_HEAVY (steps; 0 off; -1 = auto: kSplitAutoSteps on tiles of at most
+    // kSplitAutoPixels) / ORT_OPT_SPLIT_LEVEL (0: auto): the heavy camera rays of a 1-sample
+    // frame walked by ort_trace_split on aux_stream (k_heavy_scan lists them)
+    int split_steps = -1;
     int split_level = 0;
     static constexpr int kSplitCap = 4096;  // heavy rays listed per frame at most
     hipStream_t aux_stream = nullptr;
     hipEvent_t ev_scan = nullptr, ev_split = nullptr;
-    DevBuf hbits, hlist, hsync;
+    DevBuf hbits, hlist;
     DevBuf bcost;
     unsigned long long bcost_sig = 0;
     float root_lo[3] = {0, 0, 0}, root_hi[3] = {0, 0, 0};  // root box (coherence-sort key)
@@ -1665,7 +1729,8 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     const int tilesX = (t->width + 15) / 16, tilesY = (t->rows + 15) / 16;
     // tile pairs (ORT_OPT_TILE_PAIRS; the compact layout, trees of 4+ levels: cost_order_pair's
     // scratch): the slot blocks of a pair are consecutive, a last odd column's second tile a hole
-    const bool pairs = mode == 0 && ctx->tile_pairs && ctx->depth >= 4;
+    const bool pairs = mode == 0 && ctx->depth >= 4 &&
+                       (ctx->tile_pairs > 0 || (ctx->tile_pairs < 0 && (long long)pix >= kPairsAutoPixels));
     const int gridX = pairs ? (tilesX + 1) / 2 : tilesX;
     const long long blocks = (long long)(pairs ? 2 * gridX : tilesX) * tilesY;
     if (blocks * kBlock > 0x7fffffffLL) return fail(ctx, ORT_ERR_INVALID_ARG, "ort_render: tile too large");
@@ -1782,12 +1847,13 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
         a.prio_steps = ctx->heavy_prio;
     }
     // split walks of the heavy camera rays (1 sample; the production kernels, bounce 0)
-    const bool split = (fuse || fuse_first) && a.pcost && ctx->split_steps > 0 && !dcounters && ns == 1;
+    const int split_steps = ctx->split_steps >= 0 ? ctx->split_steps
+                                                  : ((long long)pix <= kSplitAutoPixels ? kSplitAutoSteps : 0);
+    const bool split = (fuse || fuse_first) && a.pcost && split_steps > 0 && !dcounters && ns == 1;
     if (split) {
-        if ((rc = ensure(ctx, ctx->hbits, 4 * (slots / 32 + 1))) || (rc = ensure(ctx, ctx->hlist, 4 * (size_t)ort_ctx::kSplitCap)) ||
-            (rc = ensure(ctx, ctx->hsync, 64)))
+        if ((rc = ensure(ctx, ctx->hbits, 4 * (slots / 32 + 1))) || (rc = ensure(ctx, ctx->hlist, 4 * (size_t)ort_ctx::kSplitCap)))
             return rc;
-        a.hsync = (int*)ctx->hsync.p;
+        a.hsync = (int*)ctx->defer_count.p + 8;  // zeroed with the deferred-ray count, one memset per bounce
         a.hlist = (const int*)ctx->hlist.p;
         a.hcap = ort_ctx::kSplitCap;
         // the subtrees dealt to the lanes: ~5 levels above the leaves (a depth-8 tree: level 3)
@@ -1810,7 +1876,9 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     const size_t lds = lds_bytes(mode, ctx->depth, false);
     const size_t lds_exact = lds_bytes(mode, ctx->depth, true);
     const int pblocks = (mode == 0 && ctx->persistent) ? persistent_blocks(ctx->device, dcounters != nullptr, ctx->depth > 8, ctx->depth, lds, blocks) : 0;
-    const int exact_blocks = 1024;
+    // the exact kernel: a grid-stride loop over the (usually no) deferred rays; a small grid
+    // dispatches fast
+    const int exact_blocks = 256;
     hipError_t e;
     HIPCHK(ctx, hipEventRecord(ctx->ev0, s));
     const int fslot = (int)(ctx->frames % ort_ctx::kRing);  // this frame's timing slot
@@ -1843,7 +1911,8 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                 const int pb = (pers_bounce && b > 0) ? pblocks : 0;
                 PipeArgs at = a;
                 if (pb > 0 && a.wclock) {  // analysis (ORT_PERSIST_CLOCK): a record range per launch
-                    const long long nw = (long long)pb * (ctx->depth > 8 ? kPersistDeepBlock : kBlock) / 64;
+                    const long long nw = (long long)pb * (ctx->depth > 8 ? kPersistDeepBlock : kBlock) / 64 *
+                                         (ORT_PERSIST_STATS ? 2 : 1);  // records per launch
                     at.wclock = (seg + 1) * nw <= ctx->wclock_n ? a.wclock + seg * nw : nullptr;
                     at.wclock_n = (int)nw;
                 }
@@ -1862,10 +1931,9 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                 if (do_split) {
                     // the heavy rays of this frame (last frame's steps), then their split walks on the
                     // second stream beside the per-tile kernel (which passes over them)
-                    HIPCHK(ctx, hipMemsetAsync(ctx->hsync.p, 0, 8, s));
                     hipLaunchKernelGGL(k_heavy_scan, dim3((unsigned)blocks), dim3(kBlock), 0, s, (const uint16_t*)a.pcost,
-                                       (int)slots, ctx->split_steps, ort_ctx::kSplitCap, (uint32_t*)ctx->hbits.p,
-                                       (int*)ctx->hlist.p, (int*)ctx->hsync.p);
+                                       (int)slots, split_steps, ort_ctx::kSplitCap, (uint32_t*)ctx->hbits.p,
+                                       (int*)ctx->hlist.p, a.hsync);
                     HIPCHK(ctx, hipGetLastError());
                     HIPCHK(ctx, hipEventRecord(ctx->ev_scan, s));
                     HIPCHK(ctx, hipStreamWaitEvent(ctx->aux_stream, ctx->ev_scan, 0));
@@ -2051,7 +2119,7 @@ int ort_destroy(ort_ctx* ctx) {
     free_buf(ctx->counters);
     DevBuf* pipe[] = {&ctx->hit, &ctx->defer_list, &ctx->defer_count, &ctx->po, &ctx->pd, &ctx->pc, &ctx->prng, &ctx->pcol,
                       &ctx->qlist, &ctx->qlist2, &ctx->qcount, &ctx->qtemp, &ctx->skeys, &ctx->skeys2, &ctx->svals, &ctx->key_spread,
-                      &ctx->pcost, &ctx->bcost, &ctx->hbits, &ctx->hlist, &ctx->hsync};
+                      &ctx->pcost, &ctx->bcost, &ctx->hbits, &ctx->hlist};
     for (DevBuf* b : pipe) free_buf(*b);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
@@ -2113,12 +2181,12 @@ int ort_set_option(ort_ctx* ctx, int option, int value) {
         return ORT_OK;
     }
     if (option == ORT_OPT_TILE_PAIRS) {
-        if (value < 0 || value > 1) return fail(ctx, ORT_ERR_INVALID_ARG, "ORT_OPT_TILE_PAIRS: 0 or 1");
+        if (value < -1 || value > 1) return fail(ctx, ORT_ERR_INVALID_ARG, "ORT_OPT_TILE_PAIRS: -1 (auto), 0 or 1");
         ctx->tile_pairs = value;
         return ORT_OK;
     }
     if (option == ORT_OPT_SPLIT_HEAVY) {
-        if (value < 0 || value > 65535) return fail(ctx, ORT_ERR_INVALID_ARG, "ORT_OPT_SPLIT_HEAVY: 0 (off) .. 65535 steps");
+        if (value < -1 || value > 65535) return fail(ctx, ORT_ERR_INVALID_ARG, "ORT_OPT_SPLIT_HEAVY: -1 (auto), 0 (off) .. 65535 steps");
         ctx->split_steps = value;
         return ORT_OK;
     }

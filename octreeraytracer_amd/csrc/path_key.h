@@ -24,6 +24,12 @@ constexpr int kMortonBits = ORT_MORTON_BITS;
 #endif
 constexpr int kDirBits = ORT_DIR_BITS;
 constexpr int kPathKeyBits = 3 + kMortonBits + 3 * kDirBits;  // 30: alive keys < 2^30, dead = 0xffffffff
+// origin-code bits above the direction bits (the rest below them): kMortonBits = origin first
+#ifndef ORT_KEY_ORIGIN_HI
+#define ORT_KEY_ORIGIN_HI ORT_MORTON_BITS
+#endif
+constexpr int kOriginHi = ORT_KEY_ORIGIN_HI, kOriginLo = kMortonBits - kOriginHi;
+static_assert(kOriginHi >= 0 && kOriginLo >= 0, "ORT_KEY_ORIGIN_HI: 0 .. ORT_MORTON_BITS");
 static_assert(kPathKeyBits <= 30, "the heavy-first class sits above the key");
 
 struct MortonPlan {
@@ -96,7 +102,8 @@ __device__ __forceinline__ uint32_t path_key(const float4 o, const float4 d, con
         const uint32_t* t = spread + a * 768;
         code |= t[q & 255u] | t[256 + ((q >> 8) & 255u)] | t[512 + (q >> 16)];
     }
-    return (m << (3 * kDirBits + kMortonBits)) | (code << (3 * kDirBits)) | dq;
+    const uint32_t lo = code & ((1u << kOriginLo) - 1u);
+    return (m << (3 * kDirBits + kMortonBits)) | ((code >> kOriginLo) << (3 * kDirBits + kOriginLo)) | (dq << kOriginLo) | lo;
 }
 
 }  // namespace ort

@@ -148,12 +148,13 @@ class Renderer:
 
     def set_heavy_prio(self, steps: int):
         """ORT_OPT_HEAVY_PRIO: camera-ray waves holding a walk of >= steps (last frame) run at raised
-        issue priority; 0 off.  Same pixels."""
+        issue priority; 0 off (default 150).  Same pixels."""
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_HEAVY_PRIO, int(steps)))
 
     def set_split_heavy(self, steps: int):
         """ORT_OPT_SPLIT_HEAVY: camera rays whose walk took >= steps (last frame) are walked by 8 lanes
-        each, their subtrees dealt round robin, beside the per-tile kernel; 0 off.  Same pixels."""
+        each, their subtrees dealt round robin, beside the per-tile kernel; 0 off; -1 (default) 200 on
+        tiles of at most 2^21 pixels, off on larger ones.  Same pixels."""
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_SPLIT_HEAVY, int(steps)))
 
     def set_split_level(self, level: int):
@@ -162,7 +163,8 @@ class Renderer:
 
     def set_tile_pairs(self, on: int):
         """ORT_OPT_TILE_PAIRS: camera-ray workgroups of two tiles, each wave a heavy and a light 64-pixel
-        block by last frame's walk steps; 0 a tile per workgroup.  Same pixels."""
+        block by last frame's walk steps; 0 a tile per workgroup; -1 (default) pairs on tiles of at least
+        2^22 pixels.  Same pixels."""
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_TILE_PAIRS, int(on)))
 
     def set_cost_order(self, on: int):

@@ -35,7 +35,7 @@ p = ort.FrameParams.default_camera(W, H, num_samples=NS, max_depth=MD)
 out = torch.empty((tile.rows, W, 3), dtype=torch.float32, device="cuda")
 st = torch.cuda.Stream()
 torch.cuda.set_stream(st)
-nw = ((W + 15) // 16) * ((tile.rows + 15) // 16) * 4
+nw = ((W + 15) // 16) * ((tile.rows + 15) // 16) * 4 + 1024  # + ort_trace_split's records at the end
 buf = torch.zeros((nw, 4), dtype=torch.int64, device="cuda")
 f = lib.ort_debug_wave_clock
 f.restype = C.c_int
@@ -50,6 +50,14 @@ for fr in range(frames):
     torch.cuda.synchronize()
     assert f(r._ctx, None, 0) == 0
     rec = buf.cpu().numpy().astype(np.int64)
+    sp = rec[:, 2] < 0  # ort_trace_split's records (bit 63 set), written from the end
+    if sp.any():
+        S = rec[sp]
+        sbase = rec[(rec[:, 1] > 0)][:, 0].min()
+        print(f"  split kernel: {len(S)} waves, {int(S[:, 3].sum())} rays, starts {(S[:, 0].min() - sbase) / 100:.0f} us, "
+              f"ends max {(S[:, 1].max() - sbase) / 100:.0f} us (wave us max {(S[:, 1] - S[:, 0]).max() / 100:.0f})",
+              flush=True)
+    rec[sp] = 0
     ok = rec[:, 1] > 0
     if not ok.any():
         raise SystemExit("no records: is this an ORT_TILE_CLOCK=1 build?")
