@@ -142,6 +142,10 @@ typedef struct ort_scene_info {
                                       until its slowest wave ends); 0: a tile per workgroup; -1 (default):
                                       pairs on tiles of at least 2^22 pixels (on small tiles the fewer,
                                       longer workgroups lengthen the frame's tail).  Same pixels */
+#define ORT_OPT_TILE_LPT 17        /* 1 (1 sample, cost order on, a tile per workgroup): the camera-ray
+                                      workgroups of each XCD start in longest-first order of their tile's
+                                      longest walk in the previous frame of the same shape (a pre-pass
+                                      kernel deals the order); 0 (default): tile order.  Same pixels */
 
 /* Traffic counters (ort_count_traffic), in the REFERENCE layout's terms. */
 #define ORT_COUNT_NODES_POPPED 0

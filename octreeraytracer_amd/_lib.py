@@ -38,6 +38,7 @@ ORT_OPT_HEAVY_PRIO = 13
 ORT_OPT_SPLIT_HEAVY = 14
 ORT_OPT_SPLIT_LEVEL = 15
 ORT_OPT_TILE_PAIRS = 16
+ORT_OPT_TILE_LPT = 17
 ORT_LAYOUT_COMPACT_EXACT_EMULATION = 2
 ORT_COUNT_N = 6
 COUNT_NAMES = ("nodes_popped", "child_records", "leaf_objects", "accepted_hits", "pixels", "traversals")

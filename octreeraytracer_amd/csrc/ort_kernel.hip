@@ -88,6 +88,9 @@ struct PipeArgs {
     int* hsync;       // [0] heavy rays found (the list holds the first hcap), [1] ort_trace_split's cursor
     int hcap;
     int split_level;
+    // ORT_OPT_TILE_LPT: workgroup w of the per-tile camera kernel renders tile block border[w]
+    // (k_heavy_scan's order: each XCD's blocks by last frame's longest walk, longest first)
+    const int* border;
     ulonglong4* wclock;  // analysis builds only (ORT_PERSIST_CLOCK, ort_debug_wave_clock): per wave a timeline record
     int wclock_n;
 };
@@ -851,7 +854,7 @@ __device__ __forceinline__ void trace_compact_body(PipeArgs& A, unsigned char* s
     const unsigned long long tclk0 = __builtin_amdgcn_s_memrealtime();
 #endif
     LdsView L = setup_lds<true>(smem, A.S);
-    int k = blockIdx.x * kBlock + threadIdx.x;
+    int k = ((PRIMARY && A.border) ? A.border[blockIdx.x] : (int)blockIdx.x) * kBlock + threadIdx.x;
     if (PRIMARY && !COUNT && A.pcost) {  // (the counting pass: tile order)
         k = cost_order_slot<DEEP ? ORT_COST_SHIFT_DEEP : ORT_COST_SHIFT>(A.pcost, L.fr.co, k);
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -961,21 +964,72 @@ ort_trace_pair_deep(PipeArgs A) {
 // Heavy camera rays (ORT_OPT_SPLIT_HEAVY): the slots whose walk took >= T steps in the previous
 // frame (pcost), listed (the first `cap` of them) and marked in a bitmap the per-tile kernel
 // reads.  A wave's slots are listed in slot order after one atomic.
+//
+// With `order` (ORT_OPT_TILE_LPT; workgroup b = tile block b): each workgroup also records its
+// block's longest walk (the split ones aside) and the last workgroup to finish deals the blocks
+// of each XCD (block b runs on XCD b % 8) in longest-first order -- longest-processing-time
+// scheduling of the per-tile kernel's workgroups, which the GPU dispatches in index order.
+constexpr int kLptBuckets = 256;  // bucket = min(steps >> 1, 255)
 __global__ void __launch_bounds__(kBlock) k_heavy_scan(const uint16_t* pcost, int n, int T, int cap, uint32_t* bits,
-                                                       int* list, int* count) {
+                                                       int* list, int* count, uint32_t* bmax, int* order) {
     const int k = blockIdx.x * kBlock + threadIdx.x;
     const int lane = threadIdx.x & 63;
-    const bool h0 = k < n && (int)pcost[k] >= T;
-    const unsigned long long m = __ballot(h0);
-    int base = 0;
-    if (lane == 0 && m) base = atomicAdd(count, __popcll(m));
-    base = __shfl(base, 0);
-    const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    const int pos = base + __popcll(m & below);
-    const bool h = h0 && pos < cap;  // past the cap the per-tile kernel walks them itself
-    if (h) list[pos] = k;
-    const unsigned long long mh = __ballot(h);
-    if (k < n && (lane & 31) == 0) bits[k >> 5] = (uint32_t)(mh >> (lane & 32));
+    const int c = k < n ? (int)pcost[k] : 0;
+    if (bits) {
+        const bool h0 = k < n && c >= T;
+        const unsigned long long m = __ballot(h0);
+        int base = 0;
+        if (lane == 0 && m) base = atomicAdd(count, __popcll(m));
+        base = __shfl(base, 0);
+        const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+        const int pos = base + __popcll(m & below);
+        const bool h = h0 && pos < cap;  // past the cap the per-tile kernel walks them itself
+        if (h) list[pos] = k;
+        const unsigned long long mh = __ballot(h);
+        if (k < n && (lane & 31) == 0) bits[k >> 5] = (uint32_t)(mh >> (lane & 32));
+    }
+    if (!order) return;
+    __shared__ int wmax[kBlock / 64];
+    __shared__ int last;
+    __shared__ int hist[8 * kLptBuckets];
+    int v = (bits && c >= T) ? 0 : c;  // (a capped heavy ray is walked here after all: approximate)
+    for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o));
+    if (lane == 0) wmax[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int bm = wmax[0];
+        for (int w = 1; w < kBlock / 64; ++w) bm = max(bm, wmax[w]);
+        __hip_atomic_store(bmax + blockIdx.x, (uint32_t)bm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __threadfence();
+        last = atomicAdd(count + 2, 1) == (int)gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    const int nb = (int)gridDim.x;
+    for (int i = threadIdx.x; i < 8 * kLptBuckets; i += kBlock) hist[i] = 0;
+    __syncthreads();
+    for (int b = threadIdx.x; b < nb; b += kBlock) {
+        const uint32_t bm = __hip_atomic_load(bmax + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        atomicAdd(&hist[(b & 7) * kLptBuckets + (kLptBuckets - 1 - (int)min(bm >> 1, (uint32_t)kLptBuckets - 1))], 1);
+    }
+    __syncthreads();
+    if (threadIdx.x < 8) {  // exclusive scan per XCD class (8 x 256 buckets: serial, tiny)
+        int* h = hist + threadIdx.x * kLptBuckets;
+        int run = 0;
+        for (int i = 0; i < kLptBuckets; ++i) {
+            const int t = h[i];
+            h[i] = run;
+            run += t;
+        }
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < nb; b += kBlock) {
+        const uint32_t bm = __hip_atomic_load(bmax + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int x = b & 7;
+        const int pos = atomicAdd(&hist[x * kLptBuckets + (kLptBuckets - 1 - (int)min(bm >> 1, (uint32_t)kLptBuckets - 1))], 1);
+        order[x + 8 * pos] = b;  // the pos-th longest block of class x (any order within a bucket)
+    }
 }
 
 // The heavy camera rays of k_heavy_scan's list, each walked by a group of 8 lanes that deal its
@@ -1291,6 +1345,8 @@ struct ort_ctx {
     hipStream_t aux_stream = nullptr;
     hipEvent_t ev_scan = nullptr, ev_split = nullptr;
     DevBuf hbits, hlist;
+    int tile_lpt = 0;     // ORT_OPT_TILE_LPT
+    DevBuf bmax, border;  // its per-block longest walks and the workgroup -> block order
     DevBuf bcost;
     unsigned long long bcost_sig = 0;
     float root_lo[3] = {0, 0, 0}, root_hi[3] = {0, 0, 0};  // root box (coherence-sort key)
@@ -1859,6 +1915,10 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
         // the subtrees dealt to the lanes: ~5 levels above the leaves (a depth-8 tree: level 3)
         a.split_level = ctx->split_level > 0 ? ctx->split_level : std::max(1, ctx->depth - 5);
     }
+    // longest-first workgroup order (ORT_OPT_TILE_LPT; a tile per workgroup)
+    const bool lpt = (fuse || fuse_first) && a.pcost && ctx->tile_lpt && !pairs && !dcounters && ns == 1;
+    if (lpt && ((rc = ensure(ctx, ctx->bmax, 4 * (size_t)blocks)) || (rc = ensure(ctx, ctx->border, 4 * (size_t)blocks))))
+        return rc;
     // heavy first: the bounce >= 1 lists of the persistent trace (sorted, default path)
     const int nbc = std::min(ns * (maxd > 0 ? maxd : 1), ort_ctx::kCostBounces);  // recorded bounce indices
     uint16_t* bcost = nullptr;
@@ -1928,12 +1988,21 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                     if (bcost && fmode == 2 && hi + 1 < nbc && b + 1 < bounces) at.bcost_r = bcost + (size_t)(hi + 1) * slots;
                 }
                 const bool do_split = split && (fmode == 1 || fmode == 2);
+                const bool do_lpt = lpt && (fmode == 1 || fmode == 2);
+                if (do_lpt && !do_split) {
+                    hipLaunchKernelGGL(k_heavy_scan, dim3((unsigned)blocks), dim3(kBlock), 0, s, (const uint16_t*)a.pcost,
+                                       (int)slots, 0, 0, nullptr, nullptr, (int*)ctx->defer_count.p + 8,
+                                       (uint32_t*)ctx->bmax.p, (int*)ctx->border.p);
+                    HIPCHK(ctx, hipGetLastError());
+                }
+                if (do_lpt) at.border = (const int*)ctx->border.p;
                 if (do_split) {
                     // the heavy rays of this frame (last frame's steps), then their split walks on the
                     // second stream beside the per-tile kernel (which passes over them)
                     hipLaunchKernelGGL(k_heavy_scan, dim3((unsigned)blocks), dim3(kBlock), 0, s, (const uint16_t*)a.pcost,
                                        (int)slots, split_steps, ort_ctx::kSplitCap, (uint32_t*)ctx->hbits.p,
-                                       (int*)ctx->hlist.p, a.hsync);
+                                       (int*)ctx->hlist.p, a.hsync, do_lpt ? (uint32_t*)ctx->bmax.p : nullptr,
+                                       do_lpt ? (int*)ctx->border.p : nullptr);
                     HIPCHK(ctx, hipGetLastError());
                     HIPCHK(ctx, hipEventRecord(ctx->ev_scan, s));
                     HIPCHK(ctx, hipStreamWaitEvent(ctx->aux_stream, ctx->ev_scan, 0));
@@ -2119,7 +2188,7 @@ int ort_destroy(ort_ctx* ctx) {
     free_buf(ctx->counters);
     DevBuf* pipe[] = {&ctx->hit, &ctx->defer_list, &ctx->defer_count, &ctx->po, &ctx->pd, &ctx->pc, &ctx->prng, &ctx->pcol,
                       &ctx->qlist, &ctx->qlist2, &ctx->qcount, &ctx->qtemp, &ctx->skeys, &ctx->skeys2, &ctx->svals, &ctx->key_spread,
-                      &ctx->pcost, &ctx->bcost, &ctx->hbits, &ctx->hlist};
+                      &ctx->pcost, &ctx->bcost, &ctx->hbits, &ctx->hlist, &ctx->bmax, &ctx->border};
     for (DevBuf* b : pipe) free_buf(*b);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
@@ -2193,6 +2262,11 @@ int ort_set_option(ort_ctx* ctx, int option, int value) {
     if (option == ORT_OPT_SPLIT_LEVEL) {
         if (value < 0 || value > ORT_COMPACT_MAX_DEPTH) return fail(ctx, ORT_ERR_INVALID_ARG, "ORT_OPT_SPLIT_LEVEL: 0 (auto) .. 10");
         ctx->split_level = value;
+        return ORT_OK;
+    }
+    if (option == ORT_OPT_TILE_LPT) {
+        if (value < 0 || value > 1) return fail(ctx, ORT_ERR_INVALID_ARG, "ORT_OPT_TILE_LPT: 0 or 1");
+        ctx->tile_lpt = value;
         return ORT_OK;
     }
     if (option == ORT_OPT_HEAVY_PRIO) {

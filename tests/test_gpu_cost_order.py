@@ -106,6 +106,15 @@ def test_heavy_first_option_range(ort):
         r.set_heavy_first(384)
 
 
+def _plain(r):
+    """The per-tile kernel alone: no heavy priority, split walks, tile pairs or longest-first order
+    (the defaults turn some of them on by tile size)."""
+    r.set_heavy_prio(0)
+    r.set_split_heavy(0)
+    r.set_tile_pairs(0)
+    r.set_tile_lpt(0)
+
+
 @pytest.mark.parametrize("split,level,prio,md", [(40, 0, 150, 1), (20, 1, 0, 1), (60, 2, 60, 1), (30, 5, 0, 1),
                                                  (40, 0, 150, 3), (25, 2, 0, 4)])
 def test_split_heavy_frames_match(ort, oracle, scene_c2, split, level, prio, md):
@@ -125,6 +134,7 @@ def test_split_heavy_frames_match(ort, oracle, scene_c2, split, level, prio, md)
     tiles = [full, full, full, full, band, band, full]
     with ort.Renderer(0) as r:
         r.upload(s, t)
+        _plain(r)
         want = _frames(ort, r, s, t, params, tiles)
     with ort.Renderer(0) as r:
         r.upload(s, t)
@@ -146,6 +156,7 @@ def test_split_heavy_deep_tree(ort, oracle):
     p = ort.FrameParams.default_camera(W, H)
     with ort.Renderer(0) as r:
         r.upload(s, t)
+        _plain(r)
         want = [r.render(p) for _ in range(2)]
     with ort.Renderer(0) as r:
         r.upload(s, t)
@@ -182,3 +193,34 @@ def test_tile_pairs_frames_match(ort, oracle, ns, md, depth):
     for i, (a, b) in enumerate(zip(got[1], got[0])):
         assert_same(a, b, f"frame {i}: tile pairs vs one tile per workgroup")
     assert_same(got[1][2][200:216], oracle.render(s, t, p1, 0, 200, W, 16), "tile pairs, moved camera vs oracle")
+
+
+@pytest.mark.parametrize("split,md,depth", [(0, 1, 6), (200, 1, 6), (30, 1, 6), (30, 3, 6), (0, 1, 9), (40, 2, 9)])
+def test_tile_lpt_frames_match(ort, oracle, split, md, depth):
+    """Longest-first workgroup order (ORT_OPT_TILE_LPT: a pre-pass deals each XCD's tile blocks by
+    last frame's longest walk; with split walks the same pre-pass also lists the heavy rays):
+    static and moved camera, a band tile and an odd tile count, bit-exact vs the plain per-tile
+    kernel and the oracle."""
+    from octreeraytracer_amd.scene import DEFAULT_YAW
+    s = ort.random_spheres(20000, 7)
+    t = ort.build_octree(s, depth, 1)
+    W, H = 720, 400  # 45 x 25 tiles
+    p0 = ort.FrameParams.default_camera(W, H, max_depth=md)
+    p1 = ort.FrameParams.default_camera(W, H, yaw=DEFAULT_YAW + 3.0, max_depth=md)
+    full = ort.Tile(0, W, 0, H)
+    band = ort.Tile(0, W, 0, 112, band_height=16, band_stride=64)
+    params = [p0, p0, p0, p1, p1, p0, p0]
+    tiles = [full, full, full, full, full, band, band]
+    with ort.Renderer(0) as r:
+        r.upload(s, t)
+        _plain(r)
+        want = _frames(ort, r, s, t, params, tiles)
+    with ort.Renderer(0) as r:
+        r.upload(s, t)
+        _plain(r)
+        r.set_tile_lpt(1)
+        r.set_split_heavy(split)
+        got = _frames(ort, r, s, t, params, tiles)
+    for i, (a, b) in enumerate(zip(got, want)):
+        assert_same(a, b, f"frame {i}: lpt (split {split}, md {md}, depth {depth}) vs plain")
+    assert_same(got[4][200:216], oracle.render(s, t, p1, 0, 200, W, 16), "moved camera, lpt vs oracle")
