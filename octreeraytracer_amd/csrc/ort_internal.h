@@ -62,6 +62,12 @@ int ort_debug_wave_stats(const float* sphere_center_radius, const float* sphere_
 // the lanes' steps back to back, one uint16 each: objects tested (bits 0-7, saturated),
 // leaf children tested (bits 8-11), bit 15 = the step's node has leaf children (LEAFKIDS).
 // Returns the number of steps (or, if cap is too small, minus the number needed).
+int ort_debug_bounce_walks(const float* sphere_center_radius, const float* sphere_mat_albedo,
+                           const float* sphere_fuzz_ri, int32_t n_spheres, const float* node_min, const float* node_max,
+                           const int32_t* children_offset, const int32_t* objects_offset, const int32_t* object_count,
+                           int32_t n_nodes, const int32_t* object_indices, int64_t n_indices, const ort_params* params,
+                           const ort_tile* tile, int32_t bounce, float* rays, int32_t* walks, int64_t cap,
+                           int64_t* n_out);
 int64_t ort_debug_walk_steps(const float* sphere_center_radius, const float* sphere_mat_albedo,
                              const float* sphere_fuzz_ri, int32_t n_spheres, const float* node_min,
                              const float* node_max, const int32_t* children_offset, const int32_t* objects_offset,

@@ -2868,6 +2868,115 @@ int ort_debug_wave_stats(const float* cr, const float* ma, const float* fr, int3
 }
 
 
+// ANALYSIS-ONLY (tools/bounce_lines.py): the rays of bounce `bounce` (>= 1) of a tile's pixels,
+// 1 sample (the host restatement of the path: trace_ray + shade_bounce per bounce, as
+// shade_pixel), and per alive ray the loads of its bounce walk (the persistent kernel's walk,
+// rejected-sphere skip on): per step {node popped, first object entry of a leaf or -1, objects}.
+// rays: 8 floats per pixel {o.xyz, d.xyz, alive, steps}.  walks: 3 ints per step, ray after
+// ray; n_out[0] = steps written (all steps if <= cap).
+int ort_debug_bounce_walks(const float* cr, const float* ma, const float* fr, int32_t n_spheres,
+                           const float* node_min, const float* node_max, const int32_t* co, const int32_t* oo,
+                           const int32_t* cnt, int32_t n_nodes, const int32_t* idx, int64_t n_indices,
+                           const ort_params* p, const ort_tile* t, int32_t bounce, float* rays, int32_t* walks,
+                           int64_t cap, int64_t* n_out) {
+    try {
+        const std::string bad = check_params(p, t);
+        if (!bad.empty() || bounce < 1 || p->num_samples != 1) return fail(nullptr, ORT_ERR_INVALID_ARG, "bad args");
+        ort::SceneInput in{cr, ma, fr, n_spheres, node_min, node_max, co, oo, cnt, n_nodes, idx, n_indices};
+        ort::CompactLayout cl;
+        std::string why;
+        if (!ort::buildCompactLayout(in, ORT_COMPACT_MAX_DEPTH, cl, why)) return fail(nullptr, ORT_ERR_UNSUPPORTED, why);
+        ort::KScene S;
+        std::memset(&S, 0, sizeof(S));
+        std::vector<float> fr2((size_t)n_spheres * 2);
+        for (int32_t i = 0; i < n_spheres; ++i) {
+            fr2[2 * (size_t)i] = fr[4 * (size_t)i];
+            fr2[2 * (size_t)i + 1] = fr[4 * (size_t)i + 1];
+        }
+        S.sph_cr = (const float4*)cr;
+        S.sph_ma = (const float4*)ma;
+        S.sph_fr = (const float2*)fr2.data();
+        S.n_spheres = n_spheres;
+        S.n_nodes = n_nodes;
+        S.node = (const uint2*)cl.node.data();
+        S.kid = (const uint2*)cl.kid.data();
+        S.tail_base = (uint32_t)in.n_indices;
+        S.leaf_sph = (const float4*)cl.leaf_sph.data();
+        S.leaf_idx = cl.leaf_idx.data();
+        S.planes = cl.planes.data();
+        S.depth = cl.depth;
+        std::vector<float> fplanes(ort::fast_plane_floats(cl.depth));
+        ort::fill_fast_planes(cl.planes.data(), fplanes.data(), cl.depth);
+        const bool rev_b = ort::Masks96Lean::kRevPlanes || ort::fast_rev_planes(cl.depth);
+        std::vector<float> fplanes_b(ort::fast_plane_floats(cl.depth, rev_b));
+        ort::fill_fast_planes(cl.planes.data(), fplanes_b.data(), cl.depth, rev_b);
+        std::vector<uint8_t> lut(kRankLutBytes);
+        for (size_t i = 0; i < lut.size(); ++i) lut[i] = ort::rank_lut_entry((uint32_t)i >> 8, (uint32_t)i & 255u);
+        const ort::PixelParams pp = pixel_params(p);
+        const TileMap tm = {t->x0, t->width, t->y0, t->rows, t->band_height, t->band_stride};
+        ort::LocalFrames lf;
+        ort::Counters cc;
+        for (int k = 0; k < 6; ++k) cc.v[k] = 0;
+        int64_t n = 0;
+        auto walk = [&](auto tag, const ort::Ray& ray, ort::V3 inv) -> int {
+            using Masks = decltype(tag);
+            ort::FastStateT<Masks> fs;
+            const float* pl = cl.depth > 8 ? fplanes_b.data() : fplanes.data();
+            if (!ort::fast_begin(S, pl, lut.data(), ray, inv, 0.001f, ORT_MAXFLOAT, fs)) return 0;
+            int steps = 0;
+            for (bool done = false; !done;) {
+                const uint2 rec = fs.rec;
+                const bool leaf = !(rec.y & ORT_INTERNAL_FLAG);
+                if (n < cap) {
+                    walks[3 * n] = fs.node;
+                    walks[3 * n + 1] = leaf ? (int)rec.x : -1;
+                    walks[3 * n + 2] = leaf ? (int)rec.y : 0;
+                }
+                ++n;
+                ++steps;
+                done = ort::fast_step<false>(S, lut.data(), fs, lf, cc);
+            }
+            return steps;
+        };
+        for (int row = 0; row < t->rows; ++row) {
+            const int y = tile_row_to_y(tm, row);
+            for (int c = 0; c < t->width; ++c) {
+                float* o = rays + 8 * ((size_t)row * t->width + c);
+                for (int k = 0; k < 8; ++k) o[k] = 0.0f;
+                if (y >= p->height) continue;
+                const int px = t->x0 + c;
+                ort_rng st;
+                ort::pixel_rng_init(pp, px, y, st);
+                ort::Ray ray = ort::primary_ray(pp, px, y, 0, st);
+                ort::V3 col = ort::mk(1.0f, 1.0f, 1.0f);
+                float importance = 1.0f;
+                bool alive = true;
+                for (int b = 0; b < bounce && alive; ++b) {
+                    if (importance < 0.01f) { alive = false; break; }
+                    float th;
+                    int entry;
+                    const int tr = ort::trace_ray<0, false>(S, fplanes.data(), lut.data(), ray, false, th, entry, lf, nullptr,
+                                                            nullptr, cc, b > 0, fplanes_b.data());
+                    ort::HitRec h;
+                    if (tr == ORT_TRACE_HIT) h = ort::hit_record<0>(S, ray, th, entry);
+                    if (ort::shade_bounce(tr == ORT_TRACE_HIT, h, ray, col, importance, st)) alive = false;
+                }
+                if (!alive || importance < 0.01f) continue;
+                ort::V3 inv = ort::mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
+                o[0] = ray.o.x; o[1] = ray.o.y; o[2] = ray.o.z;
+                o[3] = ray.d.x; o[4] = ray.d.y; o[5] = ray.d.z;
+                o[6] = 1.0f;
+                if (!ort::fast_prepare(S, ray, inv)) { o[6] = 2.0f; continue; }  // deferred (exact walk)
+                o[7] = (float)(cl.depth > 8 ? walk(ort::Masks96Lean{}, ray, inv) : walk(ort::Masks64Plain{}, ray, inv));
+            }
+        }
+        *n_out = n;
+        return ORT_OK;
+    } catch (const std::exception& ex) {
+        return fail(nullptr, ORT_ERR_INTERNAL, ex.what());
+    }
+}
+
 int64_t ort_debug_walk_steps(const float* cr, const float* ma, const float* fr, int32_t n_spheres,
                              const float* node_min, const float* node_max, const int32_t* co, const int32_t* oo,
                              const int32_t* cnt, int32_t n_nodes, const int32_t* idx, int64_t n_indices,
