@@ -140,12 +140,11 @@ typedef struct ort_scene_info {
                                       pixels dealt to 8 blocks of 64 by last frame's walk steps and each
                                       wave walking a heavy and a light block (a workgroup keeps its LDS
                                       until its slowest wave ends); 0: a tile per workgroup; -1 (default):
-                                      pairs on tiles of at least 2^22 pixels (on small tiles the fewer,
+                                      pairs on tiles of more than 2^21 pixels (on small tiles the fewer,
                                       longer workgroups lengthen the frame's tail).  Same pixels */
-#define ORT_OPT_TILE_LPT 17        /* 1 (1 sample, cost order on, a tile per workgroup): the camera-ray
-                                      workgroups of each XCD start in longest-first order of their tile's
-                                      longest walk in the previous frame of the same shape (a pre-pass
-                                      kernel deals the order); 0 (default): tile order.  Same pixels */
+#define ORT_OPT_TILE_LPT 17        /* removed (round 4): camera-ray workgroups of each XCD in longest-first
+                                      order of last frame's walks -- C3 -25 %, 1/8 band -17 % (the order
+                                      broke the XCD's runs of neighbouring tiles); ORT_ERR_UNSUPPORTED */
 
 /* Traffic counters (ort_count_traffic), in the REFERENCE layout's terms. */
 #define ORT_COUNT_NODES_POPPED 0

@@ -66,6 +66,7 @@ struct PipeArgs {
     int2* hit;        // per path: {entry (-1 miss), t bits}
     int* defer_list;
     int* sync;        // [0] deferred count, [1] work cursor of the persistent trace
+    int* sync_next;   // ort_trace_exact zeroes these 16 ints: the next trace launch's sync (the other set)
     float4* po;       // o.xyz, importance
     float4* pd;       // d.xyz, alive (1/0)
     float4* pc;       // path throughput c.xyz
@@ -86,11 +87,9 @@ struct PipeArgs {
     const uint32_t* hbits;
     const int* hlist;
     int* hsync;       // [0] heavy rays found (the list holds the first hcap), [1] ort_trace_split's cursor
+    int* hsync_next;  // the other pair: ort_trace_split zeroes it for the next frame's scan
     int hcap;
     int split_level;
-    // ORT_OPT_TILE_LPT: workgroup w of the per-tile camera kernel renders tile block border[w]
-    // (k_heavy_scan's order: each XCD's blocks by last frame's longest walk, longest first)
-    const int* border;
     ulonglong4* wclock;  // analysis builds only (ORT_PERSIST_CLOCK, ort_debug_wave_clock): per wave a timeline record
     int wclock_n;
 };
@@ -854,7 +853,7 @@ __device__ __forceinline__ void trace_compact_body(PipeArgs& A, unsigned char* s
     const unsigned long long tclk0 = __builtin_amdgcn_s_memrealtime();
 #endif
     LdsView L = setup_lds<true>(smem, A.S);
-    int k = ((PRIMARY && A.border) ? A.border[blockIdx.x] : (int)blockIdx.x) * kBlock + threadIdx.x;
+    int k = blockIdx.x * kBlock + threadIdx.x;
     if (PRIMARY && !COUNT && A.pcost) {  // (the counting pass: tile order)
         k = cost_order_slot<DEEP ? ORT_COST_SHIFT_DEEP : ORT_COST_SHIFT>(A.pcost, L.fr.co, k);
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -964,19 +963,12 @@ ort_trace_pair_deep(PipeArgs A) {
 // Heavy camera rays (ORT_OPT_SPLIT_HEAVY): the slots whose walk took >= T steps in the previous
 // frame (pcost), listed (the first `cap` of them) and marked in a bitmap the per-tile kernel
 // reads.  A wave's slots are listed in slot order after one atomic.
-//
-// With `order` (ORT_OPT_TILE_LPT; workgroup b = tile block b): each workgroup also records its
-// block's longest walk (the split ones aside) and the last workgroup to finish deals the blocks
-// of each XCD (block b runs on XCD b % 8) in longest-first order -- longest-processing-time
-// scheduling of the per-tile kernel's workgroups, which the GPU dispatches in index order.
-constexpr int kLptBuckets = 256;  // bucket = min(steps >> 1, 255)
 __global__ void __launch_bounds__(kBlock) k_heavy_scan(const uint16_t* pcost, int n, int T, int cap, uint32_t* bits,
-                                                       int* list, int* count, uint32_t* bmax, int* order) {
+                                                       int* list, int* count) {
     const int k = blockIdx.x * kBlock + threadIdx.x;
     const int lane = threadIdx.x & 63;
-    const int c = k < n ? (int)pcost[k] : 0;
-    if (bits) {
-        const bool h0 = k < n && c >= T;
+    {
+        const bool h0 = k < n && (int)pcost[k] >= T;
         const unsigned long long m = __ballot(h0);
         int base = 0;
         if (lane == 0 && m) base = atomicAdd(count, __popcll(m));
@@ -987,48 +979,6 @@ __global__ void __launch_bounds__(kBlock) k_heavy_scan(const uint16_t* pcost, in
         if (h) list[pos] = k;
         const unsigned long long mh = __ballot(h);
         if (k < n && (lane & 31) == 0) bits[k >> 5] = (uint32_t)(mh >> (lane & 32));
-    }
-    if (!order) return;
-    __shared__ int wmax[kBlock / 64];
-    __shared__ int last;
-    __shared__ int hist[8 * kLptBuckets];
-    int v = (bits && c >= T) ? 0 : c;  // (a capped heavy ray is walked here after all: approximate)
-    for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o));
-    if (lane == 0) wmax[threadIdx.x >> 6] = v;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int bm = wmax[0];
-        for (int w = 1; w < kBlock / 64; ++w) bm = max(bm, wmax[w]);
-        __hip_atomic_store(bmax + blockIdx.x, (uint32_t)bm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __threadfence();
-        last = atomicAdd(count + 2, 1) == (int)gridDim.x - 1;
-    }
-    __syncthreads();
-    if (!last) return;
-    __threadfence();
-    const int nb = (int)gridDim.x;
-    for (int i = threadIdx.x; i < 8 * kLptBuckets; i += kBlock) hist[i] = 0;
-    __syncthreads();
-    for (int b = threadIdx.x; b < nb; b += kBlock) {
-        const uint32_t bm = __hip_atomic_load(bmax + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        atomicAdd(&hist[(b & 7) * kLptBuckets + (kLptBuckets - 1 - (int)min(bm >> 1, (uint32_t)kLptBuckets - 1))], 1);
-    }
-    __syncthreads();
-    if (threadIdx.x < 8) {  // exclusive scan per XCD class (8 x 256 buckets: serial, tiny)
-        int* h = hist + threadIdx.x * kLptBuckets;
-        int run = 0;
-        for (int i = 0; i < kLptBuckets; ++i) {
-            const int t = h[i];
-            h[i] = run;
-            run += t;
-        }
-    }
-    __syncthreads();
-    for (int b = threadIdx.x; b < nb; b += kBlock) {
-        const uint32_t bm = __hip_atomic_load(bmax + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int x = b & 7;
-        const int pos = atomicAdd(&hist[x * kLptBuckets + (kLptBuckets - 1 - (int)min(bm >> 1, (uint32_t)kLptBuckets - 1))], 1);
-        order[x + 8 * pos] = b;  // the pos-th longest block of class x (any order within a bucket)
     }
 }
 
@@ -1048,6 +998,7 @@ __global__ void __launch_bounds__(kBlock) ort_trace_split(PipeArgs A) {
     const unsigned long long sclk0 = __builtin_amdgcn_s_memrealtime();
     int sitems = 0;
 #endif
+    if (A.hsync_next && blockIdx.x == 0 && threadIdx.x < 2) A.hsync_next[threadIdx.x] = 0;
     const int count = min(A.hsync[0], A.hcap);
     if (count == 0) return;
     LdsView L = setup_lds<true>(smem, A.S);
@@ -1151,6 +1102,9 @@ template <bool COUNT, bool PRIMARY, int FUSE>
 __global__ void __launch_bounds__(kBlock) ort_trace_exact(PipeArgs A) {
     extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];  // plane tables: 1 KiB-aligned
     const int n = *A.sync;
+    // the next launch's counters (the other set: its last users ended before this launch began),
+    // instead of a memset node per launch (a fill kernel: ~5 us of a 0.33 ms band frame)
+    if (A.sync_next && blockIdx.x == 0 && threadIdx.x < 16) A.sync_next[threadIdx.x] = 0;
     if ((int)(blockIdx.x * kBlock) >= n) return;  // usually no deferred ray at all: skip the LDS image copy
     LdsView L = setup_lds<false>(smem, A.S);
     ort::Counters cnt;
@@ -1276,12 +1230,13 @@ struct DevBuf {
 #endif
 // Camera-ray defaults, measured with tools/ab_stream.py: a raised issue priority
 // for waves holding a >= 150-step walk (C3 1/8 band +15 %, full frame +-0); split walks of the
-// >= 200-step rays on small tiles only (1/8 band +20 %, full frame -2 %); tile pairs on large
-// tiles only (full frame +2 %, 1/8 band -22 %).
+// >= 200-step rays on tiles of at most 2^21 pixels (C3 1/8 band +26 %, 1/4 band +21 %, 1/2 band
+// -2 %, full frame -2 %) and tile pairs on the larger ones (full frame +1.2 %, 1/2 band +0.8 %;
+// 1/4 band: split +21 % > pairs +16 %; 1/8 band: pairs with split -22 %).
 constexpr int kHeavyPrioSteps = 150;
 constexpr int kSplitAutoSteps = 200;
 constexpr long long kSplitAutoPixels = 1ll << 21;
-constexpr long long kPairsAutoPixels = 1ll << 22;
+constexpr long long kPairsAutoPixels = kSplitAutoPixels + 1;
 struct ort_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -1343,10 +1298,15 @@ struct ort_ctx {
     int split_level = 0;
     static constexpr int kSplitCap = 4096;  // heavy rays listed per frame at most
     hipStream_t aux_stream = nullptr;
-    hipEvent_t ev_scan = nullptr, ev_split = nullptr;
+    hipEvent_t ev_scan = nullptr, ev_split = nullptr, ev_tiles = nullptr, ev_pre = nullptr;
+    // the next frame's heavy list is scanned on aux_stream as soon as a frame's camera walks end
+    // (pcost final), beside its exact kernel, instead of opening the next frame: pre_ok when the
+    // list in hbits/hlist/hcnt[hpar] is that of a frame of shape pre_sig and threshold pre_steps
+    bool pre_ok = false;
+    unsigned long long pre_sig = 0;
+    int pre_steps = 0, hpar = 0;
+    DevBuf hcnt;  // two {heavy count, split cursor} pairs (16 ints): ort_trace_split zeroes the other
     DevBuf hbits, hlist;
-    int tile_lpt = 0;     // ORT_OPT_TILE_LPT
-    DevBuf bmax, border;  // its per-block longest walks and the workgroup -> block order
     DevBuf bcost;
     unsigned long long bcost_sig = 0;
     float root_lo[3] = {0, 0, 0}, root_hi[3] = {0, 0, 0};  // root box (coherence-sort key)
@@ -1367,6 +1327,8 @@ struct ort_ctx {
     DevBuf scratch_out, counters;
     // wavefront pipeline state, sized for the largest tile rendered so far
     DevBuf hit, defer_list, defer_count, po, pd, pc, prng, pcol;
+    int sync_set = 0;      // defer_count's counter set of the next trace launch (render_impl)
+    bool sync_ok = false;  // both sets zero except the one the last exact kernel left to zero
     DevBuf qlist, qlist2, qcount, qtemp;  // bounce >= 1 path compaction (two lists: read one, append the other)
     DevBuf skeys, skeys2, svals;  // coherence sort
     DevBuf key_spread;            // its origin-code tables for the scene's root box (path_key.h)
@@ -1802,7 +1764,7 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     const int ns = p->num_samples, maxd = p->max_depth;
     const bool direct = (ns == 1 && maxd == 1);
     if ((rc = ensure(ctx, ctx->hit, 8 * slots)) || (rc = ensure(ctx, ctx->defer_list, 4 * slots)) ||
-        (rc = ensure(ctx, ctx->defer_count, 64)))
+        (rc = ensure(ctx, ctx->defer_count, 128)))
         return rc;
     if (!direct || ctx->persistent) {
         if ((rc = ensure(ctx, ctx->po, 16 * slots)) || (rc = ensure(ctx, ctx->pd, 16 * slots)) ||
@@ -1876,6 +1838,14 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     a.refill = ctx->refill;
     a.hit = (int2*)ctx->hit.p;
     a.defer_list = (int*)ctx->defer_list.p;
+    // two sets of 16 counters (deferred count, persistent cursor, heavy list): a launch uses one
+    // and its exact kernel zeroes the other for the next launch; a memset re-zeroes both after a
+    // failed render or a new buffer (sync_ok)
+    if (!ctx->sync_ok) {
+        HIPCHK(ctx, hipMemsetAsync(ctx->defer_count.p, 0, 128, s));
+        ctx->sync_set = 0;
+    }
+    ctx->sync_ok = false;  // until this render has enqueued all its launches
     a.sync = (int*)ctx->defer_count.p;
     a.po = (float4*)ctx->po.p;
     a.pd = (float4*)ctx->pd.p;
@@ -1906,19 +1876,16 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     const int split_steps = ctx->split_steps >= 0 ? ctx->split_steps
                                                   : ((long long)pix <= kSplitAutoPixels ? kSplitAutoSteps : 0);
     const bool split = (fuse || fuse_first) && a.pcost && split_steps > 0 && !dcounters && ns == 1;
+    if (!split) ctx->pre_ok = false;  // (a queued heavy list is only for the next split frame)
     if (split) {
-        if ((rc = ensure(ctx, ctx->hbits, 4 * (slots / 32 + 1))) || (rc = ensure(ctx, ctx->hlist, 4 * (size_t)ort_ctx::kSplitCap)))
+        if ((rc = ensure(ctx, ctx->hbits, 4 * (slots / 32 + 1))) || (rc = ensure(ctx, ctx->hlist, 4 * (size_t)ort_ctx::kSplitCap)) ||
+            (rc = ensure(ctx, ctx->hcnt, 64)))
             return rc;
-        a.hsync = (int*)ctx->defer_count.p + 8;  // zeroed with the deferred-ray count, one memset per bounce
         a.hlist = (const int*)ctx->hlist.p;
         a.hcap = ort_ctx::kSplitCap;
         // the subtrees dealt to the lanes: ~5 levels above the leaves (a depth-8 tree: level 3)
         a.split_level = ctx->split_level > 0 ? ctx->split_level : std::max(1, ctx->depth - 5);
     }
-    // longest-first workgroup order (ORT_OPT_TILE_LPT; a tile per workgroup)
-    const bool lpt = (fuse || fuse_first) && a.pcost && ctx->tile_lpt && !pairs && !dcounters && ns == 1;
-    if (lpt && ((rc = ensure(ctx, ctx->bmax, 4 * (size_t)blocks)) || (rc = ensure(ctx, ctx->border, 4 * (size_t)blocks))))
-        return rc;
     // heavy first: the bounce >= 1 lists of the persistent trace (sorted, default path)
     const int nbc = std::min(ns * (maxd > 0 ? maxd : 1), ort_ctx::kCostBounces);  // recorded bounce indices
     uint16_t* bcost = nullptr;
@@ -1958,7 +1925,12 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
             a.last = (b == bounces - 1);
             const int fmode = fuse ? 1 : ((b == 0 && fuse_first) ? 2 : 0);
             if (!a.nobounce) {
-                HIPCHK(ctx, hipMemsetAsync(ctx->defer_count.p, 0, 64, s));
+                {   // this launch's counter set; mode 0 launches ort_trace_exact, which zeroes the other
+                    int* const set = (int*)ctx->defer_count.p + 16 * ctx->sync_set;
+                    a.sync = set;
+                    if (mode == 0) a.sync_next = (int*)ctx->defer_count.p + 16 * (ctx->sync_set ^ 1);
+                    else HIPCHK(ctx, hipMemsetAsync(set, 0, 64, s));
+                }
                 const int slot = fslot;
                 const int seg = ctx->tseg[slot];
                 const bool timed = seg < ort_ctx::kSeg;  // every trace launch of the frame, up to kSeg
@@ -1988,24 +1960,28 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                     if (bcost && fmode == 2 && hi + 1 < nbc && b + 1 < bounces) at.bcost_r = bcost + (size_t)(hi + 1) * slots;
                 }
                 const bool do_split = split && (fmode == 1 || fmode == 2);
-                const bool do_lpt = lpt && (fmode == 1 || fmode == 2);
-                if (do_lpt && !do_split) {
-                    hipLaunchKernelGGL(k_heavy_scan, dim3((unsigned)blocks), dim3(kBlock), 0, s, (const uint16_t*)a.pcost,
-                                       (int)slots, 0, 0, nullptr, nullptr, (int*)ctx->defer_count.p + 8,
-                                       (uint32_t*)ctx->bmax.p, (int*)ctx->border.p);
-                    HIPCHK(ctx, hipGetLastError());
-                }
-                if (do_lpt) at.border = (const int*)ctx->border.p;
+                const unsigned long long fsig = do_split ? frame_sig(ctx, p, t) : 0ull;
                 if (do_split) {
-                    // the heavy rays of this frame (last frame's steps), then their split walks on the
-                    // second stream beside the per-tile kernel (which passes over them)
-                    hipLaunchKernelGGL(k_heavy_scan, dim3((unsigned)blocks), dim3(kBlock), 0, s, (const uint16_t*)a.pcost,
-                                       (int)slots, split_steps, ort_ctx::kSplitCap, (uint32_t*)ctx->hbits.p,
-                                       (int*)ctx->hlist.p, a.hsync, do_lpt ? (uint32_t*)ctx->bmax.p : nullptr,
-                                       do_lpt ? (int*)ctx->border.p : nullptr);
-                    HIPCHK(ctx, hipGetLastError());
+                    // the heavy rays of this frame (last frame's steps) -- listed by the scan the last
+                    // frame of this shape queued on the second stream, or by one here -- then their
+                    // split walks there, beside the per-tile kernel (which passes over them)
+                    const bool pre = ctx->pre_ok && ctx->pre_sig == fsig && ctx->pre_steps == split_steps;
+                    ctx->pre_ok = false;
+                    int* hc = (int*)ctx->hcnt.p;
                     HIPCHK(ctx, hipEventRecord(ctx->ev_scan, s));
                     HIPCHK(ctx, hipStreamWaitEvent(ctx->aux_stream, ctx->ev_scan, 0));
+                    if (!pre) {
+                        HIPCHK(ctx, hipMemsetAsync(hc, 0, 64, ctx->aux_stream));
+                        ctx->hpar = 0;
+                        hipLaunchKernelGGL(k_heavy_scan, dim3((unsigned)blocks), dim3(kBlock), 0, ctx->aux_stream,
+                                           (const uint16_t*)a.pcost, (int)slots, split_steps, ort_ctx::kSplitCap,
+                                           (uint32_t*)ctx->hbits.p, (int*)ctx->hlist.p, hc);
+                        HIPCHK(ctx, hipGetLastError());
+                        HIPCHK(ctx, hipEventRecord(ctx->ev_pre, ctx->aux_stream));
+                    }
+                    HIPCHK(ctx, hipStreamWaitEvent(s, ctx->ev_pre, 0));  // the tile kernel reads hbits
+                    at.hsync = hc + 8 * ctx->hpar;
+                    at.hsync_next = hc + 8 * (ctx->hpar ^ 1);
                     const int hblocks = 32;  // 1024 heavy rays in flight; more loop
                     const dim3 hg(hblocks), ht(kBlock);
                     if (ctx->depth > 8 && fmode == 1) hipLaunchKernelGGL((ort_trace_split<true, 1>), hg, ht, lds, ctx->aux_stream, at);
@@ -2020,7 +1996,22 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                 e = dcounters ? launch_trace<true>(mode, prim, at, tblocks, pb, lds, s, fmode)
                               : launch_trace<false>(mode, prim, at, tblocks, pb, lds, s, fmode);
                 if (e != hipSuccess) return hip_fail(ctx, e, "trace kernel launch");
-                if (do_split) HIPCHK(ctx, hipStreamWaitEvent(s, ctx->ev_split, 0));  // joined before the exact kernel
+                if (do_split) {
+                    HIPCHK(ctx, hipStreamWaitEvent(s, ctx->ev_split, 0));  // joined before the exact kernel
+                    // the next frame's heavy list, from this frame's steps (final now), on the second
+                    // stream beside the exact kernel; ort_trace_split zeroed the other count pair
+                    HIPCHK(ctx, hipEventRecord(ctx->ev_tiles, s));
+                    HIPCHK(ctx, hipStreamWaitEvent(ctx->aux_stream, ctx->ev_tiles, 0));
+                    ctx->hpar ^= 1;
+                    hipLaunchKernelGGL(k_heavy_scan, dim3((unsigned)blocks), dim3(kBlock), 0, ctx->aux_stream,
+                                       (const uint16_t*)a.pcost, (int)slots, split_steps, ort_ctx::kSplitCap,
+                                       (uint32_t*)ctx->hbits.p, (int*)ctx->hlist.p, (int*)ctx->hcnt.p + 8 * ctx->hpar);
+                    HIPCHK(ctx, hipGetLastError());
+                    HIPCHK(ctx, hipEventRecord(ctx->ev_pre, ctx->aux_stream));
+                    ctx->pre_ok = true;
+                    ctx->pre_sig = fsig;
+                    ctx->pre_steps = split_steps;
+                }
                 if (timed) {
                     HIPCHK(ctx, hipEventRecord(ctx->tr1[slot][seg], s));
                     ctx->tseg[slot] = seg + 1;
@@ -2036,6 +2027,7 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                     else if (prim) hipLaunchKernelGGL((ort_trace_exact<false, true, 0>), g, t, lds_exact, s, at);
                     else hipLaunchKernelGGL((ort_trace_exact<false, false, 0>), g, t, lds_exact, s, at);
                     if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "ort_trace_exact launch");
+                    ctx->sync_set ^= 1;  // it zeroes the other set for the next launch
                 }
             }
             if (!fuse && fmode != 2) {
@@ -2116,6 +2108,7 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     }
     HIPCHK(ctx, hipEventRecord(ctx->ev1, s));
     ctx->timed = true;
+    ctx->sync_ok = true;  // every launch enqueued: the counter sets are in step again
     if (!out_is_device) {
         HIPCHK(ctx, hipMemcpyAsync(out, dout, 12 * pix, hipMemcpyDeviceToHost, s));
         HIPCHK(ctx, hipStreamSynchronize(s));
@@ -2170,7 +2163,9 @@ int ort_create(int device, ort_ctx** out) {
         }
     if ((e = hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking)) != hipSuccess ||
         (e = hipEventCreateWithFlags(&c->ev_scan, hipEventDisableTiming)) != hipSuccess ||
-        (e = hipEventCreateWithFlags(&c->ev_split, hipEventDisableTiming)) != hipSuccess) {
+        (e = hipEventCreateWithFlags(&c->ev_split, hipEventDisableTiming)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&c->ev_tiles, hipEventDisableTiming)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&c->ev_pre, hipEventDisableTiming)) != hipSuccess) {
         const int rc = hip_fail(nullptr, e, "ort_create: second stream");
         ort_destroy(c);
         return rc;
@@ -2188,7 +2183,7 @@ int ort_destroy(ort_ctx* ctx) {
     free_buf(ctx->counters);
     DevBuf* pipe[] = {&ctx->hit, &ctx->defer_list, &ctx->defer_count, &ctx->po, &ctx->pd, &ctx->pc, &ctx->prng, &ctx->pcol,
                       &ctx->qlist, &ctx->qlist2, &ctx->qcount, &ctx->qtemp, &ctx->skeys, &ctx->skeys2, &ctx->svals, &ctx->key_spread,
-                      &ctx->pcost, &ctx->bcost, &ctx->hbits, &ctx->hlist, &ctx->bmax, &ctx->border};
+                      &ctx->pcost, &ctx->bcost, &ctx->hbits, &ctx->hlist, &ctx->hcnt};
     for (DevBuf* b : pipe) free_buf(*b);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
@@ -2207,6 +2202,8 @@ int ort_destroy(ort_ctx* ctx) {
     }
     if (ctx->ev_scan) (void)hipEventDestroy(ctx->ev_scan);
     if (ctx->ev_split) (void)hipEventDestroy(ctx->ev_split);
+    if (ctx->ev_tiles) (void)hipEventDestroy(ctx->ev_tiles);
+    if (ctx->ev_pre) (void)hipEventDestroy(ctx->ev_pre);
     delete ctx;
     return ORT_OK;
 }
@@ -2264,11 +2261,8 @@ int ort_set_option(ort_ctx* ctx, int option, int value) {
         ctx->split_level = value;
         return ORT_OK;
     }
-    if (option == ORT_OPT_TILE_LPT) {
-        if (value < 0 || value > 1) return fail(ctx, ORT_ERR_INVALID_ARG, "ORT_OPT_TILE_LPT: 0 or 1");
-        ctx->tile_lpt = value;
-        return ORT_OK;
-    }
+    if (option == ORT_OPT_TILE_LPT)  // longest-first workgroup order: C3 -25 %, 1/8 band -17 %
+        return fail(ctx, ORT_ERR_UNSUPPORTED, "ORT_OPT_TILE_LPT (longest-first workgroups) was removed (C3 -25 %)");
     if (option == ORT_OPT_HEAVY_PRIO) {
         if (value < 0 || value > 65535) return fail(ctx, ORT_ERR_INVALID_ARG, "ORT_OPT_HEAVY_PRIO: 0 (off) .. 65535 steps");
         ctx->heavy_prio = value;

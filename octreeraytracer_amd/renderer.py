@@ -163,14 +163,9 @@ class Renderer:
 
     def set_tile_pairs(self, on: int):
         """ORT_OPT_TILE_PAIRS: camera-ray workgroups of two tiles, each wave a heavy and a light 64-pixel
-        block by last frame's walk steps; 0 a tile per workgroup; -1 (default) pairs on tiles of at least
-        2^22 pixels.  Same pixels."""
+        block by last frame's walk steps; 0 a tile per workgroup; -1 (default) pairs on tiles of more
+        than 2^21 pixels.  Same pixels."""
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_TILE_PAIRS, int(on)))
-
-    def set_tile_lpt(self, on: int):
-        """ORT_OPT_TILE_LPT: camera-ray workgroups of each XCD start longest-first by last frame's
-        longest walk of their tile; 0 (default) tile order.  Same pixels."""
-        self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_TILE_LPT, int(on)))
 
     def set_cost_order(self, on: int):
         """ORT_OPT_COST_ORDER: 1 (default) camera rays dealt to waves by last frame's walk cost; 0 fixed blocks."""

@@ -107,12 +107,11 @@ def test_heavy_first_option_range(ort):
 
 
 def _plain(r):
-    """The per-tile kernel alone: no heavy priority, split walks, tile pairs or longest-first order
-    (the defaults turn some of them on by tile size)."""
+    """The per-tile kernel alone: no heavy priority, split walks or tile pairs (the defaults turn
+    them on by tile size)."""
     r.set_heavy_prio(0)
     r.set_split_heavy(0)
     r.set_tile_pairs(0)
-    r.set_tile_lpt(0)
 
 
 @pytest.mark.parametrize("split,level,prio,md", [(40, 0, 150, 1), (20, 1, 0, 1), (60, 2, 60, 1), (30, 5, 0, 1),
@@ -195,32 +194,34 @@ def test_tile_pairs_frames_match(ort, oracle, ns, md, depth):
     assert_same(got[1][2][200:216], oracle.render(s, t, p1, 0, 200, W, 16), "tile pairs, moved camera vs oracle")
 
 
-@pytest.mark.parametrize("split,md,depth", [(0, 1, 6), (200, 1, 6), (30, 1, 6), (30, 3, 6), (0, 1, 9), (40, 2, 9)])
-def test_tile_lpt_frames_match(ort, oracle, split, md, depth):
-    """Longest-first workgroup order (ORT_OPT_TILE_LPT: a pre-pass deals each XCD's tile blocks by
-    last frame's longest walk; with split walks the same pre-pass also lists the heavy rays):
-    static and moved camera, a band tile and an odd tile count, bit-exact vs the plain per-tile
-    kernel and the oracle."""
-    from octreeraytracer_amd.scene import DEFAULT_YAW
-    s = ort.random_spheres(20000, 7)
-    t = ort.build_octree(s, depth, 1)
-    W, H = 720, 400  # 45 x 25 tiles
-    p0 = ort.FrameParams.default_camera(W, H, max_depth=md)
-    p1 = ort.FrameParams.default_camera(W, H, yaw=DEFAULT_YAW + 3.0, max_depth=md)
+def test_split_heavy_queued_list_across_other_frames(ort, oracle, scene_c2):
+    """The next frame's heavy list is queued on the second stream at the end of a split frame; a
+    frame without split walks (another shape, a larger tile that regrows the buffers, the counting
+    render, split off) in between must not let a stale list through: bit-exact vs the plain kernel."""
+    s, t = scene_c2
+    W, H = 960, 540
+    p = ort.FrameParams.default_camera(W, H)
+    band = ort.Tile(0, W, 0, 136, band_height=16, band_stride=128)
     full = ort.Tile(0, W, 0, H)
-    band = ort.Tile(0, W, 0, 112, band_height=16, band_stride=64)
-    params = [p0, p0, p0, p1, p1, p0, p0]
-    tiles = [full, full, full, full, full, band, band]
     with ort.Renderer(0) as r:
         r.upload(s, t)
         _plain(r)
-        want = _frames(ort, r, s, t, params, tiles)
+        want_band, want_full = r.render(p, band), r.render(p, full)
     with ort.Renderer(0) as r:
         r.upload(s, t)
         _plain(r)
-        r.set_tile_lpt(1)
-        r.set_split_heavy(split)
-        got = _frames(ort, r, s, t, params, tiles)
-    for i, (a, b) in enumerate(zip(got, want)):
-        assert_same(a, b, f"frame {i}: lpt (split {split}, md {md}, depth {depth}) vs plain")
-    assert_same(got[4][200:216], oracle.render(s, t, p1, 0, 200, W, 16), "moved camera, lpt vs oracle")
+        r.set_split_heavy(30)
+        got = [r.render(p, band) for _ in range(3)]
+        r.set_split_heavy(0)
+        got.append(r.render(p, band))            # same shape, no split walks
+        r.set_split_heavy(30)
+        got += [r.render(p, band) for _ in range(2)]
+        got_full = r.render(p, full)             # another shape (larger: the buffers regrow)
+        r.count_traffic(p, band)                 # the counting render
+        got += [r.render(p, band) for _ in range(2)]
+        got_full2 = r.render(p, full)
+    for i, g in enumerate(got):
+        assert_same(g, want_band, f"band frame {i}")
+    assert_same(got_full, want_full, "full frame")
+    assert_same(got_full2, want_full, "full frame again")
+    assert_same(got[-1][0:16], oracle.render(s, t, p, 0, 0, W, 16), "band rows 0-15 vs oracle")

@@ -182,7 +182,7 @@ def test_removed_options_are_refused(ort, renderer):
     """The variants removed in round 4 (packet walk, wave queue, every-trace persistent) fail
     loudly instead of silently rendering another way."""
     from octreeraytracer_amd import _lib as L
-    for opt, val in ((L.ORT_OPT_PACKET, 1), (L.ORT_OPT_WAVE_QUEUE, 1), (L.ORT_OPT_PERSISTENT, 1)):
+    for opt, val in ((L.ORT_OPT_PACKET, 1), (L.ORT_OPT_WAVE_QUEUE, 1), (L.ORT_OPT_PERSISTENT, 1), (L.ORT_OPT_TILE_LPT, 1)):
         with pytest.raises(ort.OrtError):
             renderer._check(renderer._lib.ort_set_option(renderer._ctx, opt, val))
 
