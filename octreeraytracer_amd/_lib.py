@@ -39,6 +39,7 @@ ORT_OPT_SPLIT_HEAVY = 14
 ORT_OPT_SPLIT_LEVEL = 15
 ORT_OPT_TILE_PAIRS = 16
 ORT_OPT_TILE_LPT = 17
+ORT_OPT_DEBUG_FLAGS = 18
 ORT_LAYOUT_COMPACT_EXACT_EMULATION = 2
 ORT_COUNT_N = 6
 COUNT_NAMES = ("nodes_popped", "child_records", "leaf_objects", "accepted_hits", "pixels", "traversals")
@@ -170,7 +171,7 @@ def lib():
         if not Path(path).exists():
             raise OSError(f"libort.so not found at {path}: run `make lib` or __graft_entry__.build()")
         l = C.CDLL(path, mode=C.RTLD_GLOBAL)
-        _declare(l)
+        _declare(l, strict="ORT_LIB" not in os.environ)  # (an older build for A/B may lack analysis hooks)
         _lib = l
     return _lib
 

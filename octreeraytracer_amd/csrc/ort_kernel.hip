@@ -1241,6 +1241,7 @@ struct ort_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t ev0_last = nullptr;  // the last frame's start: ev0, or its first trace-timing event
     static constexpr int kRing = 64;           // trace-kernel timing of the last 64 frames
     static constexpr int kSeg = 16;            // ... of their first 16 trace launches each
     hipEvent_t tr0[kRing][kSeg] = {}, tr1[kRing][kSeg] = {};  // segment 0 created up front, others lazily
@@ -1328,6 +1329,7 @@ struct ort_ctx {
     // wavefront pipeline state, sized for the largest tile rendered so far
     DevBuf hit, defer_list, defer_count, po, pd, pc, prng, pcol;
     int sync_set = 0;      // defer_count's counter set of the next trace launch (render_impl)
+    int debug_flags = 0;   // ORT_OPT_DEBUG_FLAGS (A/B of the per-frame stream structure only)
     bool sync_ok = false;  // both sets zero except the one the last exact kernel left to zero
     DevBuf qlist, qlist2, qcount, qtemp;  // bounce >= 1 path compaction (two lists: read one, append the other)
     DevBuf skeys, skeys2, svals;  // coherence sort
@@ -1907,9 +1909,13 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     // dispatches fast
     const int exact_blocks = 256;
     hipError_t e;
-    HIPCHK(ctx, hipEventRecord(ctx->ev0, s));
     const int fslot = (int)(ctx->frames % ort_ctx::kRing);  // this frame's timing slot
     ctx->tseg[fslot] = 0;
+    // the frame's start: also the start of its first trace launch when that is timed (nothing is
+    // enqueued between them), which saves an event packet per frame (~1 % of a 1/8 band frame)
+    const bool start_is_tr0 = maxd > 0 && !(ctx->debug_flags & 1);
+    ctx->ev0_last = start_is_tr0 ? ctx->tr0[fslot][0] : ctx->ev0;
+    HIPCHK(ctx, hipEventRecord(ctx->ev0_last, s));
     for (int smp = 0; smp < ns; ++smp) {
         a.sample = smp;
         a.qlist = nullptr;  // bounce 0: every slot
@@ -1933,12 +1939,13 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                 }
                 const int slot = fslot;
                 const int seg = ctx->tseg[slot];
-                const bool timed = seg < ort_ctx::kSeg;  // every trace launch of the frame, up to kSeg
+                // every trace launch of the frame, up to kSeg (analysis flag 1: none)
+                const bool timed = seg < ort_ctx::kSeg && !(ctx->debug_flags & 1);
                 if (timed && !ctx->tr0[slot][seg]) {
                     HIPCHK(ctx, hipEventCreate(&ctx->tr0[slot][seg]));
                     HIPCHK(ctx, hipEventCreate(&ctx->tr1[slot][seg]));
                 }
-                if (timed) HIPCHK(ctx, hipEventRecord(ctx->tr0[slot][seg], s));
+                if (timed && !(seg == 0 && start_is_tr0)) HIPCHK(ctx, hipEventRecord(ctx->tr0[slot][seg], s));
                 const bool prim = b == 0;
                 const int pb = (pers_bounce && b > 0) ? pblocks : 0;
                 PipeArgs at = a;
@@ -1965,11 +1972,19 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                     // the heavy rays of this frame (last frame's steps) -- listed by the scan the last
                     // frame of this shape queued on the second stream, or by one here -- then their
                     // split walks there, beside the per-tile kernel (which passes over them)
-                    const bool pre = ctx->pre_ok && ctx->pre_sig == fsig && ctx->pre_steps == split_steps;
+                    const bool pre = ctx->pre_ok && ctx->pre_sig == fsig && ctx->pre_steps == split_steps &&
+                                     !(ctx->debug_flags & 2);
                     ctx->pre_ok = false;
                     int* hc = (int*)ctx->hcnt.p;
-                    HIPCHK(ctx, hipEventRecord(ctx->ev_scan, s));
-                    HIPCHK(ctx, hipStreamWaitEvent(ctx->aux_stream, ctx->ev_scan, 0));
+                    // the second stream follows this one up to here: with shading fused (1 bounce)
+                    // nothing of this frame precedes the split walks on it but ev0 (event packets
+                    // cost the frame ~1 % each); bounce 0 of a longer path needs the list memset too
+                    if (fmode == 1) {
+                        HIPCHK(ctx, hipStreamWaitEvent(ctx->aux_stream, ctx->ev0_last, 0));
+                    } else {
+                        HIPCHK(ctx, hipEventRecord(ctx->ev_scan, s));
+                        HIPCHK(ctx, hipStreamWaitEvent(ctx->aux_stream, ctx->ev_scan, 0));
+                    }
                     if (!pre) {
                         HIPCHK(ctx, hipMemsetAsync(hc, 0, 64, ctx->aux_stream));
                         ctx->hpar = 0;
@@ -2000,8 +2015,13 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                     HIPCHK(ctx, hipStreamWaitEvent(s, ctx->ev_split, 0));  // joined before the exact kernel
                     // the next frame's heavy list, from this frame's steps (final now), on the second
                     // stream beside the exact kernel; ort_trace_split zeroed the other count pair
-                    HIPCHK(ctx, hipEventRecord(ctx->ev_tiles, s));
-                    HIPCHK(ctx, hipStreamWaitEvent(ctx->aux_stream, ctx->ev_tiles, 0));
+                    hipEvent_t tiles = ctx->ev_tiles;  // (the trace-timing event when there is one)
+                    if (timed) {
+                        tiles = ctx->tr1[slot][seg];
+                        ctx->tseg[slot] = seg + 1;
+                    }
+                    HIPCHK(ctx, hipEventRecord(tiles, s));
+                    HIPCHK(ctx, hipStreamWaitEvent(ctx->aux_stream, tiles, 0));
                     ctx->hpar ^= 1;
                     hipLaunchKernelGGL(k_heavy_scan, dim3((unsigned)blocks), dim3(kBlock), 0, ctx->aux_stream,
                                        (const uint16_t*)a.pcost, (int)slots, split_steps, ort_ctx::kSplitCap,
@@ -2011,8 +2031,7 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                     ctx->pre_ok = true;
                     ctx->pre_sig = fsig;
                     ctx->pre_steps = split_steps;
-                }
-                if (timed) {
+                } else if (timed) {
                     HIPCHK(ctx, hipEventRecord(ctx->tr1[slot][seg], s));
                     ctx->tseg[slot] = seg + 1;
                 }
@@ -2261,6 +2280,11 @@ int ort_set_option(ort_ctx* ctx, int option, int value) {
         ctx->split_level = value;
         return ORT_OK;
     }
+    if (option == ORT_OPT_DEBUG_FLAGS) {  // analysis: 1 no trace-timing events, 2 no queued heavy scan
+        if (value < 0 || value > 3) return fail(ctx, ORT_ERR_INVALID_ARG, "ORT_OPT_DEBUG_FLAGS: 0 .. 3");
+        ctx->debug_flags = value;
+        return ORT_OK;
+    }
     if (option == ORT_OPT_TILE_LPT)  // longest-first workgroup order: C3 -25 %, 1/8 band -17 %
         return fail(ctx, ORT_ERR_UNSUPPORTED, "ORT_OPT_TILE_LPT (longest-first workgroups) was removed (C3 -25 %)");
     if (option == ORT_OPT_HEAVY_PRIO) {
@@ -2399,7 +2423,7 @@ int ort_last_kernel_ms(ort_ctx* ctx, float* ms) {
     if (!ctx || !ms) return fail(nullptr, ORT_ERR_INVALID_ARG, "ort_last_kernel_ms: null argument");
     if (!ctx->timed) return fail(ctx, ORT_ERR_NO_SCENE, "no kernel launched yet");
     HIPCHK(ctx, hipEventSynchronize(ctx->ev1));
-    HIPCHK(ctx, hipEventElapsedTime(ms, ctx->ev0, ctx->ev1));
+    HIPCHK(ctx, hipEventElapsedTime(ms, ctx->ev0_last, ctx->ev1));
     return ORT_OK;
 }
 

@@ -167,6 +167,10 @@ class Renderer:
         than 2^21 pixels.  Same pixels."""
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_TILE_PAIRS, int(on)))
 
+    def set_debug_flags(self, flags: int):
+        """ORT_OPT_DEBUG_FLAGS (analysis, A/B only): 1 no trace-timing events, 2 no queued heavy scan."""
+        self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_DEBUG_FLAGS, int(flags)))
+
     def set_cost_order(self, on: int):
         """ORT_OPT_COST_ORDER: 1 (default) camera rays dealt to waves by last frame's walk cost; 0 fixed blocks."""
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_COST_ORDER, int(on)))
