@@ -113,6 +113,8 @@ def parse(argv=None):
     ap.add_argument("--single-steps", type=int, default=10,
                     help="N > 1 with frames in flight: also time this many frames with one frame in flight "
                     "(reported as single_frame, after the main timed region; 0 = skip)")
+    ap.add_argument("--group-opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="--group: ort_group_set_option(ORT_OPT_<NAME>, VALUE) on every context (A/B)")
     ap.add_argument("--group", action="store_true",
                     help="one process drives all N GPUs through the C-ABI group (ort_group_*: a context per device, "
                     "RCCL ncclSend/ncclRecv gather over xGMI); with --rehearse-one-gpu every rank is GPU 0 and the "
@@ -611,6 +613,10 @@ def group_bench(args):
     spheres = ort.random_spheres(NSPH, args.seed)
     p = ort.FrameParams.default_camera(W, H, num_samples=NS, max_depth=MAXD)
     g = RenderGroup(devices, transport, inflight=inflight)
+    from octreeraytracer_amd import _lib as L
+    for o in args.group_opt:
+        name, val = o.split("=")
+        g.set_option(getattr(L, "ORT_OPT_" + name.upper()), int(val))
     t0 = time.time()
     g.build_scene(spheres, DEPTH, MPN)
     setup = {"group_build_scene_wall_s": round(time.time() - t0, 3)}

@@ -310,6 +310,9 @@ __device__ inline ort::Ray load_ray(const PipeArgs& A, int k, bool& alive) {
 #ifndef ORT_PERSIST_STATS
 #define ORT_PERSIST_STATS 0
 #endif
+#ifndef ORT_LEAF_HOLD
+#define ORT_LEAF_HOLD 0  // experiment (tools/build_variant.sh): hold leaf lanes until this many
+#endif
 #ifndef ORT_CHUNK
 #define ORT_CHUNK 64
 #endif
@@ -424,7 +427,20 @@ ort_trace_persistent(PipeArgs A) {
             ps[7] += (ni > 0 && nl > 0);
         }
 #endif
+#if ORT_LEAF_HOLD
+        // (experiment) lanes at a leaf wait until ORT_LEAF_HOLD lanes are at leaves or none is at
+        // an internal node, so the leaf block runs for more lanes at once (each lane's own walk is
+        // unchanged: same pixels)
+        bool hold = false;
+        {
+            const bool at_leaf = k >= 0 && !(st.rec.y & ORT_INTERNAL_FLAG);
+            const unsigned long long lm = __ballot(at_leaf), im = __ballot(k >= 0 && !at_leaf);
+            hold = at_leaf && im != 0 && __popcll(lm) < ORT_LEAF_HOLD;
+        }
+        if (k >= 0 && !hold) {
+#else
         if (k >= 0) {
+#endif
             ++nst;
             if (ort::fast_step<COUNT>(A.S, lut, st, L.fr, cnt)) {
                 A.hit[k] = make_int2(st.hitEntry, __float_as_int(st.closest));
@@ -2011,8 +2027,11 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                 e = dcounters ? launch_trace<true>(mode, prim, at, tblocks, pb, lds, s, fmode)
                               : launch_trace<false>(mode, prim, at, tblocks, pb, lds, s, fmode);
                 if (e != hipSuccess) return hip_fail(ctx, e, "trace kernel launch");
+                // (analysis flag 4: the exact kernel on the second stream after the split walks, this
+                // stream waiting for it instead of for the split walks)
+                const bool exact_aux = do_split && mode == 0 && (ctx->debug_flags & 4);
                 if (do_split) {
-                    HIPCHK(ctx, hipStreamWaitEvent(s, ctx->ev_split, 0));  // joined before the exact kernel
+                    if (!exact_aux) HIPCHK(ctx, hipStreamWaitEvent(s, ctx->ev_split, 0));  // joined before the exact kernel
                     // the next frame's heavy list, from this frame's steps (final now), on the second
                     // stream beside the exact kernel; ort_trace_split zeroed the other count pair
                     hipEvent_t tiles = ctx->ev_tiles;  // (the trace-timing event when there is one)
@@ -2022,6 +2041,15 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                     }
                     HIPCHK(ctx, hipEventRecord(tiles, s));
                     HIPCHK(ctx, hipStreamWaitEvent(ctx->aux_stream, tiles, 0));
+                    if (exact_aux) {
+                        const dim3 g(exact_blocks), t(kBlock);
+                        if (fuse) hipLaunchKernelGGL((ort_trace_exact<false, true, 1>), g, t, lds_exact, ctx->aux_stream, at);
+                        else hipLaunchKernelGGL((ort_trace_exact<false, true, 2>), g, t, lds_exact, ctx->aux_stream, at);
+                        if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "ort_trace_exact launch");
+                        ctx->sync_set ^= 1;
+                        HIPCHK(ctx, hipEventRecord(ctx->ev_split, ctx->aux_stream));
+                        HIPCHK(ctx, hipStreamWaitEvent(s, ctx->ev_split, 0));
+                    }
                     ctx->hpar ^= 1;
                     hipLaunchKernelGGL(k_heavy_scan, dim3((unsigned)blocks), dim3(kBlock), 0, ctx->aux_stream,
                                        (const uint16_t*)a.pcost, (int)slots, split_steps, ort_ctx::kSplitCap,
@@ -2035,7 +2063,7 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                     HIPCHK(ctx, hipEventRecord(ctx->tr1[slot][seg], s));
                     ctx->tseg[slot] = seg + 1;
                 }
-                if (mode == 0) {
+                if (mode == 0 && !exact_aux) {
                     const bool prim = b == 0;
                     const dim3 g(exact_blocks), t(kBlock);
                     if (dcounters && fuse) hipLaunchKernelGGL((ort_trace_exact<true, true, 1>), g, t, lds_exact, s, at);
@@ -2280,8 +2308,8 @@ int ort_set_option(ort_ctx* ctx, int option, int value) {
         ctx->split_level = value;
         return ORT_OK;
     }
-    if (option == ORT_OPT_DEBUG_FLAGS) {  // analysis: 1 no trace-timing events, 2 no queued heavy scan
-        if (value < 0 || value > 3) return fail(ctx, ORT_ERR_INVALID_ARG, "ORT_OPT_DEBUG_FLAGS: 0 .. 3");
+    if (option == ORT_OPT_DEBUG_FLAGS) {  // analysis: 1 no trace-timing events, 2 no queued heavy scan, 4 exact kernel on aux
+        if (value < 0 || value > 7) return fail(ctx, ORT_ERR_INVALID_ARG, "ORT_OPT_DEBUG_FLAGS: 0 .. 7");
         ctx->debug_flags = value;
         return ORT_OK;
     }
