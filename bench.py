@@ -602,8 +602,12 @@ def group_bench(args):
     # concurrently) has not run between distinct devices yet, so it is opt-in (--inflight);
     # the copy-transport rehearsal takes the per-config default
     inflight = args.inflight or (default_inflight(args.config, N) if args.rehearse_one_gpu or N == 1 else 1)
-    if inflight > 1:  # as main(): frame slots overlap only on distinct hardware queues
-        os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, max(8, 4 * inflight)))
+    if inflight > 1:  # as main(): frame slots overlap only on distinct hardware queues -- one per
+        # stream: every rank's render stream on its device (all of them on GPU 0 in the rehearsal)
+        # plus devices[0]'s gather stream, per frame slot (a shared queue serialises a gather
+        # behind another slot's render: +10 % single-frame latency in the rehearsal)
+        need = inflight * (N + 1) if args.rehearse_one_gpu else 4 * inflight
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, max(8, need)))
     import torch
 
     import octreeraytracer_amd as ort

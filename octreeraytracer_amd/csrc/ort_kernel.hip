@@ -310,8 +310,13 @@ __device__ inline ort::Ray load_ray(const PipeArgs& A, int k, bool& alive) {
 #ifndef ORT_PERSIST_STATS
 #define ORT_PERSIST_STATS 0
 #endif
+// Leaf hold in the depth 9-10 bounce walk: a lane whose next node is a leaf waits until this many
+// lanes of its wave are at leaves (or none is at an internal node), so the leaf block -- run in 92 %
+// of the steps for 6.5 lanes on average (tools/persist_stats.py) -- runs less often for more lanes.
+// C5 +2.4 / +2.7 / +2.3 / -2.4 % at 8 / 12 / 16 / 24 (tools/ab_stream.py); the depth <= 8 bounce
+// walk loses (C3 at 4 bounces: -1.7 % at 8), so it is off there.
 #ifndef ORT_LEAF_HOLD
-#define ORT_LEAF_HOLD 0  // experiment (tools/build_variant.sh): hold leaf lanes until this many
+#define ORT_LEAF_HOLD 12
 #endif
 #ifndef ORT_CHUNK
 #define ORT_CHUNK 64
@@ -428,11 +433,9 @@ ort_trace_persistent(PipeArgs A) {
         }
 #endif
 #if ORT_LEAF_HOLD
-        // (experiment) lanes at a leaf wait until ORT_LEAF_HOLD lanes are at leaves or none is at
-        // an internal node, so the leaf block runs for more lanes at once (each lane's own walk is
-        // unchanged: same pixels)
+        // leaf hold (DEEP): each lane's own walk is unchanged, only when it steps (same pixels)
         bool hold = false;
-        {
+        if (DEEP) {
             const bool at_leaf = k >= 0 && !(st.rec.y & ORT_INTERNAL_FLAG);
             const unsigned long long lm = __ballot(at_leaf), im = __ballot(k >= 0 && !at_leaf);
             hold = at_leaf && im != 0 && __popcll(lm) < ORT_LEAF_HOLD;
@@ -1896,6 +1899,7 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     const bool split = (fuse || fuse_first) && a.pcost && split_steps > 0 && !dcounters && ns == 1;
     if (!split) ctx->pre_ok = false;  // (a queued heavy list is only for the next split frame)
     if (split) {
+        if (!ctx->aux_stream) HIPCHK(ctx, hipStreamCreateWithFlags(&ctx->aux_stream, hipStreamNonBlocking));
         if ((rc = ensure(ctx, ctx->hbits, 4 * (slots / 32 + 1))) || (rc = ensure(ctx, ctx->hlist, 4 * (size_t)ort_ctx::kSplitCap)) ||
             (rc = ensure(ctx, ctx->hcnt, 64)))
             return rc;
@@ -2208,8 +2212,10 @@ int ort_create(int device, ort_ctx** out) {
             ort_destroy(c);
             return rc;
         }
-    if ((e = hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking)) != hipSuccess ||
-        (e = hipEventCreateWithFlags(&c->ev_scan, hipEventDisableTiming)) != hipSuccess ||
+    // (the second stream itself is created with the first split frame: a stream takes one of the
+    // process's few hardware queues, and contexts that never split -- group ranks sharing a
+    // device -- should not crowd the others' queues)
+    if ((e = hipEventCreateWithFlags(&c->ev_scan, hipEventDisableTiming)) != hipSuccess ||
         (e = hipEventCreateWithFlags(&c->ev_split, hipEventDisableTiming)) != hipSuccess ||
         (e = hipEventCreateWithFlags(&c->ev_tiles, hipEventDisableTiming)) != hipSuccess ||
         (e = hipEventCreateWithFlags(&c->ev_pre, hipEventDisableTiming)) != hipSuccess) {

@@ -1318,6 +1318,8 @@ ORT_FN bool traverse_fast_t(const KScene& S, const float* planes, const uint8_t*
     FastStateT<Masks> st;
     const bool in = fast_begin(S, planes, rank_lut, r, inv, t_min, t_max, st);
     int n = 0;  // walk steps (steps: the cost order's record; folds away without it)
+    // (a leaf hold as in the deep bounce walk, lanes at a leaf waiting for company, cost the deep
+    // camera walk 10-14 % at 8-16 lanes: the coherent camera rays reach leaves together anyway)
     if (in)
         while (!fast_step<COUNT>(S, rank_lut, st, fr, cnt)) {
             ++n;
