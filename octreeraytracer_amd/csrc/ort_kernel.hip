@@ -318,6 +318,9 @@ __device__ inline ort::Ray load_ray(const PipeArgs& A, int k, bool& alive) {
 #ifndef ORT_LEAF_HOLD
 #define ORT_LEAF_HOLD 12
 #endif
+#ifndef ORT_LEAF_HOLD_MIN_INTERNAL
+#define ORT_LEAF_HOLD_MIN_INTERNAL 1  // ... and only while at least this many lanes are at internal nodes
+#endif
 #ifndef ORT_CHUNK
 #define ORT_CHUNK 64
 #endif
@@ -438,7 +441,7 @@ ort_trace_persistent(PipeArgs A) {
         if (DEEP) {
             const bool at_leaf = k >= 0 && !(st.rec.y & ORT_INTERNAL_FLAG);
             const unsigned long long lm = __ballot(at_leaf), im = __ballot(k >= 0 && !at_leaf);
-            hold = at_leaf && im != 0 && __popcll(lm) < ORT_LEAF_HOLD;
+            hold = at_leaf && __popcll(im) >= ORT_LEAF_HOLD_MIN_INTERNAL && __popcll(lm) < ORT_LEAF_HOLD;
         }
         if (k >= 0 && !hold) {
 #else
