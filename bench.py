@@ -344,6 +344,13 @@ def main():
         setup["build_scene_wall_s"] = round((time.time() - t0) / inflight, 3)
     info = r.info()
     p = ort.FrameParams.default_camera(W, H, num_samples=NS, max_depth=MAXD)
+    if inflight > 1:
+        # frames in flight fill each frame's tail themselves: split walks of the heaviest camera
+        # rays (ORT_OPT_SPLIT_HEAVY, on by default for tiles <= 2^21 px) only add launches then --
+        # C3 1/8 band at 3 in flight 0.266 -> 0.227 ms/frame without them, 1/4 band 0.458 -> 0.423
+        # (profiles/r04_host_overhead_inflight_o.log); the single-frame phase below turns them on
+        for x in rs:
+            x.set_split_heavy(0)
 
     # partition: 16-row bands dealt round-robin; every rank renders the same number of rows
     from octreeraytracer_amd.distributed import FrameGather, rank_tile
@@ -427,6 +434,7 @@ def main():
     single = None
     trace_ms_in_flight = None
     if inflight > 1 and args.single_steps > 0:
+        rs[0].set_split_heavy(-1)  # one frame in flight: the default (split walks on small tiles)
         sev = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for _ in range(args.single_steps)]
         torch.cuda.synchronize()
         if world > 1:
@@ -511,7 +519,7 @@ def main():
         ms_per_step = elapsed / args.steps * 1e3
         value = rays_per_frame * args.steps / elapsed / 1e6
         pmc = load_pmc(args, tile.rows)
-        kernels = trace_kernel_names(args.config, info, MAXD, NS)
+        kernels = trace_kernel_names(args.config, info, MAXD, NS, tile.rows * W)
         result = {
             "metric": metric_name(args.config),
             "value": round(value, 2),
@@ -698,7 +706,9 @@ def group_bench(args):
                          "frame_latency_ms": round(single_lat, 4)},
         "trace_kernels_ms_avg_rank0": round(float(np.mean(trace_ms)), 4),
         "roofline": roofline(pmc, counts[0], (pmc or {}).get("traversals_per_frame"), alg_bytes,
-                             float(np.mean(trace_ms)), trace_kernel_names(args.config, info, MAXD, NS)),
+                             float(np.mean(trace_ms)),
+                             trace_kernel_names(args.config, info, MAXD, NS, W * -(-H // (16 * N)) * 16,
+                                                split_ok=inflight == 1 and not args.rehearse_one_gpu)),
         "frame_check": ("bit-identical to a single-context ort_render of the same scene" if same
                         else "MISMATCH against a single-context ort_render"),
         "setup": setup,
@@ -711,16 +721,24 @@ def group_bench(args):
         raise SystemExit("group frame differs from the single-context render")
 
 
-def trace_kernel_names(cfg, info, maxd, ns):
-    """The trace kernels a frame of this config launches (ort_kernel.hip render_impl)."""
+SPLIT_AUTO_PIXELS = 1 << 21  # ort_kernel.hip kSplitAutoPixels: split walks at or below, tile pairs above
+
+
+def trace_kernel_names(cfg, info, maxd, ns, pixels, split_ok=True):
+    """The trace kernels a frame of this config launches (ort_kernel.hip render_impl, default
+    options: tile pairs on tiles above 2^21 pixels, split walks of the heaviest camera rays at or
+    below it, 1 sample; split_ok False: the caller turned the split walks off, tile pairs)."""
     deep = info["tree_depth"] > 8
+    pairs = pixels > SPLIT_AUTO_PIXELS or not split_ok
+    tile = ("ort_trace_pair%s<false, %d> (two tiles per workgroup: camera rays + walk + %s)" if pairs else
+            "ort_trace_compact%s<false, true, %d> (camera rays + walk + %s)")
+    split = [] if pairs or ns != 1 else ["ort_trace_split<%s, %d> (the heaviest camera rays, 8 lanes each, second "
+                                         "stream)" % (str(deep).lower(), 1 if maxd == 1 else 2)]
     if maxd == 1 and ns == 1:
-        return ["ort_trace_compact%s<false, true, 1> (camera rays + walk + shading into the frame)"
-                % ("_deep" if deep else "")]
-    return ["ort_trace_compact%s<false, true, 2> (camera rays + walk + bounce-0 shading, cost order)"
-            % ("_deep" if deep else ""),
-            "ort_trace_persistent<false, %s> (bounces >= 1, sorted alive paths heavy first, lane refill)"
-            % str(deep).lower()]
+        return [tile % ("_deep" if deep else "", 1, "shading into the frame")] + split
+    return [tile % ("_deep" if deep else "", 2, "bounce-0 shading, cost order")] + split + \
+        ["ort_trace_persistent<false, %s> (bounces >= 1, sorted alive paths heavy first, lane refill%s)"
+         % (str(deep).lower(), ", leaf hold" if deep else "")]
 
 
 def emulate(args, world, rank):

@@ -267,13 +267,12 @@ int ort_group_create_pipelined(const int32_t* devices, int32_t n_devices, int32_
         for (int r = 0; r < n_devices; ++r) {
             int rc = ort_create(devices[r], &S.ctx[r]);
             if (rc != ORT_OK) return bail(rc);
-            // ranks sharing a device fill each other's single-frame tail: no split walks there
-            // (ORT_OPT_SPLIT_HEAVY's second stream only adds launches; ort_group_set_option overrides)
-            for (int q = 0; q < n_devices; ++q)
-                if (q != r && devices[q] == devices[r]) {
-                    (void)ort_set_option(S.ctx[r], ORT_OPT_SPLIT_HEAVY, 0);
-                    break;
-                }
+            // ranks sharing a device, or frames in flight, fill each frame's tail themselves: no
+            // split walks there (ORT_OPT_SPLIT_HEAVY's second stream only adds launches: C3 1/8 band
+            // at 3 in flight -15 %; ort_group_set_option overrides)
+            bool shared = frames_in_flight > 1;
+            for (int q = 0; q < n_devices && !shared; ++q) shared = q != r && devices[q] == devices[r];
+            if (shared) (void)ort_set_option(S.ctx[r], ORT_OPT_SPLIT_HEAVY, 0);
             void* s = nullptr;
             ort_get_stream(S.ctx[r], &s);
             S.stream[r] = (hipStream_t)s;

@@ -1771,8 +1771,11 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     const int tilesX = (t->width + 15) / 16, tilesY = (t->rows + 15) / 16;
     // tile pairs (ORT_OPT_TILE_PAIRS; the compact layout, trees of 4+ levels: cost_order_pair's
     // scratch): the slot blocks of a pair are consecutive, a last odd column's second tile a hole
+    // (auto: on large tiles, and on any tile whose caller turned the split walks off -- frames in
+    // flight fill the tail, and pairs then pay on small tiles too: 1/4 band at 3 in flight +4 %)
     const bool pairs = mode == 0 && ctx->depth >= 4 &&
-                       (ctx->tile_pairs > 0 || (ctx->tile_pairs < 0 && (long long)pix >= kPairsAutoPixels));
+                       (ctx->tile_pairs > 0 ||
+                        (ctx->tile_pairs < 0 && ((long long)pix >= kPairsAutoPixels || ctx->split_steps == 0)));
     const int gridX = pairs ? (tilesX + 1) / 2 : tilesX;
     const long long blocks = (long long)(pairs ? 2 * gridX : tilesX) * tilesY;
     if (blocks * kBlock > 0x7fffffffLL) return fail(ctx, ORT_ERR_INVALID_ARG, "ort_render: tile too large");

@@ -2,7 +2,7 @@
 world size, rank 0's band tile of an N-GPU run (is the host fast enough to feed a GPU that
 renders 1/N of the frame?).  With inflight > 1, that many renderers (each with its own copy of
 the scene) take frames in turn on their own streams, so one frame's tail overlaps the next.
-usage: python tools/host_overhead.py [config] [frames] [world] [inflight] [torch|hip|prio]"""
+usage: python tools/host_overhead.py [config] [frames] [world] [inflight] [torch|hip|prio] [option=value ...]"""
 import os
 import sys
 import time
@@ -23,10 +23,13 @@ n = int(sys.argv[2]) if len(sys.argv) > 2 else 100
 world = int(sys.argv[3]) if len(sys.argv) > 3 else 1
 inflight = int(sys.argv[4]) if len(sys.argv) > 4 else 1
 kind = sys.argv[5] if len(sys.argv) > 5 else "torch"
+opts = [o.split("=") for o in sys.argv[6:]]  # Renderer setters, e.g. split_heavy=0
 W, H, N, D, M, NS, MD = bench.CONFIGS[cfg]
 s = ort.random_spheres(N, 42)
 rs = [ort.Renderer(0) for _ in range(inflight)]
 for r in rs:
+    for k, v in opts:
+        getattr(r, "set_" + k)(int(v))
     r.build_scene(s, D, M)
 from octreeraytracer_amd.distributed import rank_tile  # noqa: E402
 tile = rank_tile(W, H, 0, world)
@@ -65,6 +68,6 @@ t1 = time.perf_counter()
 torch.cuda.synchronize()
 t2 = time.perf_counter()
 r = rs[0]
-print(f"{cfg} world={world} inflight={inflight}: enqueue {1e3 * (t1 - t0) / n:.3f} ms/frame, wall {1e3 * (t2 - t0) / n:.3f} ms/frame, "
+print(f"{cfg} world={world} inflight={inflight}{' ' + ' '.join(sys.argv[6:]) if opts else ''}: enqueue {1e3 * (t1 - t0) / n:.3f} ms/frame, wall {1e3 * (t2 - t0) / n:.3f} ms/frame, "
       f"gpu span {e0.elapsed_time(e1) / n:.3f} ms/frame, last frame pipeline {r.last_kernel_ms():.3f} ms, "
       f"trace {r.last_trace_ms():.3f} ms")

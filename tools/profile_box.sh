@@ -25,7 +25,7 @@ run() {  # name, counters...  (each pass its own run; at most 8 SQ / 4 TCC / 2 G
 # (its one-frame-in-flight phase when the default keeps two in flight)
 echo "{\"steps\": $STEPS, \"warmup\": $WARM, \"config\": \"$CFG\", \"inflight\": 1}" > $OUT/bench_args.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o trace -- \
-    python3 $R/bench.py --config $CFG --steps $STEPS --warmup $WARM --inflight 1 --no-cpu-baseline > $OUT/trace_bench.log 2>&1 || { echo "trace failed"; exit 1; }
+    python3 $R/bench.py --config $CFG --steps $STEPS --warmup $WARM --inflight 1 --no-cpu-baseline --moving-steps 0 > $OUT/trace_bench.log 2>&1 || { echo "trace failed"; exit 1; }
 echo "kernel trace ok"
 run fetch FETCH_SIZE
 run write WRITE_SIZE

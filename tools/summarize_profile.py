@@ -16,7 +16,9 @@ from pathlib import Path
 args = [a for a in sys.argv[1:] if not a.startswith("--")]
 src, dst, cfg = Path(args[0]), Path(args[1]), args[2]
 record = "--no-record" not in sys.argv
-TRACE_RE = re.compile(r"ort_trace_(compact_deep|compact|persistent|kernel)<(false|0)")
+# the production trace kernels (COUNT false): per-tile camera kernels (one or two tiles per
+# workgroup), the persistent bounce kernel, the split walks (no COUNT variant)
+TRACE_RE = re.compile(r"ort_trace_((compact_deep|compact|pair_deep|pair|persistent|kernel)<(false|0)|split<)")
 
 
 def short(name):
