@@ -134,14 +134,18 @@ typedef struct ort_scene_info {
                                       the per-tile kernel: a small tile's frame no longer waits for its
                                       longest walks.  0: off.  -1 (default): T = 200 on tiles of at most
                                       2^21 pixels, off on larger ones (where the second stream costs more
-                                      than the tail it cuts).  Same pixels */
+                                      than the tail it cuts).  A caller that keeps several frames in
+                                      flight should set 0: the next frames fill the tail (C3 1/8 band at
+                                      3 in flight: 0.266 -> 0.227 ms/frame); pipelined groups do.
+                                      Same pixels */
 #define ORT_OPT_SPLIT_LEVEL 15     /* the level of those subtrees: 0 (default) = tree depth - 5 (at least 1) */
 #define ORT_OPT_TILE_PAIRS 16      /* 1: a camera-ray workgroup renders two 16x16 tiles side by side, its 512
                                       pixels dealt to 8 blocks of 64 by last frame's walk steps and each
                                       wave walking a heavy and a light block (a workgroup keeps its LDS
                                       until its slowest wave ends); 0: a tile per workgroup; -1 (default):
-                                      pairs on tiles of more than 2^21 pixels (on small tiles the fewer,
-                                      longer workgroups lengthen the frame's tail).  Same pixels */
+                                      pairs on tiles of more than 2^21 pixels, or on any tile when
+                                      ORT_OPT_SPLIT_HEAVY is 0 (on small tiles at one frame in flight the
+                                      fewer, longer workgroups lengthen the frame's tail).  Same pixels */
 #define ORT_OPT_DEBUG_FLAGS 18     /* analysis only (tools/ab_stream.py): 1 records no per-launch trace-timing
                                       events (ort_trace_times_ms then reports none), 2 scans the heavy
                                       list at the start of each split frame instead of queueing it at

@@ -76,3 +76,20 @@ def test_sample_rows_spans_the_frame(height):
         assert abs(rows - want) <= max(2, want // 10), (height, n, rows)  # about the asked size
         if want >= 4:  # evenly spread: rows in both the bottom and the top eighth of the frame
             assert min(ys) < height / 8 + bs and max(ys) >= height * 7 / 8 - bs, (height, n, ys[:3], ys[-3:])
+
+
+@pytest.mark.parametrize("pixels,split_ok,pairs,split", [
+    (3840 * 2160, True, True, False),   # full C3 frame: tile pairs
+    (3840 * 1080, True, True, False),   # 1/2 band (> 2^21 px)
+    (3840 * 544, True, False, True),    # 1/4 band: split walks at one frame in flight
+    (3840 * 272, True, False, True),    # 1/8 band
+    (3840 * 272, False, True, False),   # frames in flight: split walks off, pairs
+])
+def test_trace_kernel_names_follow_the_tile_rules(pixels, split_ok, pairs, split):
+    """The roofline's kernel list names what render_impl launches by default (tile pairs above
+    2^21 px or with split walks off, split walks at or below it)."""
+    names = bench.trace_kernel_names("c3", {"tree_depth": 8}, 1, 1, pixels, split_ok=split_ok)
+    assert names[0].startswith("ort_trace_pair<" if pairs else "ort_trace_compact<")
+    assert any(n.startswith("ort_trace_split<false, 1>") for n in names) == split
+    deep = bench.trace_kernel_names("c5", {"tree_depth": 10}, 4, 1, 7680 * 4320)
+    assert deep[0].startswith("ort_trace_pair_deep<false, 2>") and deep[-1].startswith("ort_trace_persistent<false, true>")
