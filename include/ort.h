@@ -148,9 +148,8 @@ typedef struct ort_scene_info {
                                       fewer, longer workgroups lengthen the frame's tail).  Same pixels */
 #define ORT_OPT_DEBUG_FLAGS 18     /* analysis only (tools/ab_stream.py): 1 records no per-launch trace-timing
                                       events (ort_trace_times_ms then reports none), 2 scans the heavy
-                                      list at the start of each split frame instead of queueing it at
-                                      the end of the last, 4 runs the exact kernel of a split frame on the
-                                      second stream after the split walks; 0 (default).  Same pixels */
+                                      list at the start of each split frame instead of in the last
+                                      frame's exact kernel; 0 (default).  Same pixels */
 #define ORT_OPT_TILE_LPT 17        /* removed (round 4): camera-ray workgroups of each XCD in longest-first
                                       order of last frame's walks -- C3 -25 %, 1/8 band -17 % (the order
                                       broke the XCD's runs of neighbouring tiles); ORT_ERR_UNSUPPORTED */

@@ -67,6 +67,11 @@ struct PipeArgs {
     int* defer_list;
     int* sync;        // [0] deferred count, [1] work cursor of the persistent trace
     int* sync_next;   // ort_trace_exact zeroes these 16 ints: the next trace launch's sync (the other set)
+    const uint16_t* scan_pcost;  // ort_trace_exact also lists the next frame's heavy rays (split frames)
+    int scan_T;
+    uint32_t* scan_bits;
+    int* scan_list;
+    int* scan_count;
     float4* po;       // o.xyz, importance
     float4* pd;       // d.xyz, alive (1/0)
     float4* pc;       // path throughput c.xyz
@@ -985,23 +990,52 @@ ort_trace_pair_deep(PipeArgs A) {
 // Heavy camera rays (ORT_OPT_SPLIT_HEAVY): the slots whose walk took >= T steps in the previous
 // frame (pcost), listed (the first `cap` of them) and marked in a bitmap the per-tile kernel
 // reads.  A wave's slots are listed in slot order after one atomic.
-__global__ void __launch_bounds__(kBlock) k_heavy_scan(const uint16_t* pcost, int n, int T, int cap, uint32_t* bits,
-                                                       int* list, int* count) {
-    const int k = blockIdx.x * kBlock + threadIdx.x;
+// One wave scans 1024 slots from `base` (a multiple of 1024; n a multiple of 256): 16 per lane,
+// read as two 16-byte loads, one atomic per wave, each lane pair writing one bitmap word.
+struct HeavyScan {
+    const uint16_t* pcost;
+    int n, T, cap;
+    uint32_t* bits;
+    int* list;
+    int* count;
+};
+__device__ inline void heavy_scan_wave(const HeavyScan& H, int base) {
     const int lane = threadIdx.x & 63;
-    {
-        const bool h0 = k < n && (int)pcost[k] >= T;
-        const unsigned long long m = __ballot(h0);
-        int base = 0;
-        if (lane == 0 && m) base = atomicAdd(count, __popcll(m));
-        base = __shfl(base, 0);
-        const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-        const int pos = base + __popcll(m & below);
-        const bool h = h0 && pos < cap;  // past the cap the per-tile kernel walks them itself
-        if (h) list[pos] = k;
-        const unsigned long long mh = __ballot(h);
-        if (k < n && (lane & 31) == 0) bits[k >> 5] = (uint32_t)(mh >> (lane & 32));
+    const int s0 = base + 16 * lane;
+    uint32_t m = 0;
+    if (s0 < H.n) {
+        const uint4 a = *(const uint4*)(H.pcost + s0), b = *(const uint4*)(H.pcost + s0 + 8);
+        const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        for (int i = 0; i < 8; ++i) {
+            m |= (uint32_t)((int)(w[i] & 0xffffu) >= H.T) << (2 * i);
+            m |= (uint32_t)((int)(w[i] >> 16) >= H.T) << (2 * i + 1);
+        }
     }
+    const int c = __popc(m);
+    int incl = c;  // inclusive scan of the lanes' counts
+    for (int off = 1; off < 64; off <<= 1) {
+        const int v = __shfl_up(incl, off);
+        if (lane >= off) incl += v;
+    }
+    const int total = __shfl(incl, 63);
+    int at = 0;
+    if (lane == 0 && total) at = atomicAdd(H.count, total);
+    int pos = __shfl(at, 0) + incl - c;
+    uint32_t mh = 0;  // the listed ones (past the cap the per-tile kernel walks them itself)
+    for (uint32_t r = m; r; r &= r - 1, ++pos) {
+        const int i = __builtin_ctz(r);
+        if (pos < H.cap) {
+            H.list[pos] = s0 + i;
+            mh |= 1u << i;
+        }
+    }
+    const uint32_t other = (uint32_t)__shfl_xor((int)mh, 1);
+    if (s0 < H.n && !(lane & 1)) H.bits[s0 >> 5] = mh | (other << 16);
+}
+__global__ void __launch_bounds__(kBlock) k_heavy_scan(HeavyScan H) {
+    for (int base = (int)(blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * 1024; base < H.n;
+         base += (int)(gridDim.x * (kBlock / 64)) * 1024)
+        heavy_scan_wave(H, base);
 }
 
 // The heavy camera rays of k_heavy_scan's list, each walked by a group of 8 lanes that deal its
@@ -1127,6 +1161,12 @@ __global__ void __launch_bounds__(kBlock) ort_trace_exact(PipeArgs A) {
     // the next launch's counters (the other set: its last users ended before this launch began),
     // instead of a memset node per launch (a fill kernel: ~5 us of a 0.33 ms band frame)
     if (A.sync_next && blockIdx.x == 0 && threadIdx.x < 16) A.sync_next[threadIdx.x] = 0;
+    if (A.scan_pcost) {  // the next frame's heavy list from this frame's final steps (split frames)
+        const HeavyScan H{A.scan_pcost, (int)A.total, A.scan_T, A.hcap, A.scan_bits, A.scan_list, A.scan_count};
+        for (int base = (int)(blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * 1024; base < H.n;
+             base += (int)(gridDim.x * (kBlock / 64)) * 1024)
+            heavy_scan_wave(H, base);
+    }
     if ((int)(blockIdx.x * kBlock) >= n) return;  // usually no deferred ray at all: skip the LDS image copy
     LdsView L = setup_lds<false>(smem, A.S);
     ort::Counters cnt;
@@ -1321,10 +1361,10 @@ struct ort_ctx {
     int split_level = 0;
     static constexpr int kSplitCap = 4096;  // heavy rays listed per frame at most
     hipStream_t aux_stream = nullptr;
-    hipEvent_t ev_scan = nullptr, ev_split = nullptr, ev_tiles = nullptr, ev_pre = nullptr;
-    // the next frame's heavy list is scanned on aux_stream as soon as a frame's camera walks end
-    // (pcost final), beside its exact kernel, instead of opening the next frame: pre_ok when the
-    // list in hbits/hlist/hcnt[hpar] is that of a frame of shape pre_sig and threshold pre_steps
+    hipEvent_t ev_scan = nullptr, ev_split = nullptr, ev_pre = nullptr;
+    // the next frame's heavy list is listed by a split frame's exact kernel (pcost final by then)
+    // instead of by a scan opening the next frame: pre_ok when the list in hbits/hlist/hcnt[hpar]
+    // is that of a frame of shape pre_sig and threshold pre_steps
     bool pre_ok = false;
     unsigned long long pre_sig = 0;
     int pre_steps = 0, hpar = 0;
@@ -2011,16 +2051,17 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                         HIPCHK(ctx, hipEventRecord(ctx->ev_scan, s));
                         HIPCHK(ctx, hipStreamWaitEvent(ctx->aux_stream, ctx->ev_scan, 0));
                     }
-                    if (!pre) {
+                    if (!pre) {  // (with pre, the last frame's exact kernel listed them, in this stream's order)
                         HIPCHK(ctx, hipMemsetAsync(hc, 0, 64, ctx->aux_stream));
                         ctx->hpar = 0;
-                        hipLaunchKernelGGL(k_heavy_scan, dim3((unsigned)blocks), dim3(kBlock), 0, ctx->aux_stream,
-                                           (const uint16_t*)a.pcost, (int)slots, split_steps, ort_ctx::kSplitCap,
-                                           (uint32_t*)ctx->hbits.p, (int*)ctx->hlist.p, hc);
+                        const HeavyScan H{(const uint16_t*)a.pcost, (int)slots, split_steps, ort_ctx::kSplitCap,
+                                          (uint32_t*)ctx->hbits.p, (int*)ctx->hlist.p, hc};
+                        hipLaunchKernelGGL(k_heavy_scan, dim3((unsigned)((slots + 4095) / 4096)), dim3(kBlock), 0,
+                                           ctx->aux_stream, H);
                         HIPCHK(ctx, hipGetLastError());
                         HIPCHK(ctx, hipEventRecord(ctx->ev_pre, ctx->aux_stream));
+                        HIPCHK(ctx, hipStreamWaitEvent(s, ctx->ev_pre, 0));  // the tile kernel reads hbits
                     }
-                    HIPCHK(ctx, hipStreamWaitEvent(s, ctx->ev_pre, 0));  // the tile kernel reads hbits
                     at.hsync = hc + 8 * ctx->hpar;
                     at.hsync_next = hc + 8 * (ctx->hpar ^ 1);
                     const int hblocks = 32;  // 1024 heavy rays in flight; more loop
@@ -2037,35 +2078,21 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                 e = dcounters ? launch_trace<true>(mode, prim, at, tblocks, pb, lds, s, fmode)
                               : launch_trace<false>(mode, prim, at, tblocks, pb, lds, s, fmode);
                 if (e != hipSuccess) return hip_fail(ctx, e, "trace kernel launch");
-                // (analysis flag 4: the exact kernel on the second stream after the split walks, this
-                // stream waiting for it instead of for the split walks)
-                const bool exact_aux = do_split && mode == 0 && (ctx->debug_flags & 4);
                 if (do_split) {
-                    if (!exact_aux) HIPCHK(ctx, hipStreamWaitEvent(s, ctx->ev_split, 0));  // joined before the exact kernel
-                    // the next frame's heavy list, from this frame's steps (final now), on the second
-                    // stream beside the exact kernel; ort_trace_split zeroed the other count pair
-                    hipEvent_t tiles = ctx->ev_tiles;  // (the trace-timing event when there is one)
+                    HIPCHK(ctx, hipStreamWaitEvent(s, ctx->ev_split, 0));  // joined before the exact kernel
                     if (timed) {
-                        tiles = ctx->tr1[slot][seg];
+                        HIPCHK(ctx, hipEventRecord(ctx->tr1[slot][seg], s));
                         ctx->tseg[slot] = seg + 1;
                     }
-                    HIPCHK(ctx, hipEventRecord(tiles, s));
-                    HIPCHK(ctx, hipStreamWaitEvent(ctx->aux_stream, tiles, 0));
-                    if (exact_aux) {
-                        const dim3 g(exact_blocks), t(kBlock);
-                        if (fuse) hipLaunchKernelGGL((ort_trace_exact<false, true, 1>), g, t, lds_exact, ctx->aux_stream, at);
-                        else hipLaunchKernelGGL((ort_trace_exact<false, true, 2>), g, t, lds_exact, ctx->aux_stream, at);
-                        if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "ort_trace_exact launch");
-                        ctx->sync_set ^= 1;
-                        HIPCHK(ctx, hipEventRecord(ctx->ev_split, ctx->aux_stream));
-                        HIPCHK(ctx, hipStreamWaitEvent(s, ctx->ev_split, 0));
-                    }
+                    // the exact kernel also lists the next frame's heavy rays, from this frame's
+                    // steps (final now) -- no scan launch or cross-stream wait opens the next frame;
+                    // ort_trace_split zeroed the other count pair
                     ctx->hpar ^= 1;
-                    hipLaunchKernelGGL(k_heavy_scan, dim3((unsigned)blocks), dim3(kBlock), 0, ctx->aux_stream,
-                                       (const uint16_t*)a.pcost, (int)slots, split_steps, ort_ctx::kSplitCap,
-                                       (uint32_t*)ctx->hbits.p, (int*)ctx->hlist.p, (int*)ctx->hcnt.p + 8 * ctx->hpar);
-                    HIPCHK(ctx, hipGetLastError());
-                    HIPCHK(ctx, hipEventRecord(ctx->ev_pre, ctx->aux_stream));
+                    at.scan_pcost = a.pcost;
+                    at.scan_T = split_steps;
+                    at.scan_bits = (uint32_t*)ctx->hbits.p;
+                    at.scan_list = (int*)ctx->hlist.p;
+                    at.scan_count = (int*)ctx->hcnt.p + 8 * ctx->hpar;
                     ctx->pre_ok = true;
                     ctx->pre_sig = fsig;
                     ctx->pre_steps = split_steps;
@@ -2073,7 +2100,7 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                     HIPCHK(ctx, hipEventRecord(ctx->tr1[slot][seg], s));
                     ctx->tseg[slot] = seg + 1;
                 }
-                if (mode == 0 && !exact_aux) {
+                if (mode == 0) {
                     const bool prim = b == 0;
                     const dim3 g(exact_blocks), t(kBlock);
                     if (dcounters && fuse) hipLaunchKernelGGL((ort_trace_exact<true, true, 1>), g, t, lds_exact, s, at);
@@ -2223,7 +2250,6 @@ int ort_create(int device, ort_ctx** out) {
     // device -- should not crowd the others' queues)
     if ((e = hipEventCreateWithFlags(&c->ev_scan, hipEventDisableTiming)) != hipSuccess ||
         (e = hipEventCreateWithFlags(&c->ev_split, hipEventDisableTiming)) != hipSuccess ||
-        (e = hipEventCreateWithFlags(&c->ev_tiles, hipEventDisableTiming)) != hipSuccess ||
         (e = hipEventCreateWithFlags(&c->ev_pre, hipEventDisableTiming)) != hipSuccess) {
         const int rc = hip_fail(nullptr, e, "ort_create: second stream");
         ort_destroy(c);
@@ -2261,7 +2287,6 @@ int ort_destroy(ort_ctx* ctx) {
     }
     if (ctx->ev_scan) (void)hipEventDestroy(ctx->ev_scan);
     if (ctx->ev_split) (void)hipEventDestroy(ctx->ev_split);
-    if (ctx->ev_tiles) (void)hipEventDestroy(ctx->ev_tiles);
     if (ctx->ev_pre) (void)hipEventDestroy(ctx->ev_pre);
     delete ctx;
     return ORT_OK;
@@ -2320,8 +2345,8 @@ int ort_set_option(ort_ctx* ctx, int option, int value) {
         ctx->split_level = value;
         return ORT_OK;
     }
-    if (option == ORT_OPT_DEBUG_FLAGS) {  // analysis: 1 no trace-timing events, 2 no queued heavy scan, 4 exact kernel on aux
-        if (value < 0 || value > 7) return fail(ctx, ORT_ERR_INVALID_ARG, "ORT_OPT_DEBUG_FLAGS: 0 .. 7");
+    if (option == ORT_OPT_DEBUG_FLAGS) {  // analysis: 1 no trace-timing events, 2 no queued heavy scan
+        if (value < 0 || value > 3) return fail(ctx, ORT_ERR_INVALID_ARG, "ORT_OPT_DEBUG_FLAGS: 0 .. 3");
         ctx->debug_flags = value;
         return ORT_OK;
     }
