@@ -829,7 +829,7 @@ def cpu_baseline(spheres, tree, p, budget_s, threads=0):
     def where(rows, geo):
         y0, bh, bs = geo
         last = y0 + ((rows - 1) // bh) * bs + (rows - 1) % bh
-        return (f"{rows} of {p.height} rows (every {bs}th from row {y0})" if bh == 1 else
+        return (f"{rows} of {p.height} rows (row stride {bs} from row {y0})" if bh == 1 else
                 f"{rows} of {p.height} rows ({bh} of every {bs}, rows {y0}..{last})")
 
     n = 2 * threads
