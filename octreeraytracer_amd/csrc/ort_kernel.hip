@@ -742,7 +742,9 @@ __device__ __forceinline__ bool trace_slot(PipeArgs& A, LdsView& L, int k, ort::
 // frames).  A first frame (pcost cleared) keeps tile order.  Scratch: the first 512 ints of the
 // frame columns (free before the walk; lds_bytes >= 2 levels).
 #ifndef ORT_COST_SHIFT
-#define ORT_COST_SHIFT 2  // bucket = steps >> shift (64 buckets)
+// bucket = steps >> shift (64 buckets): 2-step buckets since tile pairs (C3 +1.3 % in A/B over
+// 4-step ones, profiles/r04_c3_xr.log; with one tile per workgroup they measured alike)
+#define ORT_COST_SHIFT 1
 #endif
 #ifndef ORT_COST_SHIFT_DEEP
 #define ORT_COST_SHIFT_DEEP 2  // the depth 9-10 camera kernel's bucket width
