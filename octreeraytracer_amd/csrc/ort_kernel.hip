@@ -323,8 +323,11 @@ __device__ inline ort::Ray load_ray(const PipeArgs& A, int k, bool& alive) {
 #ifndef ORT_LEAF_HOLD
 #define ORT_LEAF_HOLD 12
 #endif
+// ... and only while at least this many lanes are at internal nodes: in a launch's drain (few lanes
+// left) a held leaf lane would wait for a lone internal walk -- C5 1/8 band at one frame in
+// flight 7.2 -> 8.2 ms with 1 (full frame: 16 and 1 alike)
 #ifndef ORT_LEAF_HOLD_MIN_INTERNAL
-#define ORT_LEAF_HOLD_MIN_INTERNAL 1  // ... and only while at least this many lanes are at internal nodes
+#define ORT_LEAF_HOLD_MIN_INTERNAL 16
 #endif
 #ifndef ORT_CHUNK
 #define ORT_CHUNK 64
