@@ -14,10 +14,26 @@ HOST_OBJS := $(addprefix $(OBJ)/,$(HOST_SRCS:.cpp=.o))
 HIP_OBJS := $(OBJ)/ort_kernel.o $(OBJ)/gpu_build.o $(OBJ)/group.o
 HDRS := $(wildcard $(SRC)/*.h) $(SRC)/prebuilt_scene.inc include/ort.h include/ort_math.h
 
-.PHONY: all lib oracle ref examples san clean
-all: lib oracle examples
+# The analysis library (test/analysis surface: ort_debug_* host emulation and walk statistics,
+# ORT_OPT_DEBUG_FLAGS) -- the same sources with -DORT_ANALYSIS=1; the CPU suite and tools/
+# load it, the product library does not carry it.
+ALIB := octreeraytracer_amd/lib/libort_analysis.so
+AOBJ := build/obj_analysis
+
+.PHONY: all lib analysis oracle ref examples san clean
+all: lib analysis oracle examples
 
 lib: $(LIB)
+
+analysis: $(ALIB)
+
+$(AOBJ)/%.o: $(SRC)/%.hip $(HDRS)
+	@mkdir -p $(AOBJ)
+	$(HIPCC) $(HIPFLAGS) -DORT_ANALYSIS=1 -c $< -o $@
+
+$(ALIB): $(HOST_OBJS) $(AOBJ)/ort_kernel.o $(OBJ)/gpu_build.o $(AOBJ)/group.o
+	@mkdir -p $(dir $(ALIB))
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -ldl -Wl,-soname,libort_analysis.so
 
 $(OBJ)/%.o: $(SRC)/%.cpp $(HDRS)
 	@mkdir -p $(OBJ)
@@ -72,7 +88,7 @@ $(SANOBJ)/%.o: $(SRC)/%.cpp $(HDRS)
 
 $(SANOBJ)/%.o: $(SRC)/%.hip $(HDRS) $(SRC)/gpu_build.h $(SRC)/group_map.h
 	@mkdir -p $(SANOBJ)
-	$(HIPCC) -O1 -g -std=c++17 --offload-arch=$(ARCH) -ffp-contract=off -fno-fast-math -fno-slp-vectorize -Wno-unused-result $(HIP_SAN) -c $< -o $@
+	$(HIPCC) -O1 -g -std=c++17 --offload-arch=$(ARCH) -ffp-contract=off -fno-fast-math -fno-slp-vectorize -Wno-unused-result -DORT_ANALYSIS=1 $(HIP_SAN) -c $< -o $@
 
 $(SANOBJ)/ort_oracle.o: oracle/ort_oracle.c oracle/ort_oracle.h include/ort_math.h
 	@mkdir -p $(SANOBJ)
@@ -89,5 +105,5 @@ ref:
 	$(MAKE) -C oracle ref
 
 clean:
-	rm -rf build $(LIB)
+	rm -rf build $(LIB) $(ALIB)
 	$(MAKE) -C oracle clean

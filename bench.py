@@ -119,6 +119,9 @@ def parse(argv=None):
                     help="one process drives all N GPUs through the C-ABI group (ort_group_*: a context per device, "
                     "RCCL ncclSend/ncclRecv gather over xGMI); with --rehearse-one-gpu every rank is GPU 0 and the "
                     "gather uses device copies")
+    ap.add_argument("--gather-timeout", type=float, default=120.0,
+                    help="seconds any wait on a frame's gather may take before the run exits non-zero naming the "
+                    "rank and the frame slot (process group timeout; gloo: each gather; --group: every frame wait)")
     ap.add_argument("--save", default="", help="rank 0: save the assembled frame (.pfm/.png)")
     return ap.parse_args(argv)
 
@@ -292,6 +295,15 @@ def roofline(pmc, counts, full_traversals, alg_bytes, trace_ms_avg, kernels_ran)
 
 
 def main():
+    from octreeraytracer_amd.distributed import GatherTimeout
+    try:
+        return _main()
+    except GatherTimeout as e:  # exits non-zero naming the rank and the pending slot
+        print(f"bench.py: {e}", file=sys.stderr, flush=True)
+        sys.exit(3)
+
+
+def _main():
     args = parse()
     W, H, NSPH, DEPTH, MPN, NS, MAXD = CONFIGS[args.config]
     if args.group:
@@ -317,11 +329,13 @@ def main():
     import octreeraytracer_amd as ort
 
     torch.cuda.set_device(local)
+    from datetime import timedelta
+    pg_timeout = timedelta(seconds=args.gather_timeout)  # bounds every collective (RCCL: the watchdog aborts)
     if world > 1:
         if args.rehearse_one_gpu:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=pg_timeout)
         else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=pg_timeout)
 
     spheres = ort.random_spheres(NSPH, args.seed)
     rs = [ort.Renderer(local) for _ in range(inflight)]  # one context (scene copy + stream) per frame in flight
@@ -359,7 +373,10 @@ def main():
     # renders, and frame k+1 (next context, next stream) fills the tail of frame k
     nslot = inflight + 1
     outs = [torch.empty((tile.rows, W, 3), dtype=torch.float32, device="cuda") for _ in range(nslot)]
-    gather = FrameGather(dist, W, H, world, rank, "cuda", depth=nslot)
+    # gloo: each gather's wait bounded on the host; nccl: a wait with a bound would block the host
+    # every frame, so the process group's timeout (above) bounds a stalled gather instead
+    gather = FrameGather(dist, W, H, world, rank, "cuda", depth=nslot,
+                         timeout_s=args.gather_timeout if args.rehearse_one_gpu and world > 1 else None)
     # each context's own stream (never the HIP null stream, handle 0, which the C ABI reads
     # as "no stream" and renders synchronously)
     streams = [torch.cuda.ExternalStream(x.stream_handle()) for x in rs]
@@ -467,6 +484,10 @@ def main():
         first_trace_ms = r.trace_times_ms(n_single)
         ftrace_iso = r.frame_trace_times_ms(n_single)
         trace_ms_in_flight, trace_ms = trace_ms, [m for m, _ in ftrace_iso]
+        rs[0].set_split_heavy(0)  # back to the pipelined setting of every context (main loop)
+
+    # the split-walk setting every context runs the moving-camera phase with: the main loop's
+    split_moving = 0 if inflight > 1 else -1
 
     # moving camera: the cost order and heavy-first lists deal work by the previous frame's walk
     # steps, which a static camera makes exact; an interactive caller turns the camera
@@ -560,7 +581,7 @@ def main():
                                / moving[0] / 1e6, 2),
                 "yaw_step_deg": args.yaw_step, "steps": args.moving_steps,
                 "ms_per_step": round(moving[0] / args.moving_steps * 1e3, 4),
-                "frames_in_flight": inflight,
+                "frames_in_flight": inflight, "split_heavy": split_moving,
                 "note": "the camera turns yaw_step_deg per frame (the interactive case): the per-slot walk-cost "
                         "hints that order work are one frame stale; `value` above is the static camera of the "
                         "reference's saveStats runs"},
@@ -597,6 +618,17 @@ def main():
 
 
 def group_bench(args):
+    import octreeraytracer_amd as ort
+    try:
+        return _group_bench(args)
+    except ort.OrtError as e:
+        if e.code == ort.ORT_ERR_TIMEOUT:  # the message names the frame, its slot and the pending ranks
+            print(f"bench.py --group: {e}", file=sys.stderr, flush=True)
+            sys.exit(3)
+        raise
+
+
+def _group_bench(args):
     """--group: ONE process drives N GPUs through the C-ABI group (include/ort.h ort_group_*),
     the path a caller of Raytracer::render() uses: a context per device per frame slot, the
     same 16-row band partition, the bands gathered to devices[0] by RCCL ncclSend/ncclRecv
@@ -625,6 +657,7 @@ def group_bench(args):
     spheres = ort.random_spheres(NSPH, args.seed)
     p = ort.FrameParams.default_camera(W, H, num_samples=NS, max_depth=MAXD)
     g = RenderGroup(devices, transport, inflight=inflight)
+    g.set_timeout(int(args.gather_timeout * 1000))  # a stalled frame: OrtError(ORT_ERR_TIMEOUT) names slot + ranks
     from octreeraytracer_amd import _lib as L
     for o in args.group_opt:
         name, val = o.split("=")

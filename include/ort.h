@@ -39,6 +39,8 @@ extern "C" {
 #define ORT_ERR_OUT_OF_MEMORY 4
 #define ORT_ERR_UNSUPPORTED 5
 #define ORT_ERR_INTERNAL 6
+#define ORT_ERR_TIMEOUT 7     /* a bounded wait expired (ort_group_wait: the message names the slot and the
+                                 ranks whose render or band send had not completed) */
 
 typedef struct ort_ctx ort_ctx;
 
@@ -88,8 +90,6 @@ typedef struct ort_scene_info {
                                       bounce >= 1 traces only: their incoherent rays gain from
                                       refilling idle lanes (C5 -4.5 %); 1 (every trace) was removed in
                                       round 4 (C5 -19 %): ORT_ERR_UNSUPPORTED */
-#define ORT_OPT_PACKET 5           /* removed in round 4 (the wave-level walk was SALU-bound, 1.2-1.35x
-                                      slower): ORT_ERR_UNSUPPORTED */
 #define ORT_OPT_SORT_PATHS 6       /* order of the alive paths between bounces (coherence; same pixels):
                                       2 (default) radix-sort the compacted list by direction octant +
                                       origin cell + direction; the list's length stays on the device
@@ -97,8 +97,6 @@ typedef struct ort_scene_info {
                                       frame of the same shape + 1/64 + 1024, read back asynchronously;
                                       a longer list goes on unsorted): no host wait; 1 sort every
                                       slot's key; 0 slot order */
-#define ORT_OPT_WAVE_QUEUE 7       /* removed in round 4 (the wave-level block queue traced a 1/8 band in
-                                      0.83 vs 0.61 ms): ORT_ERR_UNSUPPORTED */
 #define ORT_OPT_XCD_SWIZZLE 8      /* workgroup -> tile order (same pixels): 2 (default) each XCD renders
                                       runs of consecutive raster tiles (about 1/15 of a tile row, a power
                                       of two: 16 at 3840 px); 1: each XCD renders 128x128-pixel
@@ -146,13 +144,14 @@ typedef struct ort_scene_info {
                                       pairs on tiles of more than 2^21 pixels, or on any tile when
                                       ORT_OPT_SPLIT_HEAVY is 0 (on small tiles at one frame in flight the
                                       fewer, longer workgroups lengthen the frame's tail).  Same pixels */
-#define ORT_OPT_DEBUG_FLAGS 18     /* analysis only (tools/ab_stream.py): 1 records no per-launch trace-timing
-                                      events (ort_trace_times_ms then reports none), 2 scans the heavy
-                                      list at the start of each split frame instead of in the last
-                                      frame's exact kernel; 0 (default).  Same pixels */
-#define ORT_OPT_TILE_LPT 17        /* removed (round 4): camera-ray workgroups of each XCD in longest-first
-                                      order of last frame's walks -- C3 -25 %, 1/8 band -17 % (the order
-                                      broke the XCD's runs of neighbouring tiles); ORT_ERR_UNSUPPORTED */
+#define ORT_OPT_DEBUG_FLAGS 18     /* analysis library only (libort_analysis.so, tools/ab_stream.py): 1 records
+                                      no per-launch trace-timing events, 2 scans the heavy list at the start
+                                      of each split frame; libort.so: ORT_ERR_UNSUPPORTED */
+/* Retired option codes, reserved (ORT_ERR_UNSUPPORTED): options that lost to the defaults in
+ * A/B and were removed -- 5 the wave-level packet walk (1.2-1.35x slower),
+ * 7 the wave-level block queue (1/8 band 0.83 vs 0.61 ms), 17 longest-first workgroups
+ * (C3 -25 %).  ORT_OPT_PERSISTENT value 1 is refused likewise (C5 -19 %). */
+#define ORT_OPT_IS_RETIRED(o) ((o) == 5 || (o) == 7 || (o) == 17)
 
 /* Traffic counters (ort_count_traffic), in the REFERENCE layout's terms. */
 #define ORT_COUNT_NODES_POPPED 0
@@ -306,14 +305,23 @@ int ort_group_build_scene(ort_group* group, const float* sphere_center_radius, c
  * slots' communicators concurrently: not yet measured between distinct devices. */
 int ort_group_submit(ort_group* group, const ort_params* params, float* rgb_out, int32_t out_is_device,
                      int64_t* ticket);
-/* Wait until frame `ticket` is in rgb_out (gathered, assembled and, for host output, copied). */
+/* Wait until frame `ticket` is in rgb_out (gathered, assembled and, for host output, copied).
+ * The wait is bounded (ort_group_set_timeout): when it expires the call returns
+ * ORT_ERR_TIMEOUT and ort_group_last_error names the frame, its slot and every rank whose
+ * render / band send had not completed (or the gather and assembly on devices[0]); the frame
+ * stays submitted, so a later ort_group_wait may still see it complete. */
 int ort_group_wait(ort_group* group, int64_t ticket);
+/* The bound of every wait of the group on a frame (ort_group_wait, ort_group_render, and the
+ * wait of ort_group_submit for the frame that last used its slot), in milliseconds: default
+ * 120000; 0 = poll once (ORT_ERR_TIMEOUT unless the frame has already completed). */
+int ort_group_set_timeout(ort_group* group, int64_t timeout_ms);
 /* submit + wait for it and every earlier frame: synchronous. */
 int ort_group_render(ort_group* group, const ort_params* params, float* rgb_out, int32_t out_is_device);
 /* Device time, on devices[0], of the frame the last ort_group_wait / ort_group_render waited
  * for: from its submission on devices[0]'s stream to its assembly (renders, gather,
  * de-interleave; HIP events), taken when that frame completed -- the frame's latency, not its
- * share of a pipelined throughput. */
+ * share of a pipelined throughput.  The group keeps the times of the last 64 frames: waiting
+ * for an older ticket leaves the time unknown (ORT_ERR_NO_SCENE here). */
 int ort_group_last_frame_ms(ort_group* group, float* ms);
 
 /* ---- host scene-build stage (kept reference API, src/raytracer.cpp + src/octree.cpp) -- */

@@ -5,11 +5,11 @@ API (Sphere / Octree / GPUOctreeNode, BFS layout) is kept, and its OpenGL fragme
 tracer (shaders/octree_fragment_shader.glsl) is replaced by a hand-written HIP kernel
 behind the C ABI of include/ort.h (libort.so).
 """
-from ._lib import OrtError, lib
+from ._lib import ORT_ERR_TIMEOUT, OrtError, lib
 from .renderer import FrameParams, Renderer, Tile, algorithmic_bytes
 from .scene import (FlatOctree, SphereSet, build_octree, camera_view, debug_spheres, prebuilt_spheres,
                     random_spheres)
 
-__all__ = ["OrtError", "lib", "FrameParams", "Renderer", "Tile", "algorithmic_bytes", "FlatOctree", "SphereSet",
+__all__ = ["ORT_ERR_TIMEOUT", "OrtError", "lib", "FrameParams", "Renderer", "Tile", "algorithmic_bytes", "FlatOctree", "SphereSet",
            "build_octree", "camera_view", "debug_spheres", "prebuilt_spheres", "random_spheres"]
 __version__ = "0.1.0"

@@ -19,7 +19,9 @@
 #include <rccl/rccl.h>
 
 #include <cstring>
+#include <chrono>
 #include <mutex>
+#include <thread>
 #include <new>
 #include <string>
 #include <type_traits>
@@ -28,6 +30,10 @@
 #include "../../include/ort.h"
 #include "group_map.h"
 #include "ort_internal.h"
+
+#ifndef ORT_ANALYSIS
+#define ORT_ANALYSIS 0
+#endif
 
 namespace {
 
@@ -132,6 +138,7 @@ struct ort_group {
     long long ms_ticket[kMsRing];
     float ms_value[kMsRing];
     float last_ms = -1.0f;             // of the frame ort_group_wait / ort_group_render saw complete last
+    long long timeout_ms = 120000;     // every wait on a frame (ort_group_set_timeout)
     std::string err;
     ort_group() {
         for (int i = 0; i < kMsRing; ++i) ms_ticket[i] = -1;
@@ -209,10 +216,44 @@ int for_each_ctx(ort_group* g, F f) {
     return ORT_OK;
 }
 
+// hipSuccess when the event has completed, hipErrorNotReady while pending, else an error.
+hipError_t query(int device, hipEvent_t e) {
+    const hipError_t d = hipSetDevice(device);
+    return d != hipSuccess ? d : hipEventQuery(e);
+}
+
+// The slot's frame: wait (bounded by g->timeout_ms) until it has completed.  On expiry the
+// error names what is still pending: each rank whose render / band send has not completed
+// (its `done` event, recorded after them on its stream) and the gather + assembly on
+// devices[0] -- so a first multi-GPU run that stalls says where instead of hanging.
 int wait_slot(ort_group* g, GroupSlot& S) {
     if (S.ticket < 0) return ORT_OK;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (long long spin = 0;; ++spin) {
+        const hipError_t e = query(g->dev[0], S.finished);
+        if (e == hipSuccess) break;
+        if (e != hipErrorNotReady) GCHK(g, e);
+        const long long ms =
+            std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count();
+        if (ms >= g->timeout_ms) {
+            std::string pend;
+            for (int r = 0; r < g->n; ++r) {
+                const hipError_t q = S.done[r] ? query(g->dev[r], S.done[r]) : hipSuccess;
+                if (q == hipErrorNotReady)
+                    pend += (pend.empty() ? "" : ", ") + std::string("rank ") + std::to_string(r) + " (device " +
+                            std::to_string(g->dev[r]) + ": render" + (r > 0 && g->n > 1 ? " / band send)" : ")");
+            }
+            if (pend.empty()) pend = "the gather / assembly on device " + std::to_string(g->dev[0]);
+            (void)hipSetDevice(g->dev[0]);
+            return gfail(g, ORT_ERR_TIMEOUT, "ort_group: frame " + std::to_string(S.ticket) + " (slot " +
+                                                 std::to_string((long long)(S.ticket % (long long)g->slot.size())) +
+                                                 ") not complete after " + std::to_string(ms) + " ms; pending: " + pend);
+        }
+        // poll: yield first, then sleep in growing steps up to 1 ms (a frame takes 0.2-50 ms)
+        if (spin < 64) std::this_thread::yield();
+        else std::this_thread::sleep_for(std::chrono::microseconds(spin < 1024 ? 50 : 1000));
+    }
     GCHK(g, hipSetDevice(g->dev[0]));
-    GCHK(g, hipEventSynchronize(S.finished));
     const int i = (int)(S.ticket % ort_group::kMsRing);
     if (g->ms_ticket[i] != S.ticket) {  // first time this frame is seen complete: keep its time
         float ms = 0.0f;
@@ -403,6 +444,7 @@ int ort_group_submit(ort_group* g, const ort_params* p, float* rgb_out, int32_t 
     }
     GCHK(g, hipSetDevice(g->dev[0]));
     GCHK(g, hipEventRecord(S.rendered0, S.stream[0]));
+    GCHK(g, hipEventRecord(S.done[0], S.stream[0]));
     // 2. the one exchange: bands of ranks 1..N-1 to devices[0], received on the gather stream
     //    (each band as soon as its rank is done, also while rank 0 still renders); the slot's
     //    previous assembly ran on that stream too, so recv[] is free when they land
@@ -418,6 +460,10 @@ int ort_group_submit(ort_group* g, const ort_params* p, float* rgb_out, int32_t 
             const ncclResult_t e2 = R.groupEnd();
             if (e != ncclSuccess || e2 != ncclSuccess)
                 return gfail(g, ORT_ERR_HIP, std::string("RCCL gather: ") + R.errorString(e != ncclSuccess ? e : e2));
+            for (int r = 1; r < N; ++r) {  // each rank's render + send done (a bounded wait names the laggard)
+                GCHK(g, hipSetDevice(g->dev[r]));
+                GCHK(g, hipEventRecord(S.done[r], S.stream[r]));
+            }
         } else {
             for (int r = 1; r < N; ++r) {
                 GCHK(g, hipSetDevice(g->dev[r]));
@@ -462,7 +508,14 @@ int ort_group_wait(ort_group* g, int64_t ticket) {
         if (rc) return rc;
     }
     const int i = (int)(ticket % ort_group::kMsRing);
-    if (g->ms_ticket[i] == ticket) g->last_ms = g->ms_value[i];
+    // the ring keeps the last kMsRing frames' times: an older ticket's is gone
+    g->last_ms = g->ms_ticket[i] == ticket ? g->ms_value[i] : -1.0f;
+    return ORT_OK;
+}
+
+int ort_group_set_timeout(ort_group* g, int64_t timeout_ms) {
+    if (!g || timeout_ms < 0) return gfail(g, ORT_ERR_INVALID_ARG, "ort_group_set_timeout: null group or negative bound");
+    g->timeout_ms = timeout_ms;
     return ORT_OK;
 }
 
@@ -478,11 +531,14 @@ int ort_group_render(ort_group* g, const ort_params* p, float* rgb_out, int32_t 
 
 int ort_group_last_frame_ms(ort_group* g, float* ms) {
     if (!g || !ms) return gfail(g, ORT_ERR_INVALID_ARG, "ort_group_last_frame_ms: null argument");
-    if (g->last_ms < 0.0f) return gfail(g, ORT_ERR_NO_SCENE, "no frame completed yet (ort_group_wait)");
+    if (g->last_ms < 0.0f)
+        return gfail(g, ORT_ERR_NO_SCENE, "no frame time: none completed yet, or the last ticket waited for is more "
+                                          "than 64 frames old (ort_group_wait)");
     *ms = g->last_ms;  // taken when that frame completed (wait_slot): later submissions do not move it
     return ORT_OK;
 }
 
+#if ORT_ANALYSIS  // the analysis library only (libort_analysis.so)
 // TEST-ONLY (no GPU): the group's partition and assembly with an in-memory transport -- every
 // rank's band tile rendered by the host emulation of the kernel (ort_debug_emulate_render),
 // one after another, then assembled by the same row map the device kernel uses.
@@ -508,5 +564,7 @@ int ort_debug_group_emulate(const float* cr, const float* ma, const float* fr, i
     }
     return ORT_OK;
 }
+
+#endif  // ORT_ANALYSIS
 
 }  // extern "C"

@@ -10,6 +10,8 @@ void set_thread_error(const std::string& msg);
 const char* thread_error();
 }  // namespace ort
 
+// The ort_debug_* entry points below exist in the analysis library only (Makefile `analysis`,
+// -DORT_ANALYSIS=1: octreeraytracer_amd/lib/libort_analysis.so); libort.so exports include/ort.h.
 extern "C" {
 // TEST-ONLY: run the kernel's per-pixel code (render_core.h, compact or explicit layout)
 // on the host CPU, single-threaded, for CPU-side validation of the traversal logic

@@ -33,6 +33,19 @@
 
 #pragma clang fp contract(off)
 
+// ORT_ANALYSIS (Makefile `analysis`: octreeraytracer_amd/lib/libort_analysis.so) adds the
+// test/analysis surface: the ort_debug_* entry points (host emulation of the kernel's per-pixel
+// code for the CPU suite, walk statistics for tools/), ORT_OPT_DEBUG_FLAGS, and the per-wave
+// timeline builds (ORT_TILE_CLOCK, ORT_PERSIST_CLOCK, ORT_PERSIST_STATS).  The product library
+// libort.so is built without it and exports only include/ort.h.
+#ifndef ORT_ANALYSIS
+#define ORT_ANALYSIS 0
+#endif
+#if !ORT_ANALYSIS && ((defined(ORT_TILE_CLOCK) && ORT_TILE_CLOCK) || (defined(ORT_PERSIST_CLOCK) && ORT_PERSIST_CLOCK) || \
+                      (defined(ORT_PERSIST_STATS) && ORT_PERSIST_STATS))
+#error "per-wave timeline builds are analysis builds: add -DORT_ANALYSIS=1"
+#endif
+
 namespace {
 
 constexpr int kBlock = 256;  // 4 waves, 16x16 pixels
@@ -95,8 +108,10 @@ struct PipeArgs {
     int* hsync_next;  // the other pair: ort_trace_split zeroes it for the next frame's scan
     int hcap;
     int split_level;
+#if ORT_ANALYSIS
     ulonglong4* wclock;  // analysis builds only (ORT_PERSIST_CLOCK, ort_debug_wave_clock): per wave a timeline record
     int wclock_n;
+#endif
 };
 
 __host__ __device__ inline int tile_row_to_y(const TileMap& t, int j) {
@@ -1076,7 +1091,7 @@ __global__ void __launch_bounds__(kBlock) ort_trace_split(PipeArgs A) {
 #if ORT_TILE_CLOCK && defined(__HIP_DEVICE_COMPILE__)
         sitems += min(64 / kSplitLanes, count - base);
 #endif
-        int pos = kNoHit, entry = -1, steps = 0;
+        int pos = kNoHit, entry = -1, steps = 0, own = 0;
         float t = 0.0f;
         bool walked = false;
         ort_rng rng0;
@@ -1089,13 +1104,16 @@ __global__ void __launch_bounds__(kBlock) ort_trace_split(PipeArgs A) {
             if (alive && !A.exact_only && ort::fast_path_ok(ray, inv, 0.001f, ORT_MAXFLOAT)) {
                 walked = true;
                 ort::traverse_split<Masks>(A.S, L.planes, L.lut, ray, inv, A.split_level, kSplitLanes, j, pos, entry, t,
-                                           L.fr, steps);
+                                           L.fr, steps, own);
             } else if (alive && j == 0) {  // (a moved camera: rare) the exact kernel walks and shades it
                 A.defer_list[atomicAdd(A.sync, 1)] = k;
                 if (A.pcost) A.pcost[k] = 0;
             }
         }
-        // the group's result: the hit with the lowest DFS position
+        // the group's result: the hit with the lowest DFS position; the walk's steps as ONE walk
+        // would take them (the next frame's cost order and heavy list read them): the longest
+        // stretch above the level plus every lane's own subtree steps
+        steps -= own;
         for (int o = 1; o < kSplitLanes; o <<= 1) {
             const int op = __shfl_xor(pos, o, kSplitLanes);
             const int oe = __shfl_xor(entry, o, kSplitLanes);
@@ -1105,8 +1123,10 @@ __global__ void __launch_bounds__(kBlock) ort_trace_split(PipeArgs A) {
                 entry = oe;
                 t = ot;
             }
-            steps += __shfl_xor(steps, o, kSplitLanes);
+            steps = max(steps, __shfl_xor(steps, o, kSplitLanes));
+            own += __shfl_xor(own, o, kSplitLanes);
         }
+        steps += own;
         if (walked && j == 0) {
             if (A.pcost) A.pcost[k] = (uint16_t)min(steps, 65535);
             if constexpr (FUSE == 1) {
@@ -1320,8 +1340,10 @@ struct ort_ctx {
     int exact_only = 0;
     int refill = 16;  // ORT_OPT_REFILL: C5 (64-item chunks) 16 > 12 (-0.6 %) > 8 (-1.2 %); tools/ab_stream.py
     int persistent = 2;  // ORT_OPT_PERSISTENT: 0 off, 2 bounce >= 1 traces (default)
+#if ORT_ANALYSIS
     void* wclock = nullptr;  // ort_debug_wave_clock (ORT_PERSIST_CLOCK analysis builds)
     long long wclock_n = 0;
+#endif
     int xcd_swizzle = 2;  // ORT_OPT_XCD_SWIZZLE: workgroup -> tile order (block_tile)
     int kid_skip = 1;     // ORT_OPT_KID_SKIP: rejected-sphere skip of one-sphere leaf children (2: without nk)
     // ORT_OPT_SORT_PATHS: order of the alive paths between bounces.  2 (default): the list the
@@ -1916,6 +1938,7 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     if (!ctx->sync_ok) {
         HIPCHK(ctx, hipMemsetAsync(ctx->defer_count.p, 0, 128, s));
         ctx->sync_set = 0;
+        ctx->pre_ok = false;  // a failed render may not have listed the next frame's heavy rays
     }
     ctx->sync_ok = false;  // until this render has enqueued all its launches
     a.sync = (int*)ctx->defer_count.p;
@@ -1926,8 +1949,10 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     a.pcol = (float4*)ctx->pcol.p;
     a.out = dout;
     a.counters = dcounters;
+#if ORT_ANALYSIS
     a.wclock = (ulonglong4*)ctx->wclock;
     a.wclock_n = (int)ctx->wclock_n;
+#endif
     a.mp = ort::mortonPlan(ctx->root_lo, ctx->root_hi);
     // with bounce 0 shaded in the trace kernels every pixel's path ends in a kernel that knows
     // its pixel, so the last sample writes the final pixels itself (no finalize pass)
@@ -2020,12 +2045,14 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                 const bool prim = b == 0;
                 const int pb = (pers_bounce && b > 0) ? pblocks : 0;
                 PipeArgs at = a;
+#if ORT_ANALYSIS
                 if (pb > 0 && a.wclock) {  // analysis (ORT_PERSIST_CLOCK): a record range per launch
                     const long long nw = (long long)pb * (ctx->depth > 8 ? kPersistDeepBlock : kBlock) / 64 *
                                          (ORT_PERSIST_STATS ? 2 : 1);  // records per launch
                     at.wclock = (seg + 1) * nw <= ctx->wclock_n ? a.wclock + seg * nw : nullptr;
                     at.wclock_n = (int)nw;
                 }
+#endif
                 if (fmode == 2) {  // the trace kernels append bounce 1's list (as ort_shade_kernel would)
                     HIPCHK(ctx, hipMemsetAsync(qcnt[cur ^ 1], 0, sizeof(int), s));
                     at.qnext = qbuf[cur ^ 1];
@@ -2098,7 +2125,6 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                     at.scan_bits = (uint32_t*)ctx->hbits.p;
                     at.scan_list = (int*)ctx->hlist.p;
                     at.scan_count = (int*)ctx->hcnt.p + 8 * ctx->hpar;
-                    ctx->pre_ok = true;
                     ctx->pre_sig = fsig;
                     ctx->pre_steps = split_steps;
                 } else if (timed) {
@@ -2117,6 +2143,8 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                     else hipLaunchKernelGGL((ort_trace_exact<false, false, 0>), g, t, lds_exact, s, at);
                     if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "ort_trace_exact launch");
                     ctx->sync_set ^= 1;  // it zeroes the other set for the next launch
+                    // it listed the next frame's heavy rays: only now may that frame skip its scan
+                    if (do_split) ctx->pre_ok = true;
                 }
             }
             if (!fuse && fmode != 2) {
@@ -2313,8 +2341,6 @@ int ort_set_option(ort_ctx* ctx, int option, int value) {
         ctx->persistent = value;
         return ORT_OK;
     }
-    if (option == ORT_OPT_PACKET || option == ORT_OPT_WAVE_QUEUE)  // removed in round 4
-        return fail(ctx, ORT_ERR_UNSUPPORTED, "ORT_OPT_PACKET / ORT_OPT_WAVE_QUEUE were removed (measured slower: DESIGN.md 4)");
     if (option == ORT_OPT_KID_SKIP) {
         if (value < 0 || value > 2) return fail(ctx, ORT_ERR_INVALID_ARG, "ORT_OPT_KID_SKIP: 0, 1 or 2");
         ctx->kid_skip = value;
@@ -2350,13 +2376,21 @@ int ort_set_option(ort_ctx* ctx, int option, int value) {
         ctx->split_level = value;
         return ORT_OK;
     }
+#if ORT_ANALYSIS
     if (option == ORT_OPT_DEBUG_FLAGS) {  // analysis: 1 no trace-timing events, 2 no queued heavy scan
         if (value < 0 || value > 3) return fail(ctx, ORT_ERR_INVALID_ARG, "ORT_OPT_DEBUG_FLAGS: 0 .. 3");
         ctx->debug_flags = value;
         return ORT_OK;
     }
-    if (option == ORT_OPT_TILE_LPT)  // longest-first workgroup order: C3 -25 %, 1/8 band -17 %
-        return fail(ctx, ORT_ERR_UNSUPPORTED, "ORT_OPT_TILE_LPT (longest-first workgroups) was removed (C3 -25 %)");
+#else
+    if (option == ORT_OPT_DEBUG_FLAGS)
+        return fail(ctx, ORT_ERR_UNSUPPORTED, "ORT_OPT_DEBUG_FLAGS: analysis library only (libort_analysis.so)");
+#endif
+    if (ORT_OPT_IS_RETIRED(option))  // removed options
+        return fail(ctx, ORT_ERR_UNSUPPORTED, "option " + std::to_string(option) + " is retired (" +
+                                                  (option == 5 ? "packet walk" : option == 7 ? "wave queue"
+                                                                                             : "longest-first workgroups") +
+                                                  ": measured slower, DESIGN.md 4)");
     if (option == ORT_OPT_HEAVY_PRIO) {
         if (value < 0 || value > 65535) return fail(ctx, ORT_ERR_INVALID_ARG, "ORT_OPT_HEAVY_PRIO: 0 (off) .. 65535 steps");
         ctx->heavy_prio = value;
@@ -2563,6 +2597,8 @@ int ort_count_traffic(ort_ctx* ctx, const ort_params* params, const ort_tile* ti
     return rc;
 }
 
+#if ORT_ANALYSIS  // the analysis library only (libort_analysis.so)
+
 // ---- TEST-ONLY host emulation (see ort_internal.h) ----------------------------------
 int ort_debug_trace_rays(const float* cr, int32_t n_spheres, const float* node_min, const float* node_max,
                          const int32_t* co, const int32_t* oo, const int32_t* cnt, int32_t n_nodes, const int32_t* idx,
@@ -2670,16 +2706,17 @@ int ort_debug_split_rays(const float* cr, int32_t n_spheres, const float* node_m
             o[3] = 0;
             if (!ort::fast_path_ok(r, inv, 0.001f, ORT_MAXFLOAT)) continue;
             // the lanes of one group one after another; the lowest DFS position wins
-            int best = 0x7fffffff, be = -1, steps = 0;
+            int best = 0x7fffffff, be = -1, top = 0, owns = 0;  // steps as ort_trace_split records them
             float bt = 0.0f;
             for (int j = 0; j < lanes; ++j) {
-                int pos = 0x7fffffff, e = -1, st = 0;
+                int pos = 0x7fffffff, e = -1, st = 0, own = 0;
                 float t = 0.0f;
                 if (S.depth > 8)
-                    ort::traverse_split<ort::Masks96Split>(S, fplanes.data(), lut.data(), r, inv, level, lanes, j, pos, e, t, lf, st);
+                    ort::traverse_split<ort::Masks96Split>(S, fplanes.data(), lut.data(), r, inv, level, lanes, j, pos, e, t, lf, st, own);
                 else
-                    ort::traverse_split<ort::Masks64Split>(S, fplanes.data(), lut.data(), r, inv, level, lanes, j, pos, e, t, lf, st);
-                steps += st;
+                    ort::traverse_split<ort::Masks64Split>(S, fplanes.data(), lut.data(), r, inv, level, lanes, j, pos, e, t, lf, st, own);
+                top = std::max(top, st - own);
+                owns += own;
                 if (pos < best) {
                     best = pos;
                     be = e;
@@ -2689,7 +2726,7 @@ int ort_debug_split_rays(const float* cr, int32_t n_spheres, const float* node_m
             o[0] = be;
             o[1] = (int32_t)ort::f2u(bt);
             o[2] = best;
-            o[3] = steps;
+            o[3] = top + owns;
         }
         return ORT_OK;
     } catch (const std::exception& ex) {
@@ -3130,5 +3167,7 @@ int64_t ort_debug_walk_steps(const float* cr, const float* ma, const float* fr, 
         return fail(nullptr, ORT_ERR_INTERNAL, ex.what());
     }
 }
+
+#endif  // ORT_ANALYSIS
 
 }  // extern "C"

@@ -1343,17 +1343,22 @@ ORT_FN bool traverse_fast_t(const KScene& S, const float* planes, const uint8_t*
 // hits by their place in the DFS -- 2i + 1 for a hit inside subtree i, 2c for a hit in a leaf
 // above the level visited after c subtrees -- and the lowest `pos` of the G lanes is the result
 // of the whole walk (bit-identical: each lane's visits are the reference walk's own).
-// Returns whether this lane found a hit; steps = the nodes it visited.
+// Returns whether this lane found a hit; steps = the nodes it visited, own = those of them inside
+// its own subtrees (the rest, above the level, every lane visits up to where it stops: a single
+// walk's length is about the largest `steps - own` of the lanes plus the sum of their `own`).
 template <class Masks, class Frames>
 ORT_FN bool traverse_split(const KScene& S, const float* planes, const uint8_t* rank_lut, const Ray& r, V3 inv,
-                           int level, int G, int j, int& pos, int& hitEntry, float& hitT, Frames& fr, int& steps) {
+                           int level, int G, int j, int& pos, int& hitEntry, float& hitT, Frames& fr, int& steps,
+                           int& own) {
     FastStateT<Masks> st;
     Counters cnt;  // (COUNT = false: untouched)
     steps = 0;
+    own = 0;
     if (!fast_begin(S, planes, rank_lut, r, inv, kFastTMin, ORT_MAXFLOAT, st)) return false;
     int sub = -1, seen = 0;  // the level-`level` subtree the walk is in; how many were popped
     for (;;) {
         ++steps;
+        own += st.depth >= level ? 1 : 0;
         if (fast_visit<false>(S, rank_lut, st, fr, cnt)) {
             pos = st.depth >= level ? 2 * sub + 1 : 2 * seen;
             hitEntry = st.hitEntry;

@@ -53,6 +53,15 @@ def assemble(gathered, height: int, world: int, band: int = BAND, out=None):
     return g[:height]
 
 
+class GatherTimeout(RuntimeError):
+    """A frame's band gather did not complete within FrameGather's bound."""
+
+    def __init__(self, rank: int, slot: int, timeout_s: float, why: str = ""):
+        super().__init__(f"rank {rank}: the band gather of slot {slot} did not complete within {timeout_s} s"
+                         + (f" ({why.splitlines()[0][:200]})" if why else ""))
+        self.rank, self.slot = rank, slot
+
+
 class FrameGather:
     """Gather every rank's band tile to rank 0 and assemble the frame (torch.distributed).
 
@@ -63,9 +72,15 @@ class FrameGather:
     before finish() of that submission (bench.py double-buffers its tiles)."""
 
     def __init__(self, dist, width: int, height: int, world: int, rank: int, device, band: int = BAND,
-                 depth: int = 1):
+                 depth: int = 1, timeout_s: float | None = None):
+        """timeout_s: bound of finish()'s wait for a gather (None: the process group's own); on
+        expiry finish() raises GatherTimeout naming the rank and the slot.  (With the nccl
+        backend an async gather's wait only orders the streams: a stalled RCCL gather is
+        bounded by the process group's timeout, init_process_group(timeout=...), whose
+        watchdog aborts the process.)"""
         import torch
         self.dist, self.world, self.rank, self.height, self.band = dist, world, rank, height, band
+        self.timeout_s = timeout_s
         rows = rank_tile(width, height, rank, world, band).rows
         self.slots = [torch.empty((world, rows, width, 3), dtype=torch.float32, device=device)
                       for _ in range(depth)] if rank == 0 and world > 1 else None
@@ -93,7 +108,16 @@ class FrameGather:
         work, slot, local = handle
         if self.world == 1:
             return local[:self.height]  # nothing to gather: the tile is the frame
-        work.wait()
+        if self.timeout_s is None:
+            work.wait()
+        else:
+            from datetime import timedelta
+            try:
+                ok = work.wait(timeout=timedelta(seconds=self.timeout_s))
+            except RuntimeError as e:  # gloo raises on expiry
+                raise GatherTimeout(self.rank, slot, self.timeout_s, str(e)) from e
+            if ok is False:
+                raise GatherTimeout(self.rank, slot, self.timeout_s, "wait returned False")
         if self.rank == 0:
             assemble(self.slots[slot], self.height, self.world, self.band, out=self.frame)
             return self.frame

@@ -57,6 +57,11 @@ class RenderGroup:
         except Exception:
             pass
 
+    def set_timeout(self, ms: int):
+        """Bound of every wait on a frame (ort_group_set_timeout; 0 = poll once): an expired wait
+        raises OrtError(ORT_ERR_TIMEOUT) naming the frame, its slot and the pending ranks."""
+        self._check(self._lib.ort_group_set_timeout(self._g, int(ms)))
+
     def set_option(self, option: int, value: int):
         self._check(self._lib.ort_group_set_option(self._g, int(option), int(value)))
 
@@ -160,7 +165,7 @@ class RenderGroup:
 def emulate_group_host(spheres: SphereSet, tree: FlatOctree, params: FrameParams, world: int) -> np.ndarray:
     """TEST-ONLY (no GPU): the group's partition and row map with an in-memory transport, each
     band tile rendered by the host emulation of the kernel (ort_debug_group_emulate)."""
-    lib = L.lib()
+    lib = L.analysis_lib()
     out = np.empty((params.height, params.width, 3), np.float32)
     cr, ma, fr = (np.ascontiguousarray(a, np.float32) for a in (spheres.center_radius, spheres.mat_albedo,
                                                                   spheres.fuzz_ri))
@@ -168,7 +173,7 @@ def emulate_group_host(spheres: SphereSet, tree: FlatOctree, params: FrameParams
         (tree.node_min, np.float32), (tree.node_max, np.float32), (tree.children_offset, np.int32),
         (tree.objects_offset, np.int32), (tree.object_count, np.int32), (tree.object_indices, np.int32))]
     p = params.to_c()
-    L.check(lib.ort_debug_group_emulate(L.fptr(cr), L.fptr(ma), L.fptr(fr), spheres.n, L.fptr(t[0]), L.fptr(t[1]),
+    L.acheck(lib.ort_debug_group_emulate(L.fptr(cr), L.fptr(ma), L.fptr(fr), spheres.n, L.fptr(t[0]), L.fptr(t[1]),
                                         L.iptr(t[2]), L.iptr(t[3]), L.iptr(t[4]), tree.n_nodes, L.iptr(t[5]),
                                         tree.n_indices, int(world), C.byref(p), L.fptr(out)))
     return out

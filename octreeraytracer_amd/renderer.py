@@ -317,7 +317,7 @@ def emulate_render_host(spheres: SphereSet, tree: FlatOctree | None, params: Fra
     """TEST-ONLY: run the kernel's per-pixel code (render_core.h) on the host CPU.
     Used by the CPU test suite to validate the kernel's traversal logic against the
     independent oracle without a GPU.  ``Renderer.render`` never calls this."""
-    lib = L.lib()
+    lib = L.analysis_lib()
     tile = tile or Tile.full(params)
     out = np.empty((tile.rows, tile.width, 3), np.float32)
     counts = (C.c_uint64 * L.ORT_COUNT_N)()
@@ -334,7 +334,7 @@ def emulate_render_host(spheres: SphereSet, tree: FlatOctree | None, params: Fra
             (tree.objects_offset, np.int32), (tree.object_count, np.int32), (tree.object_indices, np.int32)))
         args = (L.fptr(keep[0]), L.fptr(keep[1]), L.iptr(keep[2]), L.iptr(keep[3]), L.iptr(keep[4]),
                 tree.n_nodes, L.iptr(keep[5]), tree.n_indices)
-    L.check(lib.ort_debug_emulate_render(L.fptr(cr), L.fptr(ma), L.fptr(fr), spheres.n, *args, layout,
+    L.acheck(lib.ort_debug_emulate_render(L.fptr(cr), L.fptr(ma), L.fptr(fr), spheres.n, *args, layout,
                                          C.byref(p), C.byref(t), L.fptr(out), counts))
     del keep
     return out, dict(zip(L.COUNT_NAMES, [int(v) for v in counts]))

@@ -86,3 +86,21 @@ def test_header_constants_match_the_bindings():
     assert not wrong, wrong
     # every option has a binding constant (the setters use them)
     assert not [k for k in missing if k.startswith("ORT_OPT_")], missing
+
+
+def test_product_library_has_no_analysis_surface(ort):
+    """libort.so exports include/ort.h and nothing of the test/analysis surface: the ort_debug_*
+    hooks (host emulation, walk statistics) live in libort_analysis.so (Makefile `analysis`,
+    -DORT_ANALYSIS=1), which the CPU suite loads."""
+    import subprocess
+    from octreeraytracer_amd import _lib
+    out = subprocess.run(["nm", "-D", "--defined-only", str(_lib.LIB_PATH)], capture_output=True, text=True,
+                         check=True).stdout
+    exported = sorted({l.split()[-1] for l in out.splitlines() if l.split()[-1].startswith("ort_")})
+    assert exported == declared_symbols(), sorted(set(exported) ^ set(declared_symbols()))
+    alib = _lib.analysis_lib()
+    for name in ("ort_debug_emulate_render", "ort_debug_group_emulate", "ort_debug_trace_rays", "ort_debug_split_rays",
+                 "ort_debug_fast_order", "ort_debug_walk_steps", "ort_debug_bounce_walks", "ort_debug_wave_stats",
+                 "ort_debug_wave_clock"):
+        assert hasattr(alib, name), name
+        assert not hasattr(ort.lib(), name), name

@@ -127,7 +127,46 @@ def _bench_line(out: str) -> dict:
     return json.loads(lines[0])
 
 
-@pytest.mark.parametrize("world", [2, 3])
+def worker_timeout(rank, world, port, q, done):
+    """Rank 1 never sends its band: rank 0's bounded finish() must raise naming rank and slot."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from octreeraytracer_amd.distributed import FrameGather, GatherTimeout
+    W, H = 8, 64
+    g = FrameGather(dist, W, H, world, rank, "cpu", depth=2, timeout_s=2.0)
+    if rank == 0:
+        local = torch.zeros((g.slots[0].shape[1], W, 3))
+        h = g.submit(local, 1)
+        try:
+            g.finish(h)
+            q.put("no timeout")
+        except GatherTimeout as e:
+            q.put(str(e))
+        done.set()
+    else:
+        done.wait(120)  # alive but sending nothing (a dead peer would end the gather with an error instead)
+    os._exit(0)  # the gather is still posted: leave without tearing the group down
+
+
+def test_gather_wait_is_bounded():
+    """FrameGather(timeout_s) bounds a frame's gather: a rank that never sends makes rank 0's
+    finish() raise GatherTimeout naming the rank and the slot (bench.py then exits 3)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    done = ctx.Event()
+    procs = [ctx.Process(target=worker_timeout, args=(r, 2, port, q, done)) for r in range(2)]
+    for p in procs:
+        p.start()
+    msg = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        if p.exitcode is None:
+            p.kill()
+    assert "rank 0" in msg and "slot 1" in msg and "within 2.0 s" in msg, msg
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_bench_self_launch(world):
     """`bench.py --gpus N` with no launcher starts its own N ranks (torch.distributed.run as a
     child process) and prints rank 0's line only; --emulate renders on the host and gathers

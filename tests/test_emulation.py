@@ -152,7 +152,7 @@ def test_walk_steps_analysis_matches_counters(ort, oracle, scene_c1):
     s, t = scene_c1
     p = ort.FrameParams.default_camera(256, 256)
     _, rc = oracle.render(s, t, p, counts=True)
-    f = L.lib().ort_debug_walk_steps
+    f = L.analysis_lib().ort_debug_walk_steps
     f.restype = C.c_int64
     fp = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
     arr = [np.ascontiguousarray(x) for x in (s.center_radius, s.mat_albedo, s.fuzz_ri)]
@@ -170,14 +170,14 @@ def test_walk_steps_analysis_matches_counters(ort, oracle, scene_c1):
 
 def _trace_rays(ort, s, t, rays, bounce):
     from octreeraytracer_amd import _lib as L
-    lib = L.lib()
+    lib = L.analysis_lib()
     arr = [np.ascontiguousarray(a, d) for a, d in (
         (s.center_radius, np.float32), (t.node_min, np.float32), (t.node_max, np.float32),
         (t.children_offset, np.int32), (t.objects_offset, np.int32), (t.object_count, np.int32),
         (t.object_indices, np.int32))]
     rays = np.ascontiguousarray(rays, np.float32)
     out = np.zeros((len(rays), 5), np.int32)
-    L.check(lib.ort_debug_trace_rays(L.fptr(arr[0]), s.n, L.fptr(arr[1]), L.fptr(arr[2]), L.iptr(arr[3]),
+    L.acheck(lib.ort_debug_trace_rays(L.fptr(arr[0]), s.n, L.fptr(arr[1]), L.fptr(arr[2]), L.iptr(arr[3]),
                                      L.iptr(arr[4]), L.iptr(arr[5]), t.n_nodes, L.iptr(arr[6]), t.n_indices,
                                      L.fptr(rays), len(rays), int(bounce), L.iptr(out)))
     return out
@@ -239,14 +239,14 @@ def test_ordinary_rays_fast_equals_exact(ort):
 
 def _split_rays(ort, s, t, rays, level, lanes):
     from octreeraytracer_amd import _lib as L
-    lib = L.lib()
+    lib = L.analysis_lib()
     arr = [np.ascontiguousarray(a, d) for a, d in (
         (s.center_radius, np.float32), (t.node_min, np.float32), (t.node_max, np.float32),
         (t.children_offset, np.int32), (t.objects_offset, np.int32), (t.object_count, np.int32),
         (t.object_indices, np.int32))]
     rays = np.ascontiguousarray(rays, np.float32)
     out = np.zeros((len(rays), 4), np.int32)
-    L.check(lib.ort_debug_split_rays(L.fptr(arr[0]), s.n, L.fptr(arr[1]), L.fptr(arr[2]), L.iptr(arr[3]),
+    L.acheck(lib.ort_debug_split_rays(L.fptr(arr[0]), s.n, L.fptr(arr[1]), L.fptr(arr[2]), L.iptr(arr[3]),
                                      L.iptr(arr[4]), L.iptr(arr[5]), t.n_nodes, L.iptr(arr[6]), t.n_indices,
                                      L.fptr(rays), len(rays), int(level), int(lanes), L.iptr(out)))
     return out
@@ -274,12 +274,22 @@ def test_split_walk_equals_the_walk(ort, oracle, n, d, m):
     want = _trace_rays(ort, s, t, rays, 0)
     fast = want[:, 0] == 1
     assert fast.mean() > 0.99
+    one = None  # the walk's own steps (one lane walks it all)
     for level in range(1, d + 1):
         for lanes in (1, 3, 8):
             got = _split_rays(ort, s, t, rays, level, lanes)
             assert np.array_equal(got[fast, 0], want[fast, 1]), (level, lanes)
             hit = want[fast, 1] >= 0
             assert np.array_equal(got[fast, 1][hit], want[fast, 2][hit]), (level, lanes)
+            # the steps ort_trace_split records for the next frame (the longest stretch above the
+            # level + the lanes' own subtree steps): the walk's own count when it misses (every
+            # lane walks to the end), at least that when a hit ends it early
+            if one is None:
+                one = got[:, 3].copy()
+            assert np.array_equal(got[fast, 3][~hit], one[fast][~hit]), (level, lanes)
+            assert (got[fast, 3] >= one[fast]).all(), (level, lanes)
+            if lanes == 1:
+                assert np.array_equal(got[:, 3], one), level
     # and the oracle's traverseOctree on a sample
     ref = oracle.trace_rays(s, t, rays[:400])
     got = _split_rays(ort, s, t, rays[:400], max(1, d - 5), 8)

@@ -179,12 +179,16 @@ def test_kernel_variants_identical(ort, oracle, renderer, scene_c2, persistent, 
 
 
 def test_removed_options_are_refused(ort, renderer):
-    """The variants removed in round 4 (packet walk, wave queue, every-trace persistent) fail
-    loudly instead of silently rendering another way."""
+    """The retired option codes (ort.h ORT_OPT_IS_RETIRED: packet walk 5, wave queue 7,
+    longest-first workgroups 17), every-trace persistent and, in the product library, the
+    analysis-only ORT_OPT_DEBUG_FLAGS fail loudly (ORT_ERR_UNSUPPORTED) instead of silently
+    rendering another way."""
     from octreeraytracer_amd import _lib as L
-    for opt, val in ((L.ORT_OPT_PACKET, 1), (L.ORT_OPT_WAVE_QUEUE, 1), (L.ORT_OPT_PERSISTENT, 1), (L.ORT_OPT_TILE_LPT, 1)):
-        with pytest.raises(ort.OrtError):
+    for opt, val in ((L.ORT_OPT_RETIRED[0], 1), (L.ORT_OPT_RETIRED[1], 1), (L.ORT_OPT_PERSISTENT, 1),
+                     (L.ORT_OPT_RETIRED[2], 1), (L.ORT_OPT_DEBUG_FLAGS, 1)):
+        with pytest.raises(ort.OrtError) as e:
             renderer._check(renderer._lib.ort_set_option(renderer._ctx, opt, val))
+        assert e.value.code == L.ORT_ERR_UNSUPPORTED, opt
 
 
 @pytest.mark.parametrize("kid_skip", [1, 2, 0])

@@ -140,3 +140,57 @@ def test_group_submit_requires_out(ort):
     g._pending = {}
     with pytest.raises(ValueError):
         g.submit(ort.FrameParams.default_camera(64, 32), None)
+
+
+@pytest.mark.gpu
+def test_group_wait_is_bounded(ort, scene_c2):
+    """ort_group_set_timeout: a wait that expires returns ORT_ERR_TIMEOUT naming the frame, its
+    slot and what is still pending (instead of blocking: a first multi-GPU run that stalls says
+    where); the frame stays submitted and a later wait sees it complete, bit-exact."""
+    from octreeraytracer_amd.group import RenderGroup
+    s, t = scene_c2
+    p = ort.FrameParams.default_camera(1920, 1080, num_samples=8, max_depth=4)  # tens of ms
+    with ort.Renderer(0) as r:
+        r.upload(s, t)
+        want = r.render(p)
+    with RenderGroup([0, 0], 1, inflight=2) as g:
+        g.upload(s, t)
+        out = np.empty((1080, 1920, 3), np.float32)
+        msgs = []
+        for _ in range(3):
+            g.set_timeout(0)  # poll once
+            tk = g.submit(p, out)
+            try:
+                g.wait(tk)
+            except ort.OrtError as e:
+                assert e.code == ort.ORT_ERR_TIMEOUT
+                msgs.append(str(e))
+            g.set_timeout(120_000)
+            g.wait(tk)
+            assert np.array_equal(out.view(np.uint32), want.view(np.uint32))
+            if msgs:
+                break
+        assert msgs, "a 8-spp 4-bounce C2 frame completed before a zero-timeout poll"
+        assert "slot" in msgs[0] and "pending" in msgs[0] and "frame" in msgs[0], msgs[0]
+
+
+@pytest.mark.gpu
+def test_group_frame_times_window(ort, scene_c1):
+    """ort_group_last_frame_ms keeps the last 64 frames' times: waiting for an older ticket
+    leaves the time unknown (an error), not an earlier frame's."""
+    from octreeraytracer_amd.group import RenderGroup
+    s, t = scene_c1
+    p = ort.FrameParams.default_camera(64, 64)
+    with RenderGroup([0], 1, inflight=2) as g:
+        g.upload(s, t)
+        outs = [np.empty((64, 64, 3), np.float32) for _ in range(3)]
+        tks = []
+        for k in range(70):
+            tks.append(g.submit(p, outs[k % 3]))
+            g.wait(tks[-1])
+        assert g.last_frame_ms() > 0
+        g.wait(tks[0])  # 70 frames ago: its time is gone
+        with pytest.raises(ort.OrtError):
+            g.last_frame_ms()
+        g.wait(tks[-2])
+        assert g.last_frame_ms() > 0

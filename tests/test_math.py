@@ -106,7 +106,7 @@ def test_kernel_closed_form_orders_match_shader_tables(ort):
     import ctypes as C
 
     from octreeraytracer_amd import _lib as L
-    lib = L.lib()
+    lib = L.analysis_lib()
     by_vec = {tuple(v): c["order"] for c in _clauses() for v in c["sign_vectors"]}
     for sx in (-1, 1):
         for sy in (-1, 1):
@@ -114,7 +114,7 @@ def test_kernel_closed_form_orders_match_shader_tables(ort):
                 m = (int(sz < 0) << 2) | (int(sx < 0) << 1) | int(sy < 0)
                 order = (C.c_int32 * 8)()
                 lut = (C.c_uint8 * 256)()
-                L.check(lib.ort_debug_fast_order(m, order, lut))
+                L.acheck(lib.ort_debug_fast_order(m, order, lut))
                 want = by_vec[(sx, sy, sz)]
                 assert list(order) == want, (sx, sy, sz)
                 # LUT row: child mask (octant space) -> reversed rank bits (rank r = bit 7 - r)
@@ -130,13 +130,13 @@ def test_rank_lut_is_a_bit_permutation(ort):
     import ctypes as C
 
     from octreeraytracer_amd import _lib as L
-    lib = L.lib()
+    lib = L.analysis_lib()
     c = np.arange(256)[:, None]
     s = np.arange(256)[None, :]
     for m in range(8):
         order = (C.c_int32 * 8)()
         lut = (C.c_uint8 * 256)()
-        L.check(lib.ort_debug_fast_order(m, order, lut))
+        L.acheck(lib.ort_debug_fast_order(m, order, lut))
         t = np.frombuffer(bytes(lut), np.uint8).astype(np.int64)
         assert sorted(int(t[1 << k]) for k in range(8)) == [1 << r for r in range(8)], m  # one rank bit each
         assert (t[c & ~s] == (t[c] & ~t[s] & 0xFF)).all(), m

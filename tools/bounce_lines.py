@@ -166,7 +166,7 @@ def main():
     print(f"{cfg}: tree {t.n_nodes} nodes built in {time.time() - t0:.0f} s", flush=True)
     lo, hi = t.node_min[0].astype(np.float64), t.node_max[0].astype(np.float64)
     p = ort.FrameParams.default_camera(W, H, num_samples=1, max_depth=MD)
-    lib = L.lib()
+    lib = L.analysis_lib()
     f = lib.ort_debug_bounce_walks
     f.restype = C.c_int
     f.argtypes = [L._fp, L._fp, L._fp, C.c_int32, L._fp, L._fp, L._ip, L._ip, L._ip, C.c_int32, L._ip, C.c_int64,

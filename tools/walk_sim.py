@@ -27,7 +27,7 @@ W, H, N, D, M, NS, MD = bench.CONFIGS[cfg]
 s = ort.random_spheres(N, 42)
 t = ort.build_octree(s, D, M)
 p = ort.FrameParams.default_camera(W, H, num_samples=NS, max_depth=MD)
-lib = L.lib()
+lib = L.analysis_lib()
 f = lib.ort_debug_walk_steps
 f.restype = C.c_int64
 fp = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731

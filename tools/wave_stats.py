@@ -21,7 +21,7 @@ W, H, N, D, M, NS, MD = bench.CONFIGS[cfg]
 s = ort.random_spheres(N, 42)
 t = ort.build_octree(s, D, M)
 p = ort.FrameParams.default_camera(W, H, num_samples=NS, max_depth=MD)
-lib = L.lib()
+lib = L.analysis_lib()
 f = lib.ort_debug_wave_stats
 f.restype = C.c_int
 st = np.zeros(18, np.float64)
