@@ -110,6 +110,10 @@ def parse(argv=None):
                     help="also time this many frames with the camera turning --yaw-step degrees per frame (reported "
                     "as moving_camera, after the main timed region; 0 = skip)")
     ap.add_argument("--yaw-step", type=float, default=0.5, help="moving_camera: degrees of yaw per frame")
+    ap.add_argument("--moving-control", type=int, default=4,
+                    help="moving_camera: also render this many poses of the turn statically (the main loop's way, "
+                    "after warm-up frames of the pose: exact hints), reported as static_same_poses (0 = skip)")
+    ap.add_argument("--control-steps", type=int, default=8, help="static_same_poses: timed frames per pose")
     ap.add_argument("--single-steps", type=int, default=10,
                     help="N > 1 with frames in flight: also time this many frames with one frame in flight "
                     "(reported as single_frame, after the main timed region; 0 = skip)")
@@ -289,6 +293,11 @@ def roofline(pmc, counts, full_traversals, alg_bytes, trace_ms_avg, kernels_ran)
         r["hbm_GBs"] = round(traffic / t / 1e9, 1)
         r["hbm_frac"] = round(traffic / t / 1e9 / HBM_PEAK_GBS, 5)
     r["pmc_trace_ms_per_frame"] = round(tr["trace_ms_per_frame"], 4)
+    # the same VALU over the profile run's own trace time (its kernel-trace summary's timed window,
+    # profiles/<name>.md): reproducible from profiles/ alone; frac above uses this run's live time
+    if tr.get("trace_ms_per_frame"):
+        r["frac_at_profile_trace_time"] = round(insts / (tr["trace_ms_per_frame"] * share * 1e-3) / 1e9
+                                                / VALU_PEAK_GINST, 4)
     if share != 1.0:
         r["pmc_scaled_by_traversal_share"] = round(share, 5)
     return r
@@ -525,6 +534,42 @@ def _main():
             if world > 1:
                 dist.all_reduce(mov_rays)
         moving = (float(t_mov.item()), None if mov_rays is None else float(mov_rays.item()))
+        # the control: poses of the turn rendered statically, each the way the main loop renders
+        # (frames in flight, a warm-up frame of the pose first: exact hints) -- moving / control
+        # isolates what one-frame-stale hints cost from what the turned view itself costs (other
+        # geometry in view)
+        ctrl = None
+        if args.moving_control > 0:
+            sel = sorted({round(i * (args.moving_steps - 1) / max(1, args.moving_control - 1))
+                          for i in range(args.moving_control)})
+            ctrl_t, ctrl_rays, kk = 0.0, 0.0, args.warmup + args.steps + args.moving_steps
+            for i in sel:
+                for _ in range(2):  # warm-up frames of the pose (the cost hints become exact)
+                    step(kk, params=poses[i])
+                    kk += 1
+                drain(0)
+                torch.cuda.synchronize()
+                if world > 1:
+                    dist.barrier()
+                torch.cuda.synchronize()
+                t3 = time.perf_counter()
+                for _ in range(args.control_steps):
+                    step(kk, params=poses[i])
+                    kk += 1
+                drain(0)
+                torch.cuda.synchronize()
+                if world > 1:
+                    dist.barrier()
+                torch.cuda.synchronize()
+                ctrl_t += time.perf_counter() - t3
+                if NS * MAXD != 1:
+                    ctrl_rays += args.control_steps * r.count_traffic(poses[i], tile)["traversals"]
+            tc = torch.tensor([ctrl_t, ctrl_rays], dtype=torch.float64, device="cuda")
+            if world > 1:
+                dist.all_reduce(tc[:1], op=dist.ReduceOp.MAX)
+                dist.all_reduce(tc[1:])
+            ctrl = (float(tc[0].item()), float(tc[1].item()) if NS * MAXD != 1 else None, len(sel))
+        moving = moving + (ctrl,)
 
     # algorithmic traffic of this rank's launch (counting variant, untimed); the traced rays
     # of a step = traversals summed over the ranks (W*H*spp for primary-only configs)
@@ -582,6 +627,14 @@ def _main():
                 "yaw_step_deg": args.yaw_step, "steps": args.moving_steps,
                 "ms_per_step": round(moving[0] / args.moving_steps * 1e3, 4),
                 "frames_in_flight": inflight, "split_heavy": split_moving,
+                "static_same_poses": None if not moving[2] else {
+                    "value": round((moving[2][1] if moving[2][1] is not None
+                                    else rays_per_frame * args.control_steps * moving[2][2]) / moving[2][0] / 1e6, 2),
+                    "poses": moving[2][2], "steps_per_pose": args.control_steps,
+                    "ms_per_step": round(moving[2][0] / (args.control_steps * moving[2][2]) * 1e3, 4),
+                    "note": "poses of the turn, each rendered statically like the main loop (frames in flight, "
+                            "after warm-up frames of the pose: exact hints); moving value / this = the price of "
+                            "one-frame-stale hints alone"},
                 "note": "the camera turns yaw_step_deg per frame (the interactive case): the per-slot walk-cost "
                         "hints that order work are one frame stale; `value` above is the static camera of the "
                         "reference's saveStats runs"},

@@ -86,39 +86,27 @@ void Octree::build(const std::vector<Sphere>& spheres, const int debug) {
     int64_t levelBase = 0;   // BFS index of cur[0]
     int64_t objectCursor = 0;
     std::vector<int> childLists[8];
+    // The reference's buildTime covers the root box and the subdivision only, not the BFS
+    // flatten (src/octree.cpp:82-85, setGPUData after it): each level here runs the
+    // subdivision (children's boxes and sphere lists) and then emits the level's records and
+    // leaf lists, and the two are timed apart -- buildTime the first, flattenTime the second.
+    double subdivideSeconds = 0.0, emitSeconds = 0.0;
+    auto t = std::chrono::steady_clock::now();
+    subdivideSeconds += std::chrono::duration<double>(t - start).count();  // root box
+    // size_t comparison like the reference (a negative maxSpheresPerNode stops at the root)
+    const size_t mcap = static_cast<size_t>(maxSpheresPerNode);
 
     for (int depth = 0; !cur.empty(); ++depth) {
         next.clear();
         nextIdx.clear();
         const int64_t nextBase = levelBase + (int64_t)cur.size();
         if (nextBase > (int64_t)INT_MAX) throw std::length_error("octree exceeds int32 node offsets");
-        int64_t splitRank = 0;
-        // size_t comparison like the reference (a negative maxSpheresPerNode stops at the root)
-        const size_t mcap = static_cast<size_t>(maxSpheresPerNode);
+        // The reference only recurses into non-empty nodes; an empty node is a leaf whatever
+        // maxSpheresPerNode says (it can only be empty below the root).
+        auto isLeaf = [&](const LevelNode& n) { return depth >= maxDepth || (size_t)n.count <= mcap || n.count == 0; };
+        // 1. subdivision: the children of every internal node of the level, in BFS order
         for (const LevelNode& n : cur) {
-            GPUOctreeNode g;
-            g.min = n.min;
-            g.max = n.max;
-            const bool stop = depth >= maxDepth || (size_t)n.count <= mcap;
-            // The reference only recurses into non-empty nodes; an empty node is a leaf
-            // whatever maxSpheresPerNode says (it can only be empty below the root).
-            if (stop || n.count == 0) {
-                g.childrenOffset = -1;
-                if (n.count > 0) {
-                    g.objectsOffset = (int)objectCursor;
-                    g.objectCount = (int)n.count;
-                    objectIndices.insert(objectIndices.end(), curIdx.begin() + n.begin,
-                                         curIdx.begin() + n.begin + n.count);
-                    objectCursor += n.count;
-                    if (objectCursor > (int64_t)INT_MAX) throw std::length_error("object index list exceeds int32");
-                } else {
-                    g.objectsOffset = -1;
-                    g.objectCount = 0;
-                }
-                if (debug) std::cout << "Stopping subdivision at depth " << depth << " with " << n.count << " objects." << std::endl;
-                flattenedTree.push_back(g);
-                continue;
-            }
+            if (isLeaf(n)) continue;
             const vec3 mid = (n.min + n.max) * 0.5f;
             vec3 cmin[8], cmax[8];
             for (int i = 0; i < 8; ++i) {
@@ -136,19 +124,47 @@ void Octree::build(const std::vector<Sphere>& spheres, const int debug) {
                 nextIdx.insert(nextIdx.end(), childLists[i].begin(), childLists[i].end());
                 next.push_back({cmin[i], cmax[i], b, (int64_t)childLists[i].size()});
             }
-            g.childrenOffset = (int)(nextBase + 8 * splitRank);
-            g.objectsOffset = -1;
-            g.objectCount = 0;
-            ++splitRank;
+        }
+        const auto t1 = std::chrono::steady_clock::now();
+        // 2. flatten: the level's records and leaf object lists
+        int64_t splitRank = 0;
+        for (const LevelNode& n : cur) {
+            GPUOctreeNode g;
+            g.min = n.min;
+            g.max = n.max;
+            if (isLeaf(n)) {
+                g.childrenOffset = -1;
+                if (n.count > 0) {
+                    g.objectsOffset = (int)objectCursor;
+                    g.objectCount = (int)n.count;
+                    objectIndices.insert(objectIndices.end(), curIdx.begin() + n.begin,
+                                         curIdx.begin() + n.begin + n.count);
+                    objectCursor += n.count;
+                    if (objectCursor > (int64_t)INT_MAX) throw std::length_error("object index list exceeds int32");
+                } else {
+                    g.objectsOffset = -1;
+                    g.objectCount = 0;
+                }
+                if (debug) std::cout << "Stopping subdivision at depth " << depth << " with " << n.count << " objects." << std::endl;
+            } else {
+                g.childrenOffset = (int)(nextBase + 8 * splitRank);
+                g.objectsOffset = -1;
+                g.objectCount = 0;
+                ++splitRank;
+            }
             flattenedTree.push_back(g);
         }
+        const auto t2 = std::chrono::steady_clock::now();
+        subdivideSeconds += std::chrono::duration<double>(t1 - t).count();
+        emitSeconds += std::chrono::duration<double>(t2 - t1).count();
+        t = t2;
         levelBase = nextBase;
         cur.swap(next);
         curIdx.swap(nextIdx);
     }
 
-    const auto finish = std::chrono::steady_clock::now();
-    buildTime = std::chrono::duration<double>(finish - start).count();
+    buildTime = subdivideSeconds;
+    flattenTime = emitSeconds;
     if (debug) std::cout << "Total build time: " << buildTime << "s" << std::endl;
 }
 

@@ -46,7 +46,10 @@ public:
     std::vector<GPUOctreeNode> flattenedTree;
     std::vector<int> objectIndices;
 
-    double buildTime = 0.0;  // seconds: subdivision + flatten (one pass here)
+    // seconds, as the reference's (src/octree.cpp:82-85): the root box and the subdivision, not
+    // the flatten -- the saveStats "Octree Build Time" column
+    double buildTime = 0.0;
+    double flattenTime = 0.0;  // seconds: emitting the BFS records and leaf lists (the reference's setGPUData)
 
     // Throws std::invalid_argument("Sphere list is empty") like the reference.
     void build(const std::vector<Sphere>& spheres, const int debug = 0);

@@ -89,9 +89,13 @@ public:
     // maxSpheresPerNode, numSamples, maxRaysDepth, width, height, min, max, avg, minFPS,
     // maxFPS, fpsAvg, buildTime) after its 2.5-sigma z-score filter (:372-434), then, when
     // `work` is given, mrays_per_s (traversals / avg frame time), bytes_per_ray (algorithmic
-    // reference-layout bytes / traversal), roofline_fraction (mrays_per_s x bytes_per_ray /
-    // 8 TB/s: SURVEY.md 8(d)'s algorithmic fraction -- it can exceed 1, the scene being
-    // cache-resident; bench.py reports the measured VALU-issue roofline), gpus, host_cores.
+    // reference-layout bytes / traversal), ref_layout_bytes_frac (mrays_per_s x bytes_per_ray /
+    // 8 TB/s: the bytes the REFERENCE's record layout would move at this ray rate, SURVEY.md
+    // 8(d)'s algorithmic figure -- not a roofline: it exceeds 1 because the compact layout never
+    // reads the reference's child records; bench.py reports the measured VALU-issue roofline),
+    // gpus, host_cores.  buildSeconds: Octree::buildTime, the root box + subdivision like the
+    // reference's column (its flatten excluded), or with gpuBuild the GPU builder's device time
+    // (one pass, the layout included: there is no separate flatten to leave out).
     // Returns "" for no frames.
     static std::string statsRow(const RaytracerConfig& cfg, const std::vector<double>& frameSeconds,
                                 double buildSeconds, const StatsWork* work);

@@ -129,22 +129,28 @@ def _bench_line(out: str) -> dict:
 
 def worker_timeout(rank, world, port, q, done):
     """Rank 1 never sends its band: rank 0's bounded finish() must raise naming rank and slot."""
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    from octreeraytracer_amd.distributed import FrameGather, GatherTimeout
-    W, H = 8, 64
-    g = FrameGather(dist, W, H, world, rank, "cpu", depth=2, timeout_s=2.0)
-    if rank == 0:
-        local = torch.zeros((g.slots[0].shape[1], W, 3))
-        h = g.submit(local, 1)
-        try:
-            g.finish(h)
-            q.put("no timeout")
-        except GatherTimeout as e:
-            q.put(str(e))
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from octreeraytracer_amd.distributed import FrameGather, GatherTimeout
+        W, H = 8, 64
+        g = FrameGather(dist, W, H, world, rank, "cpu", depth=2, timeout_s=2.0)
+        if rank == 0:
+            local = torch.zeros((g.slots[0].shape[1], W, 3))
+            h = g.submit(local, 1)
+            try:
+                g.finish(h)
+                q.put("no timeout")
+            except GatherTimeout as e:
+                q.put(str(e))
+            done.set()
+        else:
+            done.wait(120)  # alive but sending nothing (a dead peer would end the gather with an error instead)
+    except BaseException as e:  # any other failure reaches the test as its message
+        q.put(f"rank {rank} failed: {e!r}")
         done.set()
-    else:
-        done.wait(120)  # alive but sending nothing (a dead peer would end the gather with an error instead)
+    q.close()
+    q.join_thread()  # the queue's feeder thread has written the message (os._exit would drop it)
     os._exit(0)  # the gather is still posted: leave without tearing the group down
 
 

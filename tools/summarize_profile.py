@@ -43,15 +43,24 @@ if ks:
 trace_ns_total = 0.0
 trace_launches = 0
 kt = next(src.glob("trace/**/*kernel_trace.csv"), None)
+timed_stats = {}  # per kernel over bench.py's timed window only (its warm-up frames left out)
 if kt:  # the timed steps only (bench.py's warm-up frames include the cost order's first frame)
-    durs = [(float(r["Start_Timestamp"]), float(r["End_Timestamp"]) - float(r["Start_Timestamp"]))
-            for r in csv.DictReader(open(kt)) if is_trace(r["Kernel_Name"])]
-    durs.sort()
+    allk = [(float(r["Start_Timestamp"]), float(r["End_Timestamp"]), r["Kernel_Name"]) for r in csv.DictReader(open(kt))]
+    durs = sorted((t0, t1 - t0) for t0, t1, n in allk if is_trace(n))
     warm_b = bargs.get("warmup", 3)
     durs = durs[warm_b * len(durs) // bench_frames:]
     bench_frames -= warm_b
     trace_ns_total = sum(d for _, d in durs)
     trace_launches = len(durs)
+    if durs:  # the window: first timed trace launch .. end of the last trace launch
+        w0, w1 = durs[0][0], max(t0 + d for t0, d in durs)
+        per = defaultdict(list)
+        for t0, t1, n in allk:
+            if w0 <= t0 and t1 <= w1:
+                per[n].append(t1 - t0)
+        tot = sum(sum(v) for v in per.values()) or 1.0
+        timed_stats = {n: {"Calls": len(v), "AverageNs": sum(v) / len(v), "MinNs": min(v), "MaxNs": max(v),
+                           "Percentage": 100.0 * sum(v) / tot} for n, v in per.items()}
 else:  # from the stats: production trace kernels' total time
     for n, st in stats.items():
         if is_trace(n):
@@ -127,7 +136,7 @@ if trace["trace_ms_per_frame"]:
 res = {"config": cfg, "source": str(src), "lib_sha": meta.get("lib_sha", ""), "device_sha": meta.get("device_sha", ""), "frames_profiled": frames,
        "warm_frames_excluded": warm,
        "bench_frames": bench_frames, "traversals_per_frame": meta["traversals_per_frame"], "tile_rows": meta["tile_rows"],
-       "trace": trace, "kernels": kernels, "kernel_stats": stats}
+       "trace": trace, "kernels": kernels, "kernel_stats": stats, "kernel_stats_timed": timed_stats}
 dst.parent.mkdir(parents=True, exist_ok=True)
 Path(str(dst) + ".json").write_text(json.dumps(res, indent=1))
 if record:
@@ -144,7 +153,15 @@ lines = [f"# rocprofv3 summary: {src.name} ({cfg})", "",
          f"PMC passes of `tools/prof_frame.py` ({frames} frames).", "",
          "## trace kernels per frame (the roofline's kernels)", "", "| quantity | value |", "|---|---|"]
 lines += [f"| {k} | {v:.6g} |" if isinstance(v, float) else f"| {k} | {v} |" for k, v in trace.items()]
-lines += ["", "## kernel stats (kernel trace of bench.py)", "",
+if timed_stats:
+    lines += ["", f"## kernel stats over the timed window ({bench_frames} frames of bench.py, warm-up frames left out)",
+              "", "The window the roofline's kernel time comes from: `trace_ms_per_frame` above is the sum of these "
+              "trace kernels' averages x launches per frame.", "",
+              "| kernel | calls | avg ns | min ns | max ns | % |", "|---|---|---|---|---|---|"]
+    for n, st in sorted(timed_stats.items(), key=lambda kv: -kv[1]["Percentage"]):
+        lines.append(f"| `{short(n)[:90]}` | {st['Calls']} | {st['AverageNs']:.0f} | {st['MinNs']:.0f} | "
+                     f"{st['MaxNs']:.0f} | {st['Percentage']:.2f} |")
+lines += ["", "## kernel stats over the whole run (rocprofv3 --stats: warm-up frames, the counting pass included)", "",
           "| kernel | calls | avg ns | min ns | max ns | % |", "|---|---|---|---|---|---|"]
 for n, st in sorted(stats.items(), key=lambda kv: -float(kv[1]["Percentage"])):
     lines.append(f"| `{short(n)[:90]}` | {st['Calls']} | {float(st['AverageNs']):.0f} | {st['MinNs']} | {st['MaxNs']} | "

@@ -36,7 +36,7 @@ REF_COLUMNS = ["Uses Octree", "Spheres", "Max Octree Depth", "Min Spheres Per No
                "Avg FPS", "Octree Build Time"]
 # the reference's older files (analysis/stats.csv, stats_2.csv): no per-node count, no build time
 REF_COLUMNS_13 = [c for c in REF_COLUMNS if c not in ("Min Spheres Per Node", "Octree Build Time")]
-EXT_COLUMNS = ["mrays_per_s", "bytes_per_ray", "roofline_fraction", "gpus", "host_cores"]
+EXT_COLUMNS = ["mrays_per_s", "bytes_per_ray", "ref_layout_bytes_frac", "gpus", "host_cores"]
 INT_COLUMNS = {"Uses Octree", "Spheres", "Max Octree Depth", "Min Spheres Per Node", "Num Samples", "Max Rays Depth",
                "Screen Width", "Screen Height", "gpus", "host_cores"}
 
