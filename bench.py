@@ -117,8 +117,9 @@ def parse(argv=None):
     ap.add_argument("--single-steps", type=int, default=10,
                     help="N > 1 with frames in flight: also time this many frames with one frame in flight "
                     "(reported as single_frame, after the main timed region; 0 = skip)")
-    ap.add_argument("--group-opt", action="append", default=[], metavar="NAME=VALUE",
-                    help="--group: ort_group_set_option(ORT_OPT_<NAME>, VALUE) on every context (A/B)")
+    ap.add_argument("--opt", "--group-opt", dest="group_opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="ort_set_option(ORT_OPT_<NAME>, VALUE) on every context, after bench.py's own settings "
+                    "(A/B; recorded in the line's config)")
     ap.add_argument("--group", action="store_true",
                     help="one process drives all N GPUs through the C-ABI group (ort_group_*: a context per device, "
                     "RCCL ncclSend/ncclRecv gather over xGMI); with --rehearse-one-gpu every rank is GPU 0 and the "
@@ -375,6 +376,12 @@ def _main():
         for x in rs:
             x.set_split_heavy(0)
 
+    from octreeraytracer_amd import _lib as L
+    for o in args.group_opt:  # A/B options, after the settings above
+        name, val = o.split("=")
+        for x in rs:
+            x._check(x._lib.ort_set_option(x._ctx, getattr(L, "ORT_OPT_" + name.upper()), int(val)))
+
     # partition: 16-row bands dealt round-robin; every rank renders the same number of rows
     from octreeraytracer_amd.distributed import FrameGather, rank_tile
     tile = rank_tile(W, H, rank, world)
@@ -604,7 +611,8 @@ def _main():
                             f"octree depth {DEPTH}, maxSpheresPerNode {MPN}",
                 "width": W, "height": H, "spheres": NSPH, "octree_depth": DEPTH, "max_spheres_per_node": MPN,
                 "num_samples": NS, "max_bounces": MAXD, "nodes": info["n_nodes"], "indices": info["n_indices"],
-                "layout": info["layout"], "partition": "16-row bands round-robin + RCCL gather (async, "
+                "layout": info["layout"], "options": args.group_opt or None,
+                "partition": "16-row bands round-robin + RCCL gather (async, "
                 "overlapping the next frame's render)" if world > 1
                 else "full frame", "frames_in_flight": inflight, "rays_per_step": rays_per_frame, "rays": "traced rays (octree traversals), "
                 "all bounces and ranks",

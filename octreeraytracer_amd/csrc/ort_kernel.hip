@@ -2073,7 +2073,7 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                  std::memcmp(&ctx->cost_cam, &a.pp.cam, sizeof(ort::KCamera)) != 0;
         if (reproj) {
             if ((rc = ensure(ctx, ctx->pproj, 2 * slots)) || (rc = ensure(ctx, ctx->rmap, 4 * slots))) return rc;
-            a.pcost_r = (const uint16_t*)ctx->pproj.p;
+            if (ctx->reproject == 1) a.pcost_r = (const uint16_t*)ctx->pproj.p;  // (2: analysis, the kernel's cost only)
         }
     }
     // split walks of the heavy camera rays (1 sample; the production kernels, bounce 0)
@@ -2103,7 +2103,7 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
         }
         bcost = (uint16_t*)ctx->bcost.p;
         a.heavy = ctx->heavy_first;
-        if (reproj) a.rmap = (const int*)ctx->rmap.p;  // the bounce costs through the same slot map
+        if (reproj && ctx->reproject == 1) a.rmap = (const int*)ctx->rmap.p;  // the bounce costs through the same slot map
     }
     const int key_bits = bcost ? ort::kPathKeyBits + kHeavyKeyBits : ort::kPathKeyBits;
     const size_t lds = lds_bytes(mode, ctx->depth, false);
@@ -2517,7 +2517,7 @@ int ort_set_option(ort_ctx* ctx, int option, int value) {
         return ORT_OK;
     }
     if (option == ORT_OPT_REPROJECT) {
-        if (value < 0 || value > 1) return fail(ctx, ORT_ERR_INVALID_ARG, "ORT_OPT_REPROJECT: 0 or 1");
+        if (value < 0 || value > (ORT_ANALYSIS ? 2 : 1)) return fail(ctx, ORT_ERR_INVALID_ARG, "ORT_OPT_REPROJECT: 0 or 1");
         ctx->reproject = value;
         return ORT_OK;
     }

@@ -9,6 +9,10 @@ walks the same arrays; a 239 M-node host build would take ~21 s.  The frame is c
 64 rows spread over its height (four 16-row bands) and on a ragged sub-tile, with the frame's
 own resolution, camera and bounce depth.  Bar: bit-exact.
 """
+import hashlib
+import json
+from pathlib import Path
+
 import numpy as np
 import pytest
 
@@ -17,6 +21,14 @@ from test_gpu_parity import assert_same
 pytestmark = pytest.mark.gpu
 
 C5 = dict(width=7680, height=4320, spheres=1_000_000, depth=10, mspn=1, bounces=4)
+MANIFEST = json.loads((Path(__file__).resolve().parent / "golden" / "manifest.json").read_text())
+
+
+def _sha(*arrays):
+    h = hashlib.sha256()
+    for a in arrays:
+        h.update(np.ascontiguousarray(a).tobytes())
+    return h.hexdigest()
 
 
 @pytest.fixture(scope="module")
@@ -26,6 +38,13 @@ def c5(ort):
     r.build_scene(s, C5["depth"], C5["mspn"], keep_tree=True)
     info = r.info()
     t = r.export_octree()
+    # the GPU-built tree IS the reference builder's (src/octree.cpp run on the same 1M spheres:
+    # tools/hash_ref_tree.py): checked before the oracle walks it, so a builder error cannot
+    # hide behind an oracle walking the same wrong tree
+    ref = MANIFEST["trees"]["rand1M_d10_m1"]
+    assert _sha(s.center_radius, s.mat_albedo, s.fuzz_ri) == ref["spheres"]["sha256"], "C5 sphere set"
+    assert (t.n_nodes, t.n_indices) == (ref["nodes"], ref["indices"])
+    assert _sha(t.gpu_records(), t.object_indices) == ref["sha256"], "C5 GPU tree differs from the reference builder's"
     yield s, t, r, info
     r.close()
 
@@ -41,6 +60,8 @@ def _tiles():
 
 
 def test_c5_tree_is_the_reference_tree(c5):
+    """The fixture asserted the exported tree's SHA-256 against the reference builder's
+    (manifest rand1M_d10_m1); here the counts and layout."""
     _, t, _, info = c5
     # SURVEY.md 8(d): the reference builder's counts for 1M spheres, depth 10, M=1
     assert info["n_nodes"] == 239_220_401 and info["n_indices"] == 172_356_841

@@ -126,3 +126,15 @@ def test_builder_matches_live_reference(ort, oracle, n, d, m, seed):
     rec, idx, _ = oracle.ref_build_octree(s.center_radius, d, m)
     t = ort.build_octree(s, d, m)
     assert np.array_equal(t.gpu_records(), rec) and np.array_equal(t.object_indices, idx)
+
+
+def test_c5_reference_tree_pin(ort):
+    """The C5 tree's pin (1M spheres, depth 10, maxSpheresPerNode 1):
+    the reference builder's SHA-256 and counts (tools/hash_ref_tree.py), taken over THIS sphere
+    set -- its hash is the generator's output here -- which tests/test_gpu_c5.py asserts the
+    GPU-built tree against."""
+    e = MANIFEST["trees"]["rand1M_d10_m1"]
+    assert e["hash_only"] and (e["nodes"], e["indices"]) == (239_220_401, 172_356_841)
+    assert len(e["sha256"]) == 64
+    s = ort.random_spheres(e["spheres"]["n"], e["spheres"]["seed"])
+    assert sha(s.center_radius, s.mat_albedo, s.fuzz_ri) == e["spheres"]["sha256"]
