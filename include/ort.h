@@ -144,11 +144,6 @@ typedef struct ort_scene_info {
                                       pairs on tiles of more than 2^21 pixels, or on any tile when
                                       ORT_OPT_SPLIT_HEAVY is 0 (on small tiles at one frame in flight the
                                       fewer, longer workgroups lengthen the frame's tail).  Same pixels */
-#define ORT_OPT_REPROJECT 19        /* 1 (default): when the camera moved since the frame whose walk costs
-                                      the cost order, heavy priority, split walks and heavy-first lists
-                                      read, those costs are first reprojected to the new pixels (the
-                                      pixel-centre ray into the last frame's image: exact for a turned
-                                      camera); 0: read them where they were recorded.  Same pixels */
 #define ORT_OPT_DEBUG_FLAGS 18     /* analysis library only (libort_analysis.so, tools/ab_stream.py): 1 records
                                       no per-launch trace-timing events, 2 scans the heavy list at the start
                                       of each split frame; libort.so: ORT_ERR_UNSUPPORTED */

@@ -93,11 +93,6 @@ struct PipeArgs {
     float* out;
     unsigned long long* counters;
     uint16_t* pcost;  // ORT_OPT_COST_ORDER: per slot, the walk steps of its last camera ray, or null
-    // ... the costs the cost order, heavy priority and heavy scan READ: pcost itself, or, after a
-    // camera move (ORT_OPT_REPROJECT), last frame's costs reprojected to this frame's pixels
-    // (k_cost_reproject) -- the walks write pcost, which other workgroups must not read meanwhile
-    const uint16_t* pcost_r;
-    const int* rmap;  // ... and the reprojection's slot map, through which bcost_r is read (or null)
     uint16_t* bcost_w;        // ORT_OPT_HEAVY_FIRST: the persistent bounce trace records each walk's steps here
     const uint16_t* bcost_r;  // ... the kernels appending the next bounce's list read that bounce's last-frame steps
     int heavy;                // ... walks of at least this many steps are heavy: they sort first
@@ -281,90 +276,6 @@ __host__ __device__ inline bool slot_coords(const PipeArgs& A, int k, int& col, 
     col = bx * 16 + (wave & 1) * 8 + (lane & 7);  // an 8x8 block per wave (16x4 and 4x16: no faster, §8)
     row = by * 16 + (wave >> 1) * 8 + (lane >> 3);
     return col < A.tm.tw && row < A.tm.th;
-}
-
-// The inverse of slot_coords: the path slot of tile pixel (col, row), for the dispatch orders
-// the reprojection supports (raster, XCD runs; tile pairs or not) -- checked slot by slot against
-// slot_coords on the host (ort_debug_slot_map, tests/test_emulation.py).
-__host__ __device__ inline int block_of_tile_grid(const PipeArgs& A, int bx, int by) {
-    const int l = by * A.tilesX + bx;
-    if (A.swizzle != 2) return l;
-    const int lr = A.xrun_log2, run = 1 << lr, group = 8 << lr;
-    if ((l | (group - 1)) >= A.tilesX * A.tilesY) return l;  // a last partial group keeps raster order
-    return (l & ~(group - 1)) | ((l & (run - 1)) << 3) | ((l >> lr) & 7);
-}
-__host__ __device__ inline int pixel_slot(const PipeArgs& A, int col, int row) {
-    const int bx = col >> 4, by = row >> 4;
-    const int blk = A.pair ? 2 * block_of_tile_grid(A, bx >> 1, by) + (bx & 1) : block_of_tile_grid(A, bx, by);
-    const int wave = ((row & 15) >> 3) * 2 + ((col & 15) >> 3), lane = ((row & 7) << 3) | (col & 7);
-    return blk * kBlock + wave * 64 + lane;
-}
-// The tile row nearest to frame row y (a band tile holds bands of bh rows every bs rows).
-__host__ __device__ inline int tile_row_near(const TileMap& t, int y) {
-    int j;
-    if (t.bh > 0) {
-        const int rel = y - t.y0;
-        int band = rel >= 0 ? rel / t.bs : -((-rel + t.bs - 1) / t.bs);
-        int off = rel - band * t.bs;
-        if (off >= t.bh) {  // between two of the tile's bands: the nearer one's edge row
-            if (off - (t.bh - 1) <= t.bs - off) off = t.bh - 1;
-            else {
-                band += 1;
-                off = 0;
-            }
-        }
-        j = band * t.bh + off;
-    } else {
-        j = y - t.y0;
-    }
-    return j < 0 ? 0 : (j >= t.th ? t.th - 1 : j);
-}
-
-// Cost reprojection (ORT_OPT_REPROJECT): after the camera moved, slot k's cost hint is the cost
-// last frame recorded for the pixel that saw this pixel's direction -- the pixel-centre ray of
-// this frame's camera projected into last frame's image (exact for a camera that turned; a moved
-// camera's parallax is ignored).  Off the tile or behind last frame's camera: no hint (0).  Only
-// which lane walks which slot, and which paths sort first, follow from these: same pixels.
-struct Reproject {
-    ort::KCamera prev;      // the camera of the frame whose costs src holds
-    const uint16_t* src;    // last frame's pcost
-    uint16_t* dst;          // this frame's pcost_r
-    int* rmap;              // this frame's slot -> last frame's slot (bcost reads), or null
-    int n;
-};
-__host__ __device__ inline int reproject_slot(const PipeArgs& A, const Reproject& R, int k) {
-    int col, row;
-    if (!slot_coords<0>(A, k, col, row)) return -1;
-    const int X = A.tm.x0 + col, Y = tile_row_to_y(A.tm, row);
-    if (Y >= A.pp.H) return -1;  // a band tile's padding row
-    const ort::KCamera& c = A.pp.cam;
-    const float sx = ((float)X + 0.5f) / (float)A.pp.W, sy = ((float)Y + 0.5f) / (float)A.pp.H;
-    ort::V3 d;
-    d.x = c.lowerLeft.x + sx * c.horizontal.x + sy * c.vertical.x - c.origin.x;
-    d.y = c.lowerLeft.y + sx * c.horizontal.y + sy * c.vertical.y - c.origin.y;
-    d.z = c.lowerLeft.z + sx * c.horizontal.z + sy * c.vertical.z - c.origin.z;
-    const ort::KCamera& p = R.prev;
-    const ort::V3 ll = ort::mk(p.lowerLeft.x - p.origin.x, p.lowerLeft.y - p.origin.y, p.lowerLeft.z - p.origin.z);
-    const float dw = ort::dot(d, p.w), lw = ort::dot(ll, p.w);
-    if (!(dw * lw > 0.0f)) return -1;  // behind (or level with) last frame's image plane
-    const float lam = lw / dw;
-    const ort::V3 q = ort::mk(lam * d.x - ll.x, lam * d.y - ll.y, lam * d.z - ll.z);
-    float s2 = ort::dot(q, p.horizontal) / ort::dot(p.horizontal, p.horizontal);
-    float t2 = ort::dot(q, p.vertical) / ort::dot(p.vertical, p.vertical);
-    s2 = fminf(fmaxf(s2, -1.0f), 2.0f);  // (NaN -> -1: no overflow in the conversions below)
-    t2 = fminf(fmaxf(t2, -1.0f), 2.0f);
-    const int X2 = (int)floorf(s2 * (float)A.pp.W), Y2 = (int)floorf(t2 * (float)A.pp.H);
-    if (X2 < 0 || X2 >= A.pp.W || Y2 < 0 || Y2 >= A.pp.H) return -1;  // outside last frame's image
-    int col2 = X2 - A.tm.x0;
-    col2 = col2 < 0 ? 0 : (col2 >= A.tm.tw ? A.tm.tw - 1 : col2);
-    return pixel_slot(A, col2, tile_row_near(A.tm, Y2));
-}
-__global__ void __launch_bounds__(kBlock) k_cost_reproject(PipeArgs A, Reproject R) {
-    const int k = (int)(blockIdx.x * kBlock + threadIdx.x);
-    if (k >= R.n) return;
-    const int k2 = reproject_slot(A, R, k);
-    R.dst[k] = k2 >= 0 ? R.src[k2] : (uint16_t)0;
-    if (R.rmap) R.rmap[k] = k2 >= 0 ? k2 : k;
 }
 
 template <bool COUNT>
@@ -752,9 +663,9 @@ static_assert(ORT_HEAVY_LEVELS >= 1 && ORT_HEAVY_LEVELS <= 7, "ORT_HEAVY_LEVELS:
 constexpr int kHeavyKeyBits = ORT_HEAVY_LEVELS > 3 ? 3 : (ORT_HEAVY_LEVELS > 1 ? 2 : 1);
 // the class sits above the path key's bits in a 32-bit radix key (sortListBounded's end bit)
 static_assert(ort::kPathKeyBits + kHeavyKeyBits <= 32, "heavy-first class bits + path key bits exceed 32");
-__device__ __forceinline__ uint32_t light_bit(const uint16_t* bcost_r, const int* rmap, int heavy, int k) {
+__device__ __forceinline__ uint32_t light_bit(const uint16_t* bcost_r, int heavy, int k) {
     if (!bcost_r) return 0u;
-    const int c = bcost_r[rmap ? rmap[k] : k];  // (rmap: the slot this one's pixel was last frame)
+    const int c = bcost_r[k];
     uint32_t cls = ORT_HEAVY_LEVELS;
     for (int l = 0; l < ORT_HEAVY_LEVELS; ++l) cls -= c >= (heavy << (ORT_HEAVY_RATIO_LOG2 * l)) ? 1u : 0u;
     return cls << ort::kPathKeyBits;
@@ -991,12 +902,12 @@ __device__ __forceinline__ void trace_compact_body(PipeArgs& A, unsigned char* s
     LdsView L = setup_lds<true>(smem, A.S);
     int k = blockIdx.x * kBlock + threadIdx.x;
     if (PRIMARY && !COUNT && A.pcost) {  // (the counting pass: tile order)
-        k = cost_order_slot<DEEP ? ORT_COST_SHIFT_DEEP : ORT_COST_SHIFT>(A.pcost_r, L.fr.co, k);
+        k = cost_order_slot<DEEP ? ORT_COST_SHIFT_DEEP : ORT_COST_SHIFT>(A.pcost, L.fr.co, k);
 #if defined(__HIP_DEVICE_COMPILE__)
         // heavy priority: the few waves holding the frame's longest walks start with the first
         // workgroups but, sharing their SIMD with 7 others, finish long after the rest of a small
         // tile (tools/tile_clock.py); they get the SIMD's issue slots first
-        if (A.prio_steps > 0 && __ballot((int)A.pcost_r[k] >= A.prio_steps)) __builtin_amdgcn_s_setprio(3);
+        if (A.prio_steps > 0 && __ballot((int)A.pcost[k] >= A.prio_steps)) __builtin_amdgcn_s_setprio(3);
 #endif
     }
     if (!PRIMARY && !list_slot(A, k)) return;
@@ -1010,7 +921,7 @@ __device__ __forceinline__ void trace_compact_body(PipeArgs& A, unsigned char* s
         KernArgs* kp = (KernArgs*)__builtin_amdgcn_kernarg_segment_ptr();
         uint32_t key = 0;
         if (go && kp->qnext_keys)  // the state just stored
-            key = ort::path_key(kp->po[k], kp->pd[k], kp->mp, kp->key_spread) | light_bit(kp->bcost_r, kp->rmap, kp->heavy, k);
+            key = ort::path_key(kp->po[k], kp->pd[k], kp->mp, kp->key_spread) | light_bit(kp->bcost_r, kp->heavy, k);
         append_slots(go, k, key, kp->qnext, kp->qnext_keys, kp->qnext_count);
 #endif
     }
@@ -1032,7 +943,7 @@ __device__ __forceinline__ void trace_pair_body(PipeArgs& A, unsigned char* smem
     LdsView L0 = setup_lds<true>(smem, A.S);
     const int base = blockIdx.x * (2 * kBlock);
     int kk0 = base + threadIdx.x, kk1 = kk0 + kBlock;
-    if (!COUNT && A.pcost) cost_order_pair<DEEP ? ORT_COST_SHIFT_DEEP : ORT_COST_SHIFT>(A.pcost_r, L0.fr.co, base, kk0, kk1);
+    if (!COUNT && A.pcost) cost_order_pair<DEEP ? ORT_COST_SHIFT_DEEP : ORT_COST_SHIFT>(A.pcost, L0.fr.co, base, kk0, kk1);
     ort::Counters cnt;
     for (int q = 0; q < 6; ++q) cnt.v[q] = 0;
 #pragma unroll
@@ -1050,7 +961,7 @@ __device__ __forceinline__ void trace_pair_body(PipeArgs& A, unsigned char* smem
 #if defined(__HIP_DEVICE_COMPILE__)
         asm volatile("" : "+v"(k));
         if (!COUNT && A1.pcost && A1.prio_steps > 0) {  // heavy priority, per block
-            if (__ballot((int)A1.pcost_r[k] >= A1.prio_steps)) __builtin_amdgcn_s_setprio(3);
+            if (__ballot((int)A1.pcost[k] >= A1.prio_steps)) __builtin_amdgcn_s_setprio(3);
             else __builtin_amdgcn_s_setprio(0);
         }
 #endif
@@ -1061,7 +972,7 @@ __device__ __forceinline__ void trace_pair_body(PipeArgs& A, unsigned char* smem
             KernArgs* kq = (KernArgs*)__builtin_amdgcn_kernarg_segment_ptr();
             uint32_t key = 0;
             if (go && kq->qnext_keys)
-                key = ort::path_key(kq->po[k], kq->pd[k], kq->mp, kq->key_spread) | light_bit(kq->bcost_r, kq->rmap, kq->heavy, k);
+                key = ort::path_key(kq->po[k], kq->pd[k], kq->mp, kq->key_spread) | light_bit(kq->bcost_r, kq->heavy, k);
             append_slots(go, k, key, kq->qnext, kq->qnext_keys, kq->qnext_count);
 #endif
         }
@@ -1227,7 +1138,7 @@ __global__ void __launch_bounds__(kBlock) ort_trace_split(PipeArgs A) {
                     const int q = atomicAdd(A.qnext_count, 1);
                     A.qnext[q] = k;
                     if (A.qnext_keys)
-                        A.qnext_keys[q] = ort::path_key(A.po[k], A.pd[k], A.mp, A.key_spread) | light_bit(A.bcost_r, A.rmap, A.heavy, k);
+                        A.qnext_keys[q] = ort::path_key(A.po[k], A.pd[k], A.mp, A.key_spread) | light_bit(A.bcost_r, A.heavy, k);
                 }
             }
         }
@@ -1302,7 +1213,7 @@ __global__ void __launch_bounds__(kBlock) ort_trace_exact(PipeArgs A) {
                 const int pos = atomicAdd(A.qnext_count, 1);
                 A.qnext[pos] = k;
                 if (A.qnext_keys)
-                    A.qnext_keys[pos] = ort::path_key(A.po[k], A.pd[k], A.mp, A.key_spread) | light_bit(A.bcost_r, A.rmap, A.heavy, k);
+                    A.qnext_keys[pos] = ort::path_key(A.po[k], A.pd[k], A.mp, A.key_spread) | light_bit(A.bcost_r, A.heavy, k);
             }
         } else {
             A.hit[k] = make_int2(st == ORT_TRACE_HIT ? entry : -1, __float_as_int(t));
@@ -1369,7 +1280,7 @@ __global__ void __launch_bounds__(kBlock) ort_shade_kernel(PipeArgs A) {
     if (!DIRECT && A.qnext) {
         uint32_t key = 0;
         if (go && A.qnext_keys)  // the state just stored
-            key = ort::path_key(A.po[k], A.pd[k], A.mp, A.key_spread) | light_bit(A.bcost_r, A.rmap, A.heavy, k);
+            key = ort::path_key(A.po[k], A.pd[k], A.mp, A.key_spread) | light_bit(A.bcost_r, A.heavy, k);
         append_slots(go, k, key, A.qnext, A.qnext_keys, A.qnext_count);
     }
 }
@@ -1462,13 +1373,6 @@ struct ort_ctx {
     int cost_order = 1;
     DevBuf pcost;
     unsigned long long cost_sig = 0;
-    // ORT_OPT_REPROJECT (default 1): when the camera moved since the frame whose costs pcost
-    // holds (cost_cam), the hints are reprojected to this frame's pixels (k_cost_reproject into
-    // pproj, the slot map into rmap for the bounce costs)
-    int reproject = 1;
-    ort::KCamera cost_cam{};
-    bool cost_cam_ok = false;
-    DevBuf pproj, rmap;
     // ORT_OPT_HEAVY_FIRST: threshold in walk steps (0 off); bcost holds, per bounce >= 1 of the
     // first kCostBounces of a frame, every slot's last walk steps (cleared with cost_sig)
     static constexpr int kCostBounces = 8;
@@ -2055,26 +1959,15 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     a.final_out = fuse_first ? 1 : 0;
     a.key_spread = (const uint32_t*)ctx->key_spread.p;
     // the cost order: the per-workgroup camera-ray kernels (ort_trace_compact[_deep]) only
-    bool reproj = false;
-    ort::KCamera prev_cam = ctx->cost_cam;
     if (mode == 0 && ctx->cost_order && ctx->depth >= 2) {
         if ((rc = ensure(ctx, ctx->pcost, 2 * slots))) return rc;
         const unsigned long long sig = frame_sig(ctx, p, t);
         if (sig != ctx->cost_sig) {  // a new shape: tile order for the first frame
             HIPCHK(ctx, hipMemsetAsync(ctx->pcost.p, 0, 2 * slots, s));
             ctx->cost_sig = sig;
-            ctx->cost_cam_ok = false;
         }
         a.pcost = (uint16_t*)ctx->pcost.p;
-        a.pcost_r = a.pcost;
         a.prio_steps = ctx->heavy_prio;
-        // a moved camera: the hints follow the pixels (k_cost_reproject, launched below)
-        reproj = ctx->reproject && ctx->cost_cam_ok && ctx->xcd_swizzle != 1 && !dcounters &&
-                 std::memcmp(&ctx->cost_cam, &a.pp.cam, sizeof(ort::KCamera)) != 0;
-        if (reproj) {
-            if ((rc = ensure(ctx, ctx->pproj, 2 * slots)) || (rc = ensure(ctx, ctx->rmap, 4 * slots))) return rc;
-            if (ctx->reproject == 1) a.pcost_r = (const uint16_t*)ctx->pproj.p;  // (2: analysis, the kernel's cost only)
-        }
     }
     // split walks of the heavy camera rays (1 sample; the production kernels, bounce 0)
     const int split_steps = ctx->split_steps >= 0 ? ctx->split_steps
@@ -2103,7 +1996,6 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
         }
         bcost = (uint16_t*)ctx->bcost.p;
         a.heavy = ctx->heavy_first;
-        if (reproj && ctx->reproject == 1) a.rmap = (const int*)ctx->rmap.p;  // the bounce costs through the same slot map
     }
     const int key_bits = bcost ? ort::kPathKeyBits + kHeavyKeyBits : ort::kPathKeyBits;
     const size_t lds = lds_bytes(mode, ctx->depth, false);
@@ -2120,16 +2012,6 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     const bool start_is_tr0 = maxd > 0 && !(ctx->debug_flags & 1);
     ctx->ev0_last = start_is_tr0 ? ctx->tr0[fslot][0] : ctx->ev0;
     HIPCHK(ctx, hipEventRecord(ctx->ev0_last, s));
-    if (reproj) {  // inside the frame (and its first trace launch's timing)
-        const Reproject R{prev_cam, (const uint16_t*)ctx->pcost.p, (uint16_t*)ctx->pproj.p, (int*)ctx->rmap.p,
-                          (int)slots};
-        hipLaunchKernelGGL(k_cost_reproject, dim3((unsigned)((slots + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, a, R);
-        if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "k_cost_reproject launch");
-    }
-    if (a.pcost) {  // the costs the walks record now belong to this camera
-        ctx->cost_cam = a.pp.cam;
-        ctx->cost_cam_ok = true;
-    }
     for (int smp = 0; smp < ns; ++smp) {
         a.sample = smp;
         a.qlist = nullptr;  // bounce 0: every slot
@@ -2188,25 +2070,23 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                     // the heavy rays of this frame (last frame's steps) -- listed by the scan the last
                     // frame of this shape queued on the second stream, or by one here -- then their
                     // split walks there, beside the per-tile kernel (which passes over them)
-                    // (a moved camera: the list the last frame made is of its own pixels -- scan the
-                    // reprojected costs instead)
                     const bool pre = ctx->pre_ok && ctx->pre_sig == fsig && ctx->pre_steps == split_steps &&
-                                     !reproj && !(ctx->debug_flags & 2);
+                                     !(ctx->debug_flags & 2);
                     ctx->pre_ok = false;
                     int* hc = (int*)ctx->hcnt.p;
                     // the second stream follows this one up to here: with shading fused (1 bounce)
                     // nothing of this frame precedes the split walks on it but ev0 (event packets
                     // cost the frame ~1 % each); bounce 0 of a longer path needs the list memset too
-                    if (fmode == 1 && !reproj) {
+                    if (fmode == 1) {
                         HIPCHK(ctx, hipStreamWaitEvent(ctx->aux_stream, ctx->ev0_last, 0));
-                    } else {  // (after the list memset, or the reprojection the scan reads)
+                    } else {
                         HIPCHK(ctx, hipEventRecord(ctx->ev_scan, s));
                         HIPCHK(ctx, hipStreamWaitEvent(ctx->aux_stream, ctx->ev_scan, 0));
                     }
                     if (!pre) {  // (with pre, the last frame's exact kernel listed them, in this stream's order)
                         HIPCHK(ctx, hipMemsetAsync(hc, 0, 64, ctx->aux_stream));
                         ctx->hpar = 0;
-                        const HeavyScan H{a.pcost_r, (int)slots, split_steps, ort_ctx::kSplitCap,
+                        const HeavyScan H{(const uint16_t*)a.pcost, (int)slots, split_steps, ort_ctx::kSplitCap,
                                           (uint32_t*)ctx->hbits.p, (int*)ctx->hlist.p, hc};
                         hipLaunchKernelGGL(k_heavy_scan, dim3((unsigned)((slots + 4095) / 4096)), dim3(kBlock), 0,
                                            ctx->aux_stream, H);
@@ -2514,11 +2394,6 @@ int ort_set_option(ort_ctx* ctx, int option, int value) {
     if (option == ORT_OPT_HEAVY_PRIO) {
         if (value < 0 || value > 65535) return fail(ctx, ORT_ERR_INVALID_ARG, "ORT_OPT_HEAVY_PRIO: 0 (off) .. 65535 steps");
         ctx->heavy_prio = value;
-        return ORT_OK;
-    }
-    if (option == ORT_OPT_REPROJECT) {
-        if (value < 0 || value > (ORT_ANALYSIS ? 2 : 1)) return fail(ctx, ORT_ERR_INVALID_ARG, "ORT_OPT_REPROJECT: 0 or 1");
-        ctx->reproject = value;
         return ORT_OK;
     }
     if (option == ORT_OPT_COST_ORDER) {
@@ -2857,47 +2732,6 @@ int ort_debug_split_rays(const float* cr, int32_t n_spheres, const float* node_m
     } catch (const std::exception& ex) {
         return fail(nullptr, ORT_ERR_INTERNAL, ex.what());
     }
-}
-
-// TEST-ONLY: the slot <-> pixel maps of a frame shape (render_impl's dispatch grid for `pairs` /
-// `swizzle`) and the cost reprojection from camera `prev` to `cur`: per slot out[5 k] = {col,
-// row (-1: a hole), pixel_slot(col, row), reprojected slot (-1: none), its tile pixel col2 +
-// 65536 * row2}.
-int ort_debug_slot_map(const ort_params* cur, const ort_params* prev, const ort_tile* t, int32_t pairs,
-                       int32_t swizzle, int32_t* out, int64_t cap, int64_t* n_slots) {
-    if (!cur || !prev || !t || !n_slots) return fail(nullptr, ORT_ERR_INVALID_ARG, "ort_debug_slot_map: null argument");
-    const std::string bad = check_params(cur, t);
-    if (!bad.empty()) return fail(nullptr, ORT_ERR_INVALID_ARG, bad);
-    PipeArgs a;
-    std::memset(&a, 0, sizeof(a));
-    a.pp = pixel_params(cur);
-    a.tm = {t->x0, t->width, t->y0, t->rows, t->band_height, t->band_stride};
-    const int tilesX = (t->width + 15) / 16, tilesY = (t->rows + 15) / 16;
-    a.pair = pairs ? 1 : 0;
-    a.tilesX = pairs ? (tilesX + 1) / 2 : tilesX;
-    a.tilesY = tilesY;
-    a.swizzle = swizzle;
-    a.xrun_log2 = xcd_run_log2(a.tilesX);
-    const long long slots = (long long)(pairs ? 2 * a.tilesX : tilesX) * tilesY * kBlock;
-    *n_slots = slots;
-    if (!out || cap < 5 * slots) return ORT_OK;
-    Reproject R{pixel_params(prev).cam, nullptr, nullptr, nullptr, (int)slots};
-    for (long long k = 0; k < slots; ++k) {
-        int col, row;
-        int32_t* o = out + 5 * k;
-        if (!slot_coords<0>(a, (int)k, col, row)) {
-            o[0] = o[1] = o[2] = o[3] = o[4] = -1;
-            continue;
-        }
-        o[0] = col;
-        o[1] = row;
-        o[2] = pixel_slot(a, col, row);
-        o[3] = reproject_slot(a, R, (int)k);
-        int c2 = -1, r2 = 0;
-        if (o[3] >= 0) (void)slot_coords<0>(a, o[3], c2, r2);
-        o[4] = c2 < 0 ? -1 : c2 + 65536 * r2;
-    }
-    return ORT_OK;
 }
 
 int ort_debug_fast_order(int32_t m, int32_t* order8, uint8_t* lut256) {

@@ -157,11 +157,6 @@ class Renderer:
         tiles of at most 2^21 pixels, off on larger ones.  Same pixels."""
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_SPLIT_HEAVY, int(steps)))
 
-    def set_reproject(self, on: int):
-        """ORT_OPT_REPROJECT: after a camera move, the walk-cost hints follow the pixels (1, default)
-        or stay where they were recorded (0).  Same pixels."""
-        self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_REPROJECT, int(on)))
-
     def set_split_level(self, level: int):
         """ORT_OPT_SPLIT_LEVEL: the level of the subtrees a split walk deals (0: depth - 5)."""
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_SPLIT_LEVEL, int(level)))

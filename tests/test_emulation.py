@@ -299,61 +299,3 @@ def test_split_walk_equals_the_walk(ort, oracle, n, d, m):
     assert np.array_equal(got[sel, 1][hit], ref[sel, 1][hit])
     assert hit.mean() > 0.05
 
-
-def _slot_map(ort, cur, prev, tile, pairs, swizzle):
-    import ctypes as C
-    from octreeraytracer_amd import _lib as L
-    lib = L.analysis_lib()
-    pc, pp, tc = cur.to_c(), prev.to_c(), tile.to_c()
-    n = C.c_int64(0)
-    L.acheck(lib.ort_debug_slot_map(C.byref(pc), C.byref(pp), C.byref(tc), int(pairs), int(swizzle), None, 0,
-                                    C.byref(n)))
-    out = np.zeros((n.value, 5), np.int32)
-    L.acheck(lib.ort_debug_slot_map(C.byref(pc), C.byref(pp), C.byref(tc), int(pairs), int(swizzle), L.iptr(out),
-                                    out.size, C.byref(n)))
-    return out
-
-
-@pytest.mark.parametrize("W,H,tile", [(3840, 2160, None), (1920, 1080, (0, 1920, 16, 64, 16, 128)),
-                                      (997, 533, (13, 700, 5, 301, 0, 0)), (480, 270, (0, 480, 0, 48, 16, 96))])
-@pytest.mark.parametrize("pairs", [0, 1])
-@pytest.mark.parametrize("swizzle", [0, 2])
-def test_cost_reprojection_slot_maps(ort, oracle, W, H, tile, pairs, swizzle):
-    """The cost reprojection (ORT_OPT_REPROJECT, k_cost_reproject): pixel_slot inverts the
-    kernels' slot -> pixel map (every dispatch order it runs under, tile pairs or not, bands);
-    an unmoved camera maps every slot to itself; a turned camera maps each pixel to the pixel of
-    last frame's image that saw its direction (numpy, float64: within a pixel)."""
-    t = ort.Tile(*tile) if tile else ort.Tile(0, W, 0, H)
-    p = ort.FrameParams.default_camera(W, H)
-    m = _slot_map(ort, p, p, t, pairs, swizzle)
-    live = m[:, 0] >= 0
-    k = np.arange(len(m))
-    assert np.array_equal(m[live, 2], k[live])  # the inverse
-    rows = np.array(t.pixel_rows(H))
-    inframe = live.copy()
-    inframe[live] = rows[m[live, 1]] < H
-    assert np.array_equal(m[inframe, 3], k[inframe])  # same camera: itself
-    # turned 1.5 degrees (yaw) and tilted 0.5 (pitch): float64 projection of the pixel centres
-    from octreeraytracer_amd.scene import DEFAULT_YAW
-    q = ort.FrameParams.default_camera(W, H, yaw=DEFAULT_YAW + 1.5, pitch=0.5)
-    m2 = _slot_map(ort, q, p, t, pairs, swizzle)
-    cq = oracle.camera(q)[:12].astype(np.float64).reshape(4, 3)
-    cp = oracle.camera(p)[:12].astype(np.float64).reshape(4, 3)
-    sel = np.flatnonzero(inframe)
-    X = t.x0 + m2[sel, 0] + 0.5
-    Y = rows[m2[sel, 1]] + 0.5
-    d = cq[1] + (X / W)[:, None] * cq[2] + (Y / H)[:, None] * cq[3] - cq[0]
-    ll = cp[1] - cp[0]
-    w = np.cross(cp[2], cp[3])
-    lam = (ll @ w) / (d @ w)
-    qv = lam[:, None] * d - ll
-    X2 = np.floor(qv @ cp[2] / (cp[2] @ cp[2]) * W)
-    Y2 = np.floor(qv @ cp[3] / (cp[3] @ cp[3]) * H)
-    inside = (X2 >= t.x0) & (X2 < t.x0 + t.width) & (Y2 >= 0) & (Y2 < H) & (m2[sel, 3] >= 0)
-    assert inside.mean() > 0.5
-    got_c = m2[sel, 4] % 65536
-    got_y = rows[m2[sel, 4] // 65536]
-    ok = inside & np.isin(Y2, rows)  # rows the tile holds
-    assert (np.abs(got_c[ok] + t.x0 - X2[ok]) <= 1).all()
-    assert (np.abs(got_y[ok] - Y2[ok]) <= 1).all()
-    assert np.mean(got_c[ok] + t.x0 == X2[ok]) > 0.99

@@ -226,31 +226,3 @@ def test_split_heavy_queued_list_across_other_frames(ort, oracle, scene_c2):
     assert_same(got_full2, want_full, "full frame again")
     assert_same(got[-1][0:16], oracle.render(s, t, p, 0, 0, W, 16), "band rows 0-15 vs oracle")
 
-
-@pytest.mark.parametrize("depth,md", [(6, 1), (6, 4), (9, 4)])
-def test_reprojected_hints_keep_pixels(ort, oracle, depth, md):
-    """Cost reprojection (ORT_OPT_REPROJECT): a camera turning and moving frame after frame,
-    with the walk-cost hints reprojected (default) and not (0), on full frames with tile pairs,
-    a band tile with split walks, 1 and 4 bounces (the heavy-first lists read the bounce costs
-    through the slot map), depth 6 and 9: every frame bit-exact against the block order and,
-    on a sample, the oracle."""
-    from octreeraytracer_amd.scene import DEFAULT_YAW, DEFAULT_PITCH
-    s = ort.random_spheres(10_000 if depth == 6 else 20_000, 42)
-    t = ort.build_octree(s, depth, 0)
-    W, H = 960, 540
-    shots = [ort.FrameParams.default_camera(W, H, max_depth=md, yaw=DEFAULT_YAW + 1.5 * k,
-                                            pitch=DEFAULT_PITCH - 0.5 * k, position=(0.1 * k, 2.5, -10.0 + 0.2 * k))
-             for k in range(4)]
-    tiles = [ort.Tile(0, W, 0, H), ort.Tile(0, W, 16, 80, band_height=16, band_stride=128)]
-    got = {}
-    for mode in ("reproject", "stale", "block"):
-        with ort.Renderer(0) as r:
-            r.upload(s, t)
-            r.set_reproject(0 if mode == "stale" else 1)
-            r.set_cost_order(0 if mode == "block" else 1)
-            got[mode] = [r.render(p, tl) for tl in tiles for p in shots]
-    for i in range(len(got["block"])):
-        assert_same(got["reproject"][i], got["block"][i], f"frame {i}: reprojected hints vs block order")
-        assert_same(got["stale"][i], got["block"][i], f"frame {i}: stale hints vs block order")
-    ref = oracle.render(s, t, shots[3], 0, 300, W, 8, threads=0)
-    assert_same(got["reproject"][3][300:308], ref, "reprojected hints vs oracle")

@@ -1,6 +1,9 @@
-"""Moving-camera frames with the walk-cost hints reprojected or not (ORT_OPT_REPROJECT), one
-context, one frame at a time: per-frame GPU time (ort_last_kernel_ms) and the trace kernels'
-time (analysis).  usage: python tools/moving_ab.py [config] [frames] [yaw_step]"""
+"""Moving-camera frames, one context, one frame at a time: per-frame GPU time (ort_last_kernel_ms)
+and the trace kernels' time, against the same context's static frames, under modes
+"cost order:heavy priority" (analysis).  The reprojected-hint runs of
+profiles/r05_moving_*.log used the reprojection build (git history: "Cost-hint reprojection
+after camera moves") with a third mode field.
+usage: python tools/moving_ab.py [config] [frames] [yaw_step] [modes, e.g. 1:150,0:150,1:0]"""
 import sys
 from pathlib import Path
 
@@ -21,8 +24,11 @@ with ort.Renderer(0) as r:
     r.build_scene(s, D, M)
     import torch
     out = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
-    for rp in [int(x) for x in (sys.argv[4] if len(sys.argv) > 4 else "0,1,0,1").split(",")]:
-        r.set_reproject(rp)
+    # modes: cost order[:heavy priority], comma-separated
+    for mode in (sys.argv[4] if len(sys.argv) > 4 else "1:150,0:150,1:0").split(","):
+        co, hp = (list(map(int, mode.split(":"))) + [150])[:2]
+        r.set_cost_order(co)
+        r.set_heavy_prio(hp)
         poses = [ort.FrameParams.default_camera(W, H, num_samples=NS, max_depth=MD, yaw=DEFAULT_YAW + ys * k)
                  for k in range(nf)]
         for p in poses[:2]:
@@ -32,6 +38,9 @@ with ort.Renderer(0) as r:
             r.render(p, out=out)
             ms.append(r.last_kernel_ms())
             tr.append(r.frame_trace_times_ms(1)[0][0])
-        stat = [r.render(poses[-1], out=out) or r.last_kernel_ms() for _ in range(5)]
-        print(f"{cfg} reproject {rp}: moving frame {np.mean(ms[2:]):.4f} ms (trace {np.mean(tr[2:]):.4f}), "
+        stat = []
+        for _ in range(5):
+            r.render(poses[-1], out=out)
+            stat.append(r.last_kernel_ms())
+        print(f"{cfg} cost order {co} heavy prio {hp}: moving frame {np.mean(ms[2:]):.4f} ms (trace {np.mean(tr[2:]):.4f}), "
               f"static {np.mean(stat[1:]):.4f} ms", flush=True)

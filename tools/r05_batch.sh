@@ -1,7 +1,7 @@
 #!/bin/bash
 # Runs ON the GPU box (gpurun): one batch of round-5 measurements, every GPU step under its own
 # time limit, stopping at the first failure.  Output under gpurun_out/r05/<tag>/.
-# usage: tools/r05_batch.sh <tag> <step>...   steps: hash, tests, c3, c5, c3ab, c5ab
+# usage: tools/r05_batch.sh <tag> <step>...   steps: hash, tests, alltests, c3, c5
 set -u
 TAG=$1; shift
 OUT=gpurun_out/r05/$TAG
@@ -22,16 +22,6 @@ for step in "$@"; do
     c5)
         timeout -k 10 400 python -u bench.py --config c5 --steps 10 --warmup 3 --no-cpu-baseline \
             > $OUT/bench_c5.json 2> $OUT/bench_c5.err || exit 1 ;;
-    c3ab)  # reprojection off vs on (moving camera), static headline alike
-        timeout -k 10 200 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --opt REPROJECT=0 \
-            > $OUT/bench_c3_rp0.json 2> $OUT/bench_c3_rp0.err || exit 1
-        timeout -k 10 200 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline \
-            > $OUT/bench_c3_rp1.json 2> $OUT/bench_c3_rp1.err || exit 1 ;;
-    c5ab)
-        timeout -k 10 400 python -u bench.py --config c5 --steps 10 --warmup 3 --no-cpu-baseline --opt REPROJECT=0 \
-            > $OUT/bench_c5_rp0.json 2> $OUT/bench_c5_rp0.err || exit 1
-        timeout -k 10 400 python -u bench.py --config c5 --steps 10 --warmup 3 --no-cpu-baseline \
-            > $OUT/bench_c5_rp1.json 2> $OUT/bench_c5_rp1.err || exit 1 ;;
     *) echo "unknown step $step"; exit 2 ;;
     esac
     echo "step $step ok"
