@@ -123,7 +123,8 @@ typedef struct ort_scene_info {
 #define ORT_OPT_HEAVY_PRIO 13      /* T > 0 (default 150): a wave of the camera-ray trace (cost order on)
                                       that holds a ray whose walk took >= T steps in the previous frame of
                                       the same shape runs at raised issue priority (s_setprio), so the
-                                      frame's longest walks do not set its end; 0: off.  Same pixels */
+                                      frame's longest walks do not set its end -- while the camera stands
+                                      still (after a move the steps are stale); 0: off.  Same pixels */
 #define ORT_OPT_SPLIT_HEAVY 14     /* T > 0 (1 sample, cost order on): the camera rays whose walk took >= T
                                       steps in the previous frame of the same shape (up to 4096 a frame)
                                       are each walked by 8 lanes that deal the walk's subtrees of level

@@ -1378,6 +1378,7 @@ struct ort_ctx {
     static constexpr int kCostBounces = 8;
     int heavy_first = ORT_HEAVY_STEPS;
     int heavy_prio = kHeavyPrioSteps;  // ORT_OPT_HEAVY_PRIO (steps; 0 off)
+    ort::KCamera prio_cam{};           // the camera of this context's last frame (heavy priority: static only)
     // ORT_OPT_TILE_PAIRS: camera-ray workgroups of two tiles (cost_order_pair); -1 = auto (tiles
     // of at least kPairsAutoPixels)
     int tile_pairs = -1;
@@ -1967,7 +1968,15 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
             ctx->cost_sig = sig;
         }
         a.pcost = (uint16_t*)ctx->pcost.p;
-        a.prio_steps = ctx->heavy_prio;
+        // heavy priority only for a camera that has not moved since this context's last frame:
+        // after a move the per-slot steps are one frame stale (a pixel's walk cost follows its
+        // pixel-seeded lens/jitter sample more than the scene: same-slot hints keep an in-block
+        // correlation of 0.82 with the new walks, reprojected ones 0.05 -- profiles/r05_moving_*),
+        // and raising the wrong waves costs: C3 moving frames 1.855 -> 1.798 ms without it
+        // (profiles/r05_moving_shift_c3.log), static frames unchanged
+        const bool moved = std::memcmp(&ctx->prio_cam, &a.pp.cam, sizeof(ort::KCamera)) != 0;
+        a.prio_steps = moved ? 0 : ctx->heavy_prio;
+        if (!dcounters) ctx->prio_cam = a.pp.cam;
     }
     // split walks of the heavy camera rays (1 sample; the production kernels, bounce 0)
     const int split_steps = ctx->split_steps >= 0 ? ctx->split_steps

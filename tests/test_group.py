@@ -153,9 +153,11 @@ def test_group_wait_is_bounded(ort, scene_c2):
     with ort.Renderer(0) as r:
         r.upload(s, t)
         want = r.render(p)
+    torch = pytest.importorskip("torch")
     with RenderGroup([0, 0], 1, inflight=2) as g:
         g.upload(s, t)
-        out = np.empty((1080, 1920, 3), np.float32)
+        # device output: a pageable host output makes the submit's final copy synchronous
+        out = torch.empty((1080, 1920, 3), dtype=torch.float32, device="cuda:0")
         msgs = []
         for _ in range(3):
             g.set_timeout(0)  # poll once
@@ -167,7 +169,7 @@ def test_group_wait_is_bounded(ort, scene_c2):
                 msgs.append(str(e))
             g.set_timeout(120_000)
             g.wait(tk)
-            assert np.array_equal(out.view(np.uint32), want.view(np.uint32))
+            assert np.array_equal(out.cpu().numpy().view(np.uint32), want.view(np.uint32))
             if msgs:
                 break
         assert msgs, "a 8-spp 4-bounce C2 frame completed before a zero-timeout poll"
