@@ -3,6 +3,9 @@
 # passes over tools/prof_frame.py.  Output under gpurun_out/<tag>/; summarise afterwards with
 #   python tools/summarize_profile.py gpurun_out/<tag> profiles/<name> <config>
 # usage: tools/profile_box.sh <tag> [config] [bench steps] [bench warmup]
+# (C3 frames keep getting faster for the first ~15 frames of a run -- the clocks ramping up:
+# profiles/r05_c3_warm3.md -- so short frames need a long warm-up for the summary to describe
+# the steady state the bench line measures: c3 20 20)
 set -u
 TAG=${1:-prof}
 CFG=${2:-c3}
