@@ -145,11 +145,6 @@ typedef struct ort_scene_info {
                                       pairs on tiles of more than 2^21 pixels, or on any tile when
                                       ORT_OPT_SPLIT_HEAVY is 0 (on small tiles at one frame in flight the
                                       fewer, longer workgroups lengthen the frame's tail).  Same pixels */
-#define ORT_OPT_FRONTIER 19       /* tile frontiers for the camera-ray walks of trees of depth <= 8: each
-                                      16x16 tile's rays start from the list of depth-L nodes (and shallower
-                                      leaves) a conservative test of the tile's ray bundle admits, in the
-                                      walk's order, instead of walking the top L levels.  -1 (default):
-                                      L = min(5, depth - 3); 0: off; 1..6: that depth.  Same pixels */
 #define ORT_OPT_DEBUG_FLAGS 18     /* analysis library only (libort_analysis.so, tools/ab_stream.py): 1 records
                                       no per-launch trace-timing events, 2 scans the heavy list at the start
                                       of each split frame; libort.so: ORT_ERR_UNSUPPORTED */

@@ -41,7 +41,6 @@ ORT_OPT_SPLIT_HEAVY = 14
 ORT_OPT_SPLIT_LEVEL = 15
 ORT_OPT_TILE_PAIRS = 16
 ORT_OPT_DEBUG_FLAGS = 18  # analysis library only
-ORT_OPT_FRONTIER = 19
 ORT_OPT_RETIRED = (5, 7, 17)  # include/ort.h ORT_OPT_IS_RETIRED: ORT_ERR_UNSUPPORTED
 ORT_LAYOUT_COMPACT_EXACT_EMULATION = 2
 ORT_COUNT_N = 6
@@ -153,9 +152,6 @@ def _declare(lib, debug: str = "none"):
         "ort_debug_group_emulate": (C.c_int, [_fp, _fp, _fp, C.c_int32, _fp, _fp, _ip, _ip, _ip, C.c_int32, _ip, C.c_int64,
                                               C.c_int32, C.POINTER(OrtParams), _fp]),
         "ort_debug_fast_order": (C.c_int, [C.c_int32, _ip, C.POINTER(C.c_uint8)]),
-        "ort_debug_frontier_check": (C.c_int, [_fp, C.c_int32, _fp, _fp, _ip, _ip, _ip, C.c_int32, _ip, C.c_int64,
-                                               C.POINTER(OrtParams), C.POINTER(OrtTile), C.c_int32,
-                                               C.POINTER(C.c_int64)]),
         "ort_debug_trace_rays": (C.c_int, [_fp, C.c_int32, _fp, _fp, _ip, _ip, _ip, C.c_int32, _ip, C.c_int64, _fp,
                                            C.c_int32, C.c_int32, _ip]),
         "ort_debug_split_rays": (C.c_int, [_fp, C.c_int32, _fp, _fp, _ip, _ip, _ip, C.c_int32, _ip, C.c_int64, _fp,

@@ -102,10 +102,6 @@ struct PipeArgs {
     // previous frame, listed by k_heavy_scan, are walked by ort_trace_split (their walk dealt over 8
     // lanes by level-split_level subtrees) on the context's second stream; the per-tile kernel
     // passes over the slots hbits marks
-    // tile frontiers (ORT_OPT_FRONTIER, depth <= 8 camera rays): per 256-slot block fkf entries
-    // (render_core.h build_frontier; entry 0 kFrontierNone: walk from the root), or null
-    const uint2* fent;
-    int fkf;
     const uint32_t* hbits;
     const int* hlist;
     int* hsync;       // [0] heavy rays found (the list holds the first hcap), [1] ort_trace_split's cursor
@@ -280,40 +276,6 @@ __host__ __device__ inline bool slot_coords(const PipeArgs& A, int k, int& col, 
     col = bx * 16 + (wave & 1) * 8 + (lane & 7);  // an 8x8 block per wave (16x4 and 4x16: no faster, §8)
     row = by * 16 + (wave >> 1) * 8 + (lane >> 3);
     return col < A.tm.tw && row < A.tm.th;
-}
-
-// Tile frontiers (ORT_OPT_FRONTIER; render_core.h build_frontier): the list of 256-slot block
-// blk (one 16x16 tile) from the tile's frame pixels and the frame's camera.  One lane per block.
-__host__ __device__ inline void frontier_block(const PipeArgs& A, int blk, int L, uint2* out) {
-    int bx, by;
-    block_tile(A, blk, bx, by);
-    const int c0 = bx * 16, r0 = by * 16;
-    if (c0 >= A.tm.tw || r0 >= A.tm.th) {  // a hole (a pair's missing second tile): no rays
-        out[0] = make_uint2(ort::kFrontierEnd, 0u);
-        return;
-    }
-    const int c1 = min(c0 + 15, A.tm.tw - 1), r1 = min(r0 + 15, A.tm.th - 1);
-    int y0 = 0x7fffffff, y1 = -1;
-    for (int j = r0; j <= r1; ++j) {  // (band tiles: the rows of one tile may span bands)
-        const int y = tile_row_to_y(A.tm, j);
-        if (y < A.pp.H) {
-            y0 = min(y0, y);
-            y1 = max(y1, y);
-        }
-    }
-    if (y1 < 0) {  // band padding rows only
-        out[0] = make_uint2(ort::kFrontierEnd, 0u);
-        return;
-    }
-    // the deepest frontier that fits the list (a tile along the horizon meets many cells): L, L - 1, ...
-    for (int l = L; l >= 1; --l) {
-        const int n = ort::build_frontier(A.S, A.pp.cam, A.pp.W, A.pp.H, A.tm.x0 + c0, A.tm.x0 + c1, y0, y1, l, out, A.fkf);
-        if (n >= 0 || n == -2) return;  // a list, or mixed direction signs (no list at any depth)
-    }
-}
-__global__ void __launch_bounds__(kBlock) k_frontier(PipeArgs A, int L, int nblocks) {
-    const int blk = (int)(blockIdx.x * kBlock + threadIdx.x);
-    if (blk < nblocks) frontier_block(A, blk, L, const_cast<uint2*>(A.fent) + (size_t)blk * A.fkf);
 }
 
 template <bool COUNT>
@@ -747,21 +709,9 @@ __device__ __forceinline__ bool trace_slot(PipeArgs& A, LdsView& L, int k, ort::
     using Masks = typename std::conditional<DEEP, ort::Masks96, ort::Masks64>::type;
     ort::Ray walked;
     int steps = 0;
-    bool hit;
-    if constexpr (PRIMARY && !COUNT && !DEEP) {
-        // the tile's frontier list (or the plain walk: no list, or none for this tile)
-        int fi0 = -1;
-        if (A.fent) {
-            fi0 = (k >> 8) * A.fkf;
-            if (A.fent[fi0].x == ort::kFrontierNone) fi0 = -1;
-        }
-        hit = ort::traverse_fast_t<COUNT, Masks, ort::LdsFrames, true>(A.S, L.planes, L.lut, ray, inv, 0.001f, ORT_MAXFLOAT,
-                                                                      entry, t, L.fr, cnt, FUSE ? &walked : nullptr,
-                                                                      &steps, A.fent, fi0);
-    } else {
-        hit = ort::traverse_fast_t<COUNT, Masks>(A.S, L.planes, L.lut, ray, inv, 0.001f, ORT_MAXFLOAT, entry, t, L.fr,
-                                                 cnt, FUSE ? &walked : nullptr, (PRIMARY && !COUNT) ? &steps : nullptr);
-    }
+    const bool hit = ort::traverse_fast_t<COUNT, Masks>(A.S, L.planes, L.lut, ray, inv, 0.001f, ORT_MAXFLOAT, entry, t,
+                                                        L.fr, cnt, FUSE ? &walked : nullptr,
+                                                        (PRIMARY && !COUNT) ? &steps : nullptr);
     if (PRIMARY && !COUNT) {  // the cost order's record for the next frame (cost_order_slot)
 #if defined(__HIP_DEVICE_COMPILE__)
         typedef __attribute__((address_space(4))) const PipeArgs KernArgs;
@@ -1371,9 +1321,6 @@ struct DevBuf {
 // -2 %, full frame -2 %) and tile pairs on the larger ones (full frame +1.2 %, 1/2 band +0.8 %;
 // 1/4 band: split +21 % > pairs +16 %; 1/8 band: pairs with split -22 %).
 constexpr int kHeavyPrioSteps = 150;
-// Tile frontiers (ORT_OPT_FRONTIER -1): depth min(5, D - 3), at most 128 entries per tile
-constexpr int kFrontierAutoL = 5;
-constexpr int kFrontierCap = 128;
 constexpr int kSplitAutoSteps = 200;
 constexpr long long kSplitAutoPixels = 1ll << 21;
 constexpr long long kPairsAutoPixels = kSplitAutoPixels + 1;
@@ -1426,13 +1373,6 @@ struct ort_ctx {
     int cost_order = 1;
     DevBuf pcost;
     unsigned long long cost_sig = 0;
-    // ORT_OPT_FRONTIER (depth L of the tile frontiers; 0 off, -1 auto): built by k_frontier for a
-    // frame shape and camera (fr_sig, fr_cam), reused while both stay
-    int frontier = -1;
-    DevBuf fent;
-    unsigned long long fr_sig = 0;
-    ort::KCamera fr_cam{};
-    int fr_L = 0;
     // ORT_OPT_HEAVY_FIRST: threshold in walk steps (0 off); bcost holds, per bounce >= 1 of the
     // first kCostBounces of a frame, every slot's last walk steps (cleared with cost_sig)
     static constexpr int kCostBounces = 8;
@@ -2038,16 +1978,6 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
         a.prio_steps = moved ? 0 : ctx->heavy_prio;
         if (!dcounters) ctx->prio_cam = a.pp.cam;
     }
-    // tile frontiers for the depth <= 8 camera-ray walks (the production kernels)
-    int fr_L = 0;
-    if (mode == 0 && (fuse || fuse_first) && !dcounters && ctx->frontier != 0 && ctx->depth >= 2 && ctx->depth <= 8) {
-        fr_L = ctx->frontier > 0 ? std::min(ctx->frontier, ctx->depth - 1)
-                                 : std::max(1, std::min(kFrontierAutoL, ctx->depth - 3));
-        fr_L = std::min(fr_L, ORT_FRONTIER_MAX_L);
-        if ((rc = ensure(ctx, ctx->fent, 8 * (size_t)blocks * kFrontierCap))) return rc;
-        a.fent = (const uint2*)ctx->fent.p;
-        a.fkf = kFrontierCap;
-    }
     // split walks of the heavy camera rays (1 sample; the production kernels, bounce 0)
     const int split_steps = ctx->split_steps >= 0 ? ctx->split_steps
                                                   : ((long long)pix <= kSplitAutoPixels ? kSplitAutoSteps : 0);
@@ -2091,17 +2021,6 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     const bool start_is_tr0 = maxd > 0 && !(ctx->debug_flags & 1);
     ctx->ev0_last = start_is_tr0 ? ctx->tr0[fslot][0] : ctx->ev0;
     HIPCHK(ctx, hipEventRecord(ctx->ev0_last, s));
-    if (fr_L > 0) {  // the tile frontiers of this shape and camera (kept while both stay)
-        const unsigned long long sig = frame_sig(ctx, p, t);
-        if (sig != ctx->fr_sig || fr_L != ctx->fr_L || std::memcmp(&ctx->fr_cam, &a.pp.cam, sizeof(ort::KCamera)) != 0) {
-            hipLaunchKernelGGL(k_frontier, dim3((unsigned)((blocks + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, a, fr_L,
-                               (int)blocks);
-            if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "k_frontier launch");
-            ctx->fr_sig = sig;
-            ctx->fr_L = fr_L;
-            ctx->fr_cam = a.pp.cam;
-        }
-    }
     for (int smp = 0; smp < ns; ++smp) {
         a.sample = smp;
         a.qlist = nullptr;  // bounce 0: every slot
@@ -2486,13 +2405,6 @@ int ort_set_option(ort_ctx* ctx, int option, int value) {
         ctx->heavy_prio = value;
         return ORT_OK;
     }
-    if (option == ORT_OPT_FRONTIER) {
-        if (value < -1 || value > ORT_FRONTIER_MAX_L)
-            return fail(ctx, ORT_ERR_INVALID_ARG, "ORT_OPT_FRONTIER: -1 (auto), 0 (off) or a depth 1..6");
-        ctx->frontier = value;
-        ctx->fr_sig = 0;
-        return ORT_OK;
-    }
     if (option == ORT_OPT_COST_ORDER) {
         if (value < 0 || value > 1) return fail(ctx, ORT_ERR_INVALID_ARG, "ORT_OPT_COST_ORDER: 0 or 1");
         ctx->cost_order = value;
@@ -2825,96 +2737,6 @@ int ort_debug_split_rays(const float* cr, int32_t n_spheres, const float* node_m
             o[2] = best;
             o[3] = top + owns;
         }
-        return ORT_OK;
-    } catch (const std::exception& ex) {
-        return fail(nullptr, ORT_ERR_INTERNAL, ex.what());
-    }
-}
-
-// TEST-ONLY: the tile frontiers (ORT_OPT_FRONTIER, render_core.h build_frontier) against the
-// plain walk on the host: for every pixel of the tile, its first camera ray (sample 0) walked by
-// the depth <= 8 camera walk from the root and from the frontier of its 16x16 block (built as
-// k_frontier builds it), hit entry and t bits compared.  stats[9] = {rays, mismatches, blocks
-// with a list, blocks without, entries, longest list, rays walked from a list, steps from the
-// root, steps from the lists}.
-int ort_debug_frontier_check(const float* cr, int32_t n_spheres, const float* node_min, const float* node_max,
-                             const int32_t* co, const int32_t* oo, const int32_t* cnt, int32_t n_nodes,
-                             const int32_t* idx, int64_t n_indices, const ort_params* p, const ort_tile* t, int32_t L,
-                             int64_t* stats) {
-    try {
-        const std::string bad = check_params(p, t);
-        if (!bad.empty()) return fail(nullptr, ORT_ERR_INVALID_ARG, bad);
-        std::vector<float> ma((size_t)n_spheres * 4, 0.0f), fr((size_t)n_spheres * 4, 0.0f);
-        ort::SceneInput in{cr, ma.data(), fr.data(), n_spheres, node_min, node_max, co, oo, cnt, n_nodes, idx, n_indices};
-        const std::string vbad = ort::validateScene(in);
-        if (!vbad.empty()) return fail(nullptr, ORT_ERR_INVALID_ARG, vbad);
-        ort::CompactLayout cl;
-        std::string why;
-        if (!ort::buildCompactLayout(in, ORT_COMPACT_MAX_DEPTH, cl, why)) return fail(nullptr, ORT_ERR_UNSUPPORTED, why);
-        if (!cl.ordered || cl.depth > 8 || L < 1 || L >= cl.depth || L > ORT_FRONTIER_MAX_L)
-            return fail(nullptr, ORT_ERR_UNSUPPORTED, "frontier check: an ordered tree of depth <= 8, 1 <= L < depth");
-        ort::KScene S;
-        std::memset(&S, 0, sizeof(S));
-        S.n_spheres = n_spheres;
-        S.n_nodes = n_nodes;
-        S.node = (const uint2*)cl.node.data();
-        S.tail_base = (uint32_t)in.n_indices;
-        S.leaf_sph = (const float4*)cl.leaf_sph.data();
-        S.leaf_idx = cl.leaf_idx.data();
-        S.planes = cl.planes.data();
-        S.depth = cl.depth;
-        std::vector<float> fplanes(ort::fast_plane_floats(cl.depth));
-        ort::fill_fast_planes(cl.planes.data(), fplanes.data(), cl.depth);
-        std::vector<uint8_t> lut(kRankLutBytes);
-        for (size_t i = 0; i < lut.size(); ++i) lut[i] = ort::rank_lut_entry((uint32_t)i >> 8, (uint32_t)i & 255u);
-        PipeArgs a;
-        std::memset(&a, 0, sizeof(a));
-        a.pp = pixel_params(p);
-        a.S = S;
-        a.tm = {t->x0, t->width, t->y0, t->rows, t->band_height, t->band_stride};
-        a.tilesX = (t->width + 15) / 16;
-        a.tilesY = (t->rows + 15) / 16;
-        a.fkf = kFrontierCap;
-        std::vector<uint2> list(kFrontierCap);
-        for (int k = 0; k < 9; ++k) stats[k] = 0;
-        ort::LocalFrames lf;
-        for (int by = 0; by < a.tilesY; ++by)
-            for (int bx = 0; bx < a.tilesX; ++bx) {
-                frontier_block(a, by * a.tilesX + bx, L, list.data());  // raster blocks: block_tile is the identity
-                const bool has = list[0].x != ort::kFrontierNone;
-                stats[has ? 2 : 3] += 1;
-                if (has) {
-                    int n = 0;
-                    while (list[n].x != ort::kFrontierEnd) ++n;
-                    stats[4] += n;
-                    stats[5] = std::max<int64_t>(stats[5], n);
-                }
-                for (int row = by * 16; row < std::min(by * 16 + 16, t->rows); ++row) {
-                    const int y = tile_row_to_y(a.tm, row);
-                    if (y >= p->height) continue;
-                    for (int c = bx * 16; c < std::min(bx * 16 + 16, t->width); ++c) {
-                        ort_rng rng;
-                        ort::pixel_rng_init(a.pp, t->x0 + c, y, rng);
-                        const ort::Ray r = ort::primary_ray(a.pp, t->x0 + c, y, 0, rng);
-                        const ort::V3 inv = ort::mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
-                        if (!ort::fast_path_ok(r, inv, 0.001f, ORT_MAXFLOAT)) continue;
-                        ort::Counters cc;
-                        for (int k = 0; k < 6; ++k) cc.v[k] = 0;
-                        int e0 = -1, e1 = -1, s0 = 0, s1 = 0;
-                        float t0 = 0.0f, t1 = 0.0f;
-                        const bool h0 = ort::traverse_fast_t<false, ort::Masks64>(S, fplanes.data(), lut.data(), r, inv, 0.001f,
-                                                                                 ORT_MAXFLOAT, e0, t0, lf, cc, nullptr, &s0);
-                        const bool h1 = ort::traverse_fast_t<false, ort::Masks64, ort::LocalFrames, true>(
-                            S, fplanes.data(), lut.data(), r, inv, 0.001f, ORT_MAXFLOAT, e1, t1, lf, cc, nullptr, &s1,
-                            list.data(), has ? 0 : -1);
-                        stats[0] += 1;
-                        if (h0 != h1 || (h0 && (e0 != e1 || ort::f2u(t0) != ort::f2u(t1)))) stats[1] += 1;
-                        if (has) stats[6] += 1;
-                        stats[7] += s0;
-                        stats[8] += s1;
-                    }
-                }
-            }
         return ORT_OK;
     } catch (const std::exception& ex) {
         return fail(nullptr, ORT_ERR_INTERNAL, ex.what());

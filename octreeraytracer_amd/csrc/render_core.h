@@ -459,9 +459,6 @@ ORT_FN bool a_in_qdiv_range(float a) { return a >= 0.125f && a <= 8.0f; }
 // The fast walk's t_min (the shader's only one, glsl:hit(r, 0.001, ...)) is a literal in the
 // instruction stream rather than a per-ray register.
 constexpr float kFastTMin = 0.001f;
-#ifndef ORT_FRONTIER_MAX_L
-#define ORT_FRONTIER_MAX_L 6  // deepest frontier depth build_frontier supports
-#endif
 // The fast walk's preconditions: finite 1/d and origin (no slab value can be NaN), a
 // positive t_min and finite t_max (the push test below relies on both), dot(d,d) in
 // qdiv's range.
@@ -861,7 +858,6 @@ struct FastStateT {
     uint32_t kc_id;
     float kc_e;
     Masks masks;
-    int fi;          // (frontier walks) index of the next entry of the tile's frontier list
     ORT_FN bool hit() const { return hitEntry >= 0; }
     ORT_FN float pl(const float* p, int s, int idx) const {
         return Masks::kRevPlanes ? p[idx] : *(const float*)((const char*)p + imul24(s, idx));
@@ -1231,19 +1227,10 @@ ORT_FN void fast_pop(const KScene& S, FastStateT<Masks>& st, Frames& fr);
 
 // One node of the walk: visit st.node (push its surviving children, or test its spheres),
 // then pop the next node.  Returns true when the walk is over (hit found, or stack empty).
-template <class Masks>
-ORT_FN bool frontier_next(const KScene& S, const uint2* fent, FastStateT<Masks>& st);
-
-template <bool COUNT, class Masks, class Frames, bool FR = false>
-ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks>& st, Frames& fr, Counters& cnt,
-                      const uint2* fent = nullptr) {
+template <bool COUNT, class Masks, class Frames>
+ORT_FN bool fast_step(const KScene& S, const uint8_t* rank_lut, FastStateT<Masks>& st, Frames& fr, Counters& cnt) {
     if (fast_visit<COUNT>(S, rank_lut, st, fr, cnt)) return true;
-    // (frontier walks: the walk of one frontier node's subtree is over -- enter the next entry
-    // the ray hits, or end)
-    if (st.masks.empty()) {
-        if constexpr (FR) return !frontier_next(S, fent, st);
-        return true;
-    }
+    if (st.masks.empty()) return true;
 #if defined(__HIP_DEVICE_COMPILE__) && defined(ORT_PAD_VALU)
     {   // issue-sensitivity experiment only (tools): ORT_PAD_VALU extra VALU per step
         float pv = 0.0f;
@@ -1324,224 +1311,19 @@ ORT_FN void fast_pop(const KScene& S, FastStateT<Masks>& st, Frames& fr) {
     }
 }
 
-// ---------------------------------------------------------------------------------------
-// Tile frontiers (camera rays, depth <= 8 walk).  The nodes a walk visits at depth L -- and the
-// leaves above it -- come in one order for every ray with the same direction signs (the DFS
-// order of glsl:352-476 depends only on the sign vector), and a node is visited iff its own push
-// test passes (child boxes nest, so an ancestor's test passes whenever the node's does, and the
-// pushed tmin is max(max3(entries), t_min): DESIGN.md 4), until the first hit (glsl:336).  So
-// the walk of a tile's rays can start from the tile's frontier list -- every depth-L node and
-// shallower leaf a conservative test of its box against the tile's ray bundle admits, in that
-// order (build_frontier) -- instead of walking the top L levels: each ray tests the entries in
-// turn with the push test's own arithmetic and walks the subtree of each one it hits exactly as
-// the reference would have from there.  Same visits below L, same first hit: the same pixels.
-//
-// Entry e: e.x = node, e.y = depth << 27 | cA << 18 | cB << 9 | cC (the node's cell at its
-// depth, in ray order on the role axes A/B/C: the index of its near plane >> (D - depth)).
-constexpr uint32_t kFrontierEnd = 0xffffffffu;   // e.x: the list ends here
-constexpr uint32_t kFrontierNone = 0xfffffffeu;  // e.x of entry 0: no list for this tile (walk from the root)
-
-// The state the pop would leave for entry e's node, without its record; returns whether the
-// node passes its push test (child_drops' arithmetic: the parent's child values ARE the node's
-// own near/far plane values), and then loads its record.
-template <class Masks>
-ORT_FN bool fast_enter(const KScene& S, FastStateT<Masks>& st, uint2 e) {
-    static_assert(Masks::kRevPlanes, "frontier walks use the reversed plane tables");
-    const int D = S.depth;
-    const int l = (int)(e.y >> 27);
-    const uint32_t keep = ~(4u * (uint32_t)fast_rev_T(D) - 1u);  // the table start (a multiple of 4T bytes)
-    const uint32_t sh = (uint32_t)(D - l + 2);                   // log2 of a depth-l cell, in plane-table bytes
-    st.aA = (st.aA & keep) | (((e.y >> 18) & 511u) << sh);
-    st.aB = (st.aB & keep) | (((e.y >> 9) & 511u) << sh);
-    st.aC = (st.aC & keep) | ((e.y & 511u) << sh);
-    const uint32_t w4 = 1u << sh;
-    st.h4 = w4 >> 1;
-    st.tNA = st.iA * (st.plane(st.aA) - st.oA);
-    st.tFA = st.iA * (st.plane(st.aA + w4) - st.oA);
-    st.tNB = st.iB * (st.plane(st.aB) - st.oB);
-    st.tFB = st.iB * (st.plane(st.aB + w4) - st.oB);
-    st.tNC = st.iC * (st.plane(st.aC) - st.oC);
-    st.tFC = st.iC * (st.plane(st.aC + w4) - st.oC);
-    const float entry = fmax3(st.tNA, st.tNB, fmax_tmin(st.tNC));
-    const float exit = fmin3(st.tFA, st.tFB, fmin2(st.tFC, st.closest));
-    if (f2u(exit - entry) >> 31) return false;  // dropped, as child_drops would drop it
-    if (Masks::kPreMid) {  // (a frontier node is above depth D: h4 >= 4 bytes)
-        st.tMA = st.iA * (st.plane(st.aA + st.h4) - st.oA);
-        st.tMB = st.iB * (st.plane(st.aB + st.h4) - st.oB);
-        st.tMC = st.iC * (st.plane(st.aC + st.h4) - st.oC);
-    }
-    st.depth = l;
-    st.node = (int)e.x;
-    fetch_rec(S, st.node, false, st);
-    return true;
-}
-
-// Enter the next frontier entry the ray hits (st.fi onwards); false when the list is done.
-template <class Masks>
-ORT_FN bool frontier_next(const KScene& S, const uint2* fent, FastStateT<Masks>& st) {
-    for (;;) {
-        const uint2 e = fent[st.fi];
-        if (e.x == kFrontierEnd) return false;
-        st.fi += 1;
-        if (fast_enter(S, st, e)) return true;
-    }
-}
-
-// The frontier of one tile (see above): depth-L nodes and shallower non-empty leaves whose box a
-// ray of the tile could hit, in the walk's order.  The bundle: origins in the lens disk (radius
-// cam.lensRadius, plane of u, v), directions through the tile's pixel rectangle at the focal
-// plane, widened by the sample offset and the pixel jitter (Camera_getRay, glsl:205-221); the
-// box test is interval arithmetic in double over per-axis origin and direction intervals (the
-// axes decoupled: a superset of the rays' own tests), boxes widened by 1e-5 of their coordinates
-// against float rounding.  X0..X1, Y0..Y1: the tile's frame pixels.  Returns the entries
-// written (a kFrontierEnd entry follows them), or (entry 0 = kFrontierNone) -2 when the tile's
-// rays' direction signs differ, -1 when the list would exceed cap - 1 entries (or a root leaf).
-ORT_FN int build_frontier(const KScene& S, const KCamera& cam, int W, int H, int X0, int X1, int Y0, int Y1, int L,
-                          uint2* out, int cap) {
-    const int D = S.depth;
-    const double e = 1.0 / (double)(W > H ? W : H);
-    const double s0 = (double)X0 / W - e, s1 = (X1 + 2.0) / W + e, t0 = (double)Y0 / H - e, t1 = (Y1 + 2.0) / H + e;
-    const float* cO = &cam.origin.x;
-    const float* cL = &cam.lowerLeft.x;
-    const float* cH = &cam.horizontal.x;
-    const float* cV = &cam.vertical.x;
-    const float* cu = &cam.u.x;
-    const float* cv = &cam.v.x;
-    double ol[3], oh[3], dl[3], dh[3];
-    uint32_t neg[3];
-    for (int a = 0; a < 3; ++a) {
-        const double f00 = (double)cL[a] + s0 * cH[a] + t0 * cV[a], f10 = (double)cL[a] + s1 * cH[a] + t0 * cV[a];
-        const double f01 = (double)cL[a] + s0 * cH[a] + t1 * cV[a], f11 = (double)cL[a] + s1 * cH[a] + t1 * cV[a];
-        const double fl = fmin(fmin(f00, f10), fmin(f01, f11)), fh = fmax(fmax(f00, f10), fmax(f01, f11));
-        const double rho = (double)cam.lensRadius * (fabs((double)cu[a]) + fabs((double)cv[a])) * (1.0 + 1e-6) +
-                           1e-6 * (1.0 + fabs((double)cO[a]));
-        ol[a] = cO[a] - rho;
-        oh[a] = cO[a] + rho;
-        dl[a] = fl - oh[a] - 1e-6 * (1.0 + fabs(fl));
-        dh[a] = fh - ol[a] + 1e-6 * (1.0 + fabs(fh));
-        if (!(dl[a] > 0.0 || dh[a] < 0.0)) {
-            out[0] = make_uint2(kFrontierNone, 0u);
-            return -2;
-        }
-        neg[a] = dh[a] < 0.0 ? 1u : 0u;
-    }
-    const uint32_t m = (neg[2] << 2) | (neg[0] << 1) | neg[1];
-    const bool swap = neg[0] != 0;
-    const uint32_t otab = (swap ? 0x75643120u : 0x76543210u) ^ (m * 0x11111111u);
-    const int wA = swap ? 1 : 0, wB = swap ? 0 : 1;  // world axes of the role axes A, B (C = z)
-    const int P1 = (1 << D) + 1;
-    // may a ray of the bundle hit the depth-l box of role cells (cA, cB, cC)?
-    auto may_hit = [&](int l, uint32_t cA, uint32_t cB, uint32_t cC) -> bool {
-        double tin = -1e300, tout = 1e300;
-        const uint32_t c3[3] = {cA, cB, cC};
-        const int w3[3] = {wA, wB, 2};
-        for (int r = 0; r < 3; ++r) {
-            const int a = w3[r];
-            const uint32_t wi = neg[a] ? ((1u << l) - 1u - c3[r]) : c3[r];  // world cell index
-            const double lo0 = S.planes[a * P1 + (int)(wi << (D - l))], hi0 = S.planes[a * P1 + (int)((wi + 1u) << (D - l))];
-            const double mg = 1e-5 * (fabs(lo0) + fabs(hi0) + (hi0 - lo0)) + 1e-7;
-            const double lo = lo0 - mg, hi = hi0 + mg;
-            double ti, to;
-            if (!neg[a]) {  // d in [dl, dh], dl > 0: enters at lo, leaves at hi
-                const double n = lo - oh[a], q = hi - ol[a];
-                ti = n >= 0.0 ? n / dh[a] : n / dl[a];
-                to = q >= 0.0 ? q / dl[a] : q / dh[a];
-            } else {  // |d| in [-dh, -dl]: enters at hi, leaves at lo
-                const double n = ol[a] - hi, q = oh[a] - lo;
-                ti = n >= 0.0 ? n / -dl[a] : n / -dh[a];
-                to = q >= 0.0 ? q / -dh[a] : q / -dl[a];
-            }
-            tin = fmax(tin, ti);
-            tout = fmin(tout, to);
-        }
-        return tin <= tout && tout >= 0.0;
-    };
-    int n = 0;
-    auto emit = [&](int node, int l, uint32_t cA, uint32_t cB, uint32_t cC) -> bool {
-        if (n + 1 >= cap) return false;
-        out[n++] = make_uint2((uint32_t)node, ((uint32_t)l << 27) | (cA << 18) | (cB << 9) | cC);
-        return true;
-    };
-    if (!may_hit(0, 0, 0, 0)) {
-        out[0] = make_uint2(kFrontierEnd, 0u);
-        return 0;
-    }
-    // iterative DFS over depths < L: per level the internal node's children offset, cells and the
-    // ranks still to go (bit r = rank r)
-    int fco[ORT_FRONTIER_MAX_L + 1];
-    uint32_t fA[ORT_FRONTIER_MAX_L + 1], fB[ORT_FRONTIER_MAX_L + 1], fC[ORT_FRONTIER_MAX_L + 1], todo[ORT_FRONTIER_MAX_L + 1];
-    int lev = 0;
-    {
-        const uint2 rec = S.node[0];
-        if (!(rec.y & ORT_INTERNAL_FLAG)) {  // a root leaf: the plain walk
-            out[0] = make_uint2(kFrontierNone, 0u);
-            return -2;
-        }
-        fco[0] = (int)rec.x;
-        fA[0] = fB[0] = fC[0] = 0;
-        uint32_t rm = 0;
-        for (int r = 0; r < 8; ++r) rm |= ((rec.y >> ((otab >> (4 * r)) & 15u)) & 1u) << r;
-        todo[0] = rm;
-    }
-    while (lev >= 0) {
-        if (!todo[lev]) {
-            --lev;
-            continue;
-        }
-        const int r = __builtin_ctz(todo[lev]);
-        todo[lev] &= todo[lev] - 1u;
-        const int l = lev + 1;  // the child's depth
-        const uint32_t cA = 2u * fA[lev] + ((r >> 1) & 1), cB = 2u * fB[lev] + (r & 1), cC = 2u * fC[lev] + ((r >> 2) & 1);
-        if (!may_hit(l, cA, cB, cC)) continue;
-        const int node = fco[lev] + (int)((otab >> (4 * r)) & 15u);
-        const uint2 rec = S.node[node];
-        const bool internal = (rec.y & ORT_INTERNAL_FLAG) != 0;
-        if (!internal || l == L) {
-            if ((internal || rec.y > 0u) && !emit(node, l, cA, cB, cC)) {
-                out[0] = make_uint2(kFrontierNone, 0u);
-                return -1;
-            }
-            continue;
-        }
-        lev = l;
-        fco[lev] = (int)rec.x;
-        fA[lev] = cA;
-        fB[lev] = cB;
-        fC[lev] = cC;
-        uint32_t rm = 0;
-        for (int q = 0; q < 8; ++q) rm |= ((rec.y >> ((otab >> (4 * q)) & 15u)) & 1u) << q;
-        todo[lev] = rm;
-    }
-    out[n] = make_uint2(kFrontierEnd, 0u);
-    return n;
-}
-
-template <bool COUNT, class Masks, class Frames, bool FR = false>
+template <bool COUNT, class Masks, class Frames>
 ORT_FN bool traverse_fast_t(const KScene& S, const float* planes, const uint8_t* rank_lut, const Ray& r, V3 inv,
                             float t_min, float t_max, int& hitEntry, float& hitT, Frames& fr, Counters& cnt,
-                            Ray* walked = nullptr, int* steps = nullptr, const uint2* fent = nullptr, int fi0 = -1) {
+                            Ray* walked = nullptr, int* steps = nullptr) {
     FastStateT<Masks> st;
-    bool in = fast_begin(S, planes, rank_lut, r, inv, t_min, t_max, st);
+    const bool in = fast_begin(S, planes, rank_lut, r, inv, t_min, t_max, st);
     int n = 0;  // walk steps (steps: the cost order's record; folds away without it)
     // (a leaf hold as in the deep bounce walk, lanes at a leaf waiting for company, cost the deep
     // camera walk 10-14 % at 8-16 lanes: the coherent camera rays reach leaves together anyway)
-    bool plain = true;
-    if constexpr (FR) {
-        if (fi0 >= 0) {  // the tile's frontier instead of the top levels
-            plain = false;
-            st.fi = fi0;
-            if (in && frontier_next(S, fent, st)) {
-                while (!fast_step<COUNT, Masks, Frames, true>(S, rank_lut, st, fr, cnt, fent)) {
-                    ++n;
-                }
-            }
-        }
-    }
-    if (plain && in) {
+    if (in)
         while (!fast_step<COUNT>(S, rank_lut, st, fr, cnt)) {
             ++n;
         }
-    }
     if (steps) *steps = in ? n + 1 : 0;
     // the ray back from the walk state (bit-identical to r; no extra registers across the walk)
     if (walked) *walked = st.ray();

@@ -157,11 +157,6 @@ class Renderer:
         tiles of at most 2^21 pixels, off on larger ones.  Same pixels."""
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_SPLIT_HEAVY, int(steps)))
 
-    def set_frontier(self, depth: int):
-        """ORT_OPT_FRONTIER: tile frontiers for the depth <= 8 camera-ray walks (-1 auto, 0 off, or the
-        frontier depth).  Same pixels."""
-        self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_FRONTIER, int(depth)))
-
     def set_split_level(self, level: int):
         """ORT_OPT_SPLIT_LEVEL: the level of the subtrees a split walk deals (0: depth - 5)."""
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_SPLIT_LEVEL, int(level)))
