@@ -813,7 +813,7 @@ __device__ __forceinline__ int cost_order_slot(const uint16_t* pcost, int* sc, i
 
 // Cost order over a tile pair (ORT_OPT_TILE_PAIRS): the 512 slots of workgroup b (slots 512b ..
 // 512b + 511, two tiles) in eight blocks of 64 by last frame's walk steps (the stable counting
-// sort of cost_order_slot, buckets of 4 steps), and wave w walks block 7 - w and then block w: a
+// sort of cost_order_slot, buckets of 2^SHIFT steps: 2 by default), and wave w walks block 7 - w and then block w: a
 // workgroup holds its LDS until its slowest wave ends, and with one block per wave the cost
 // order left 12-13 % of the waves' time idle inside the workgroups (tools/tile_clock.py); the
 // longest-processing-time pairs (7,0) (6,1) (5,2) (4,3) even the waves out.  Scratch: the
