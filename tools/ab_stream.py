@@ -49,7 +49,7 @@ def worker(spec, config, block, max_depth=0, world=1, yaw_step=0.0):
     MD = max_depth or MD
     path, _, opts = spec.partition("@")
     lib = C.CDLL(str(Path(path).resolve()), mode=C.RTLD_LOCAL)
-    L._declare(lib, strict=False)
+    L._declare(lib, debug="present")
     L._lib = lib
     r = ort.Renderer(0)
     spheres = ort.random_spheres(N, 42)

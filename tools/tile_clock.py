@@ -19,7 +19,7 @@ from octreeraytracer_amd import _lib as L  # noqa: E402
 from octreeraytracer_amd.distributed import rank_tile  # noqa: E402
 
 lib = C.CDLL(str(Path(sys.argv[1]).resolve()), mode=C.RTLD_LOCAL)
-L._declare(lib, strict=False)
+L._declare(lib, debug="present")
 L._lib = lib
 cfg = sys.argv[2] if len(sys.argv) > 2 else "c3"
 world = int(sys.argv[3]) if len(sys.argv) > 3 else 8
