@@ -332,3 +332,17 @@ def test_extreme_sphere_roots(ort, oracle, renderer, use_octree):
     assert_same(renderer.render(p), oracle.render(s, t, p), "extreme roots")
     p1 = ort.FrameParams.default_camera(64, 40, use_octree=use_octree)
     assert_same(renderer.render(p1), oracle.render(s, t, p1), "extreme roots, primary")
+
+
+@pytest.mark.parametrize("name", sorted(p.stem for p in (__import__("pathlib").Path(__file__).parent / "golden" / "glsl").glob("*.npz")))
+def test_kernel_matches_reference_shader(ort, oracle, renderer, name):
+    """The HIP kernels against the reference's own shaders run by Mesa llvmpipe
+    (tests/golden/glsl, tests/test_glsl_parity.py for the tolerances) -- and bit-exact against
+    the oracle on the same frame."""
+    from test_glsl_parity import check_against_glsl, inputs, load
+    ref, meta = load(name)
+    s, t, p = inputs(ort, meta)
+    renderer.upload(s, t)
+    img = renderer.render(p)
+    check_against_glsl(img, ref, meta, f"HIP vs GLSL {name}")
+    assert_same(img, oracle.render(s, t if meta["oct"] else None, p), f"HIP vs oracle {name}")

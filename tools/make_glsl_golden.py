@@ -1,0 +1,110 @@
+"""Generate tests/golden/glsl/*.npz: frames of the REFERENCE'S OWN shaders
+(/root/reference/shaders/vertex_shader.glsl + octree_fragment_shader.glsl) executed by a real
+GLSL 4.30 implementation, the image's Mesa llvmpipe, through oracle/_ref/glsl_run
+(oracle/glsl_run.c: a headless DRI swrast loader; `make -C oracle glsl`).  Test infrastructure
+only: the fixtures pin the CPU oracle's pixel arithmetic (tests/test_glsl_parity.py) and, through
+it, the HIP kernels (tests/test_gpu_parity.py); nothing here runs on the GPU box.
+
+Inputs are this repo's seeded sphere sets and the octrees of its builder, which is
+byte-identical to the reference's own src/octree.cpp on every pinned tree
+(tests/golden/manifest.json).  Each fixture holds the frame (float32 RGB, GL row order; the
+shader's alpha is 1 everywhere and is checked, then dropped) and the case it was made from.
+
+usage: python tools/make_glsl_golden.py [case ...]
+"""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+import octreeraytracer_amd as ort  # noqa: E402
+from octreeraytracer_amd.scene import DEFAULT_PITCH, DEFAULT_YAW  # noqa: E402
+
+OUT = ROOT / "tests" / "golden" / "glsl"
+RUNNER = ROOT / "oracle" / "_ref" / "glsl_run"
+SHADERS = Path(os.environ.get("ORT_REF", "/root/reference")) / "shaders"
+
+# name: scene, (n, seed), tree depth, maxSpheresPerNode, frame (W, H, spp, maxDepth, useOctree),
+# camera (yaw, pitch offsets from the default camera), kind (primary: one traversal per pixel)
+CASES = {
+    "c1": dict(scene="random", n=100, depth=4, m=0, W=256, H=256, spp=1, md=1, oct=1, dyaw=0.0, dpitch=0.0),
+    "c1_turned": dict(scene="random", n=100, depth=4, m=0, W=192, H=144, spp=1, md=1, oct=1, dyaw=30.0, dpitch=-15.0),
+    "debug": dict(scene="debug", n=3, depth=3, m=2, W=160, H=120, spp=1, md=1, oct=1, dyaw=0.0, dpitch=0.0),
+    "m1_d6": dict(scene="random", n=2000, depth=6, m=1, W=192, H=108, spp=1, md=1, oct=1, dyaw=-12.0, dpitch=4.0),
+    "c2": dict(scene="random", n=10000, depth=6, m=0, W=320, H=180, spp=1, md=1, oct=1, dyaw=0.0, dpitch=0.0),
+    "c3": dict(scene="random", n=100000, depth=8, m=0, W=256, H=144, spp=1, md=1, oct=1, dyaw=0.0, dpitch=0.0),
+    "brute_d4": dict(scene="random", n=100, depth=4, m=0, W=128, H=96, spp=1, md=4, oct=0, dyaw=0.0, dpitch=0.0),
+    "prebuilt_spp4_d8": dict(scene="prebuilt", n=83, depth=5, m=1, W=160, H=120, spp=4, md=8, oct=1, dyaw=0.0,
+                             dpitch=0.0),
+    "c2_spp2_d4": dict(scene="random", n=10000, depth=6, m=0, W=192, H=108, spp=2, md=4, oct=1, dyaw=20.0,
+                       dpitch=-10.0),
+}
+
+
+def case_inputs(c):
+    if c["scene"] == "random":
+        s = ort.random_spheres(c["n"], 42)
+    elif c["scene"] == "prebuilt":
+        s = ort.prebuilt_spheres()
+    else:
+        s = ort.debug_spheres()
+    t = ort.build_octree(s, c["depth"], c["m"])
+    p = ort.FrameParams.default_camera(c["W"], c["H"], yaw=DEFAULT_YAW + c["dyaw"], pitch=DEFAULT_PITCH + c["dpitch"],
+                                       num_samples=c["spp"], max_depth=c["md"], use_octree=c["oct"])
+    return s, t, p
+
+
+def write_input(path, s, t, p):
+    """glsl_run's input: the header, the frame's uniforms and setupBuffers' seven arrays."""
+    c = p.to_c()
+    hdr = np.array([c.width, c.height, c.num_samples, c.max_depth, c.use_octree, s.n, t.n_nodes, t.n_indices], np.int32)
+    uni = np.array(list(c.view) + list(c.camera_position) + [c.camera_zoom], np.float32)
+    # (glm::vec4(node.min, node.childrenOffset): the offsets travel as floats, src/raytracer.cpp:98-99)
+    nmin = np.concatenate([t.node_min.astype(np.float32), t.children_offset.astype(np.float32)[:, None]], 1)
+    nmax = np.concatenate([t.node_max.astype(np.float32), t.objects_offset.astype(np.float32)[:, None]], 1)
+    with open(path, "wb") as f:
+        for a in (hdr, uni, s.center_radius.astype(np.float32), s.mat_albedo.astype(np.float32),
+                  s.fuzz_ri.astype(np.float32), nmin, nmax, t.object_count.astype(np.int32),
+                  t.object_indices.astype(np.int32)):
+            f.write(np.ascontiguousarray(a).tobytes())
+
+
+def run_glsl(s, t, p):
+    with tempfile.TemporaryDirectory() as d:
+        write_input(f"{d}/in.bin", s, t, p)
+        r = subprocess.run([str(RUNNER), str(SHADERS), f"{d}/in.bin", f"{d}/out.bin"], capture_output=True, text=True)
+        if r.returncode != 0:
+            raise SystemExit(f"glsl_run failed: {r.stderr}")
+        img = np.fromfile(f"{d}/out.bin", np.float32).reshape(p.height, p.width, 4)
+    if not (img[..., 3] == 1.0).all():
+        raise SystemExit("FragColor alpha is not 1 everywhere")
+    return np.ascontiguousarray(img[..., :3]), r.stderr.strip().splitlines()[-1]
+
+
+def main():
+    if not RUNNER.exists():
+        raise SystemExit("build the runner first: make -C oracle glsl")
+    OUT.mkdir(parents=True, exist_ok=True)
+    names = sys.argv[1:] or list(CASES)
+    for name in names:
+        c = CASES[name]
+        t0 = time.time()
+        s, t, p = case_inputs(c)
+        img, renderer = run_glsl(s, t, p)
+        meta = dict(c, name=name, renderer=renderer, shaders="shaders/vertex_shader.glsl + shaders/octree_fragment_shader.glsl",
+                    n_nodes=int(t.n_nodes), n_indices=int(t.n_indices))
+        np.savez_compressed(OUT / f"{name}.npz", rgb=img, meta=json.dumps(meta))
+        print(f"{name}: {p.width}x{p.height} in {time.time() - t0:.1f} s ({renderer})", flush=True)
+
+
+if __name__ == "__main__":
+    main()
