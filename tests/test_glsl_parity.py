@@ -85,3 +85,20 @@ def test_oracle_matches_reference_shader(ort, oracle, name):
     assert (t.n_nodes, t.n_indices) == (meta["n_nodes"], meta["n_indices"])
     img = oracle.render(s, t if meta["oct"] else None, p)
     check_against_glsl(img, ref, meta, f"oracle vs GLSL {name}")
+
+
+RUNNER = Path(__file__).resolve().parents[1] / "oracle" / "_ref" / "glsl_run"
+SHADERS = Path("/root/reference/shaders")
+
+
+@pytest.mark.skipif(not (RUNNER.exists() and SHADERS.exists()), reason="needs oracle/_ref/glsl_run and /root/reference")
+@pytest.mark.parametrize("name", ["c1", "debug", "brute_d4"])
+def test_fixtures_regenerate_bit_for_bit(name):
+    """The fixtures are what the reference's shaders give now (llvmpipe is deterministic)."""
+    import sys
+    sys.path.insert(0, str(RUNNER.parents[2] / "tools"))
+    import make_glsl_golden as M
+    ref, meta = load(name)
+    img, renderer = M.run_glsl(*M.case_inputs(M.CASES[name]))
+    assert renderer == meta["renderer"]
+    assert np.array_equal(img.view(np.uint32), ref.view(np.uint32))
