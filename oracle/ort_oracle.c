@@ -5,14 +5,16 @@
  * (as the checker / the timed CPU baseline); the product (libort.so) never does.
  *
  * The reference has no CPU ray tracer: all tracing lives in
- * shaders/octree_fragment_shader.glsl, which cannot be compiled or run here (no GL
- * driver, Windows-only GLFW).  This file restates that shader line by
- * line in plain C over the reference's buffer layout (SSBO bindings 0-6, glsl:20-46),
- * with the canonical builtins of include/ort_math.h.
- * Parity at the GL-driver boundary is therefore UNPINNED (no image, test or readback
- * exists in the reference); the octree input it consumes IS pinned
- * byte-for-byte against the reference's own src/octree.cpp (oracle/_ref, tests/golden).
- *
+ * shaders/octree_fragment_shader.glsl, whose own build (GLFW window, Windows-only) cannot run
+ * here.  This file restates that shader line by line in plain C over the
+ * reference's buffer layout (SSBO bindings 0-6, glsl:20-46), with the canonical builtins of
+ * include/ort_math.h.  Pinning: the octree input is byte-for-byte the
+ * reference's own src/octree.cpp's (oracle/_ref/ref_octree, tests/golden); the pixels are
+ * checked against the reference's UNMODIFIED shaders run by the image's Mesa llvmpipe
+ * (oracle/glsl_run.c, tests/golden/glsl, tests/test_glsl_parity.py): within 1e-6 on >= 99.99 %
+ * of a primary-ray frame's pixels, the rest on sphere silhouettes -- GLSL's builtins have a
+ * few ULP of freedom, so the pin is to rounding, not to every bit.
+
  * Differences from the GLSL, all forced: node offsets are int32 instead of float-in-
  * vec4.w; FragCoord is exactly (px+0.5, py+0.5) (vertex_shader.glsl:15);
  * the traversal order for the impossible zero sign vector is the identity.
