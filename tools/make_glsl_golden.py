@@ -47,6 +47,10 @@ CASES = {
                              dpitch=0.0),
     "c2_spp2_d4": dict(scene="random", n=10000, depth=6, m=0, W=192, H=108, spp=2, md=4, oct=1, dyaw=20.0,
                        dpitch=-10.0),
+    # the bench's C3 frame itself (3840x2160, 100k spheres, depth 8); 16 of its rows are kept
+    "c3_full_rows": dict(scene="random", n=100000, depth=8, m=0, W=3840, H=2160, spp=1, md=1, oct=1, dyaw=0.0,
+                         dpitch=0.0, rows=[0, 135, 270, 405, 540, 675, 810, 945, 1080, 1215, 1350, 1485, 1620, 1755,
+                                           1890, 2159]),
 }
 
 
@@ -100,6 +104,8 @@ def main():
         t0 = time.time()
         s, t, p = case_inputs(c)
         img, renderer = run_glsl(s, t, p)
+        if "rows" in c:  # a large frame: the listed rows (GL row order) only
+            img = np.ascontiguousarray(img[c["rows"]])
         meta = dict(c, name=name, renderer=renderer, shaders="shaders/vertex_shader.glsl + shaders/octree_fragment_shader.glsl",
                     n_nodes=int(t.n_nodes), n_indices=int(t.n_indices))
         np.savez_compressed(OUT / f"{name}.npz", rgb=img, meta=json.dumps(meta))
