@@ -32,6 +32,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include <GL/gl.h>
 #include <GL/glext.h>
@@ -290,8 +291,13 @@ int main(int argc, char **argv) {
 
     glClearColor(0.2f, 0.2f, 0.2f, 1.0f);
     glClear(GL_COLOR_BUFFER_BIT);
+    struct timespec t0, t1;
+    glFinish();
+    clock_gettime(CLOCK_MONOTONIC, &t0);
     glDrawArrays(GL_TRIANGLES, 0, 6);
     glFinish();
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    fprintf(stderr, "glsl_run: draw %.1f ms\n", (double)(t1.tv_sec - t0.tv_sec) * 1e3 + (double)(t1.tv_nsec - t0.tv_nsec) * 1e-6);
     float *out = (float *)malloc((size_t)W * (size_t)H * 16);
     if (!out) die("out of memory");
     glReadBuffer(GL_COLOR_ATTACHMENT0);

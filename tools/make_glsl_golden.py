@@ -82,7 +82,8 @@ def write_input(path, s, t, p):
             f.write(np.ascontiguousarray(a).tobytes())
 
 
-def run_glsl(s, t, p):
+def run_glsl(s, t, p, timing=None):
+    """The frame (H, W, 3) and the renderer line; timing (a dict) gets the draw's wall ms."""
     with tempfile.TemporaryDirectory() as d:
         write_input(f"{d}/in.bin", s, t, p)
         r = subprocess.run([str(RUNNER), str(SHADERS), f"{d}/in.bin", f"{d}/out.bin"], capture_output=True, text=True)
@@ -91,7 +92,10 @@ def run_glsl(s, t, p):
         img = np.fromfile(f"{d}/out.bin", np.float32).reshape(p.height, p.width, 4)
     if not (img[..., 3] == 1.0).all():
         raise SystemExit("FragColor alpha is not 1 everywhere")
-    return np.ascontiguousarray(img[..., :3]), r.stderr.strip().splitlines()[-1]
+    lines = r.stderr.strip().splitlines()
+    if timing is not None:
+        timing["draw_ms"] = float(next(x for x in lines if " draw " in x).split()[-2])
+    return np.ascontiguousarray(img[..., :3]), next(x for x in lines if "Mesa" in x)
 
 
 def main():
