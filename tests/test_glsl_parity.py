@@ -43,6 +43,9 @@ def inputs(ort, c):
         s = ort.random_spheres(c["n"], 42)
     elif c["scene"] == "prebuilt":
         s = ort.prebuilt_spheres()
+    elif c["scene"] == "extreme":
+        from test_emulation import extreme_root_scene
+        s = extreme_root_scene(ort)
     else:
         s = ort.debug_spheres()
     t = ort.build_octree(s, c["depth"], c["m"])

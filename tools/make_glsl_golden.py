@@ -47,6 +47,11 @@ CASES = {
                              dpitch=0.0),
     "c2_spp2_d4": dict(scene="random", n=10000, depth=6, m=0, W=192, H=108, spp=2, md=4, oct=1, dyaw=20.0,
                        dpitch=-10.0),
+    # sphere-root edge cases (tests/test_emulation.py extreme_root_scene): camera inside a sphere,
+    # roots near 0, half_b^2 overflow, disc > 2^100.  Primary rays only: bounced off spheres of
+    # radius 1e18-1e19 a path is chaotic at float precision (the 0.001 self-intersection bound is far
+    # below the hit point's ULP there), and at maxDepth 4 llvmpipe and the oracle agree on no pixel
+    "extreme": dict(scene="extreme", n=7, depth=5, m=0, W=160, H=100, spp=1, md=1, oct=1, dyaw=0.0, dpitch=0.0),
     # the bench's C3 frame itself (3840x2160, 100k spheres, depth 8); 16 of its rows are kept
     "c3_full_rows": dict(scene="random", n=100000, depth=8, m=0, W=3840, H=2160, spp=1, md=1, oct=1, dyaw=0.0,
                          dpitch=0.0, rows=[0, 135, 270, 405, 540, 675, 810, 945, 1080, 1215, 1350, 1485, 1620, 1755,
@@ -59,6 +64,10 @@ def case_inputs(c):
         s = ort.random_spheres(c["n"], 42)
     elif c["scene"] == "prebuilt":
         s = ort.prebuilt_spheres()
+    elif c["scene"] == "extreme":
+        sys.path.insert(0, str(ROOT / "tests"))
+        from test_emulation import extreme_root_scene
+        s = extreme_root_scene(ort)
     else:
         s = ort.debug_spheres()
     t = ort.build_octree(s, c["depth"], c["m"])
