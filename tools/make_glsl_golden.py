@@ -50,7 +50,7 @@ CASES = {
     # sphere-root edge cases (tests/test_emulation.py extreme_root_scene): camera inside a sphere,
     # roots near 0, half_b^2 overflow, disc > 2^100.  Primary rays only: bounced off spheres of
     # radius 1e18-1e19 a path is chaotic at float precision (the 0.001 self-intersection bound is far
-    # below the hit point's ULP there), and at maxDepth 4 llvmpipe and the oracle agree on no pixel
+    # below the hit point's ULP there), and at maxDepth 4 llvmpipe and the oracle agree to 1e-6 on 0.07 % of pixels
     "extreme": dict(scene="extreme", n=7, depth=5, m=0, W=160, H=100, spp=1, md=1, oct=1, dyaw=0.0, dpitch=0.0),
     # the bench's C3 frame itself (3840x2160, 100k spheres, depth 8); 16 of its rows are kept
     "c3_full_rows": dict(scene="random", n=100000, depth=8, m=0, W=3840, H=2160, spp=1, md=1, oct=1, dyaw=0.0,
