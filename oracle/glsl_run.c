@@ -20,7 +20,11 @@
  * It draws into a W x H GL_RGBA32F framebuffer object instead of the window (the reference
  * never reads pixels back) and reads FragColor back as float.
  *
- * usage: glsl_run SHADER_DIR INPUT OUTPUT
+ * usage: glsl_run SHADER_DIR INPUT OUTPUT [PRELUDE]
+ *   PRELUDE (analysis only, tools/glsl_builtins_check.py): GLSL text inserted after the
+ *   fragment shader's #version line, in memory (the reference's file is never changed) -- used
+ *   to substitute the oracle's canonical builtins for llvmpipe's and so measure how much of
+ *   the remaining difference is the builtins'.
  *   INPUT (little endian): int32 W, H, numSamples, maxDepth, useOctree, nSpheres, nNodes,
  *   nIndices; float32 view[16] (column-major, as glUniformMatrix4fv takes glm), cameraPosition[3],
  *   cameraZoom; then float32[nSpheres*4] x3, float32[nNodes*4] x2, int32[nNodes],
@@ -112,7 +116,7 @@ static char *read_file(const char *path, size_t *n) {
 }
 
 int main(int argc, char **argv) {
-    if (argc != 4) die("usage: glsl_run SHADER_DIR INPUT OUTPUT");
+    if (argc != 4 && argc != 5) die("usage: glsl_run SHADER_DIR INPUT OUTPUT [PRELUDE]");
     size_t in_n = 0;
     char *in = read_file(argv[2], &in_n);
     if (!in || in_n < 8 * 4 + 20 * 4) die("bad input file");
@@ -133,6 +137,18 @@ int main(int argc, char **argv) {
     char *vs_src = read_file(path, NULL);
     snprintf(path, sizeof path, "%s/octree_fragment_shader.glsl", argv[1]);
     char *fs_src = read_file(path, NULL);
+    if (argc == 5 && fs_src) {  /* the prelude goes right after the #version line */
+        char *pre = read_file(argv[4], NULL);
+        char *nl = strchr(fs_src, '\n');
+        if (!pre || !nl || strncmp(fs_src, "#version", 8) != 0) die("cannot insert the prelude");
+        const size_t a = (size_t)(nl + 1 - fs_src), b = strlen(pre), c = strlen(nl + 1);
+        char *m = (char *)malloc(a + b + c + 1);
+        if (!m) die("out of memory");
+        memcpy(m, fs_src, a);
+        memcpy(m + a, pre, b);
+        memcpy(m + a + b, nl + 1, c + 1);
+        fs_src = m;
+    }
     if (!vs_src || !fs_src) die("cannot read the reference shaders");
 
     /* the driver and its loader-facing extensions */

@@ -1,4 +1,14 @@
-"""Parity pinned to the REFERENCE'S OWN shaders: tests/golden/glsl/*.npz are frames of
+"""Parity pinned to the REFERENCE'S OWN shaders, in two steps.
+
+1. Bit for bit.  GLSL leaves the precision of its builtins to the implementation.  With the
+   oracle's canonical builtins (include/ort_math.h, as GLSL in oracle/glsl_canonical_builtins.glsl)
+   in place of llvmpipe's, the reference's unmodified shaders produce frames BIT-IDENTICAL to the
+   oracle's -- and so to the HIP kernels' -- on every case of tests/golden/glsl/canonical.json:
+   C1, the DEBUG scene, M=1, C2, C3 (the whole 3840x2160 bench frame), brute force at 4 bounces,
+   the prebuilt scene at 4 samples x 8 bounces, C2 at 2 x 4 and (1920x1080) 4 x 8, the sphere-root
+   edge cases.  Only SHA-256s are stored.
+
+2. Within GLSL's tolerance, with llvmpipe's own builtins: tests/golden/glsl/*.npz are frames of
 /root/reference/shaders/{vertex_shader,octree_fragment_shader}.glsl run unmodified by a real GLSL
 4.30 implementation, the image's Mesa 23.2 llvmpipe (oracle/glsl_run.c, a headless DRI swrast
 loader; tools/make_glsl_golden.py made them), on this repo's seeded scenes and builder trees
@@ -99,6 +109,35 @@ def test_oracle_matches_reference_shader(ort, oracle, name):
     check_against_glsl(img, ref, meta, f"oracle vs GLSL {name}")
 
 
+CANON = json.loads((GOLD / "canonical.json").read_text())
+PRELUDE = Path(__file__).resolve().parents[1] / "oracle" / "glsl_canonical_builtins.glsl"
+
+
+def frame_sha(img):
+    import hashlib
+    return hashlib.sha256(np.ascontiguousarray(img, np.float32).tobytes()).hexdigest()
+
+
+def test_canonical_prelude_is_ort_math():
+    """The committed prelude is include/ort_math.h's canonical builtins, as generated now."""
+    import hashlib
+    import sys
+    sys.path.insert(0, str(PRELUDE.parents[1] / "tools"))
+    import glsl_builtins_check as B
+    assert B.prelude() == PRELUDE.read_text()
+    assert hashlib.sha256(PRELUDE.read_bytes()).hexdigest() == CANON["prelude_sha256"]
+    assert "llvmpipe" in CANON["renderer"] and len(CANON["cases"]) >= 12
+
+
+@pytest.mark.parametrize("name", sorted(CANON["cases"]))
+def test_oracle_bit_exact_to_reference_shader(ort, oracle, name):
+    c = CANON["cases"][name]
+    s, t, p = inputs(ort, c)
+    assert (t.n_nodes, t.n_indices) == (c["n_nodes"], c["n_indices"])
+    img = oracle.render(s, t if c["oct"] else None, p)
+    assert frame_sha(img) == c["sha256"], f"{name}: the oracle's frame is not the reference shader's"
+
+
 RUNNER = Path(__file__).resolve().parents[1] / "oracle" / "_ref" / "glsl_run"
 SHADERS = Path("/root/reference/shaders")
 
@@ -114,3 +153,14 @@ def test_fixtures_regenerate_bit_for_bit(name):
     img, renderer = M.run_glsl(*M.case_inputs(M.CASES[name]))
     assert renderer == meta["renderer"]
     assert np.array_equal(img.view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.skipif(not (RUNNER.exists() and SHADERS.exists()), reason="needs oracle/_ref/glsl_run and /root/reference")
+@pytest.mark.parametrize("name", ["c1", "prebuilt_spp4_d8", "c2_spp2_d4"])
+def test_canonical_hashes_regenerate(name):
+    """The canonical-builtin hashes are what the reference's shaders give now."""
+    import sys
+    sys.path.insert(0, str(RUNNER.parents[2] / "tools"))
+    import make_glsl_golden as M
+    img, _ = M.run_glsl(*M.case_inputs(CANON["cases"][name]), prelude=PRELUDE)
+    assert frame_sha(img) == CANON["cases"][name]["sha256"]

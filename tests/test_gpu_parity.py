@@ -351,3 +351,16 @@ def test_kernel_matches_reference_shader(ort, oracle, renderer, name):
         img, ref_o = renderer.render(p), oracle.render(s, tree, p)
     check_against_glsl(img, ref, meta, f"HIP vs GLSL {name}")
     assert_same(img, ref_o, f"HIP vs oracle {name}")
+
+
+@pytest.mark.parametrize("name", sorted(__import__("json").loads(
+    (__import__("pathlib").Path(__file__).parent / "golden" / "glsl" / "canonical.json").read_text())["cases"]))
+def test_kernel_bit_exact_to_reference_shader(ort, renderer, name):
+    """The HIP frame IS the reference shader's frame, bit for bit, once GLSL's implementation-
+    defined builtins are the canonical ones (tests/test_glsl_parity.py, canonical.json): the
+    whole 3840x2160 C3 bench frame and C2 at 4 samples x 8 bounces included."""
+    from test_glsl_parity import CANON, frame_sha, inputs
+    c = CANON["cases"][name]
+    s, t, p = inputs(ort, c)
+    renderer.upload(s, t)
+    assert frame_sha(renderer.render(p)) == c["sha256"], f"{name}: HIP frame differs from the reference shader's"

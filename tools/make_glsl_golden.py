@@ -10,10 +10,19 @@ byte-identical to the reference's own src/octree.cpp on every pinned tree
 (tests/golden/manifest.json).  Each fixture holds the frame (float32 RGB, GL row order; the
 shader's alpha is 1 everywhere and is checked, then dropped) and the case it was made from.
 
+With --canonical the same shaders run with oracle/glsl_canonical_builtins.glsl inserted after
+the fragment shader's #version line (glsl_run's PRELUDE, in memory): the oracle's canonical
+builtins (include/ort_math.h) in place of llvmpipe's sin/cos/tan/pow/normalize/dot/length/cross/
+reflect/min/max -- GLSL leaves their precision to the implementation, and this is one
+implementation of them.  Those frames are stored as SHA-256 only (tests/golden/glsl/
+canonical.json): the oracle and the HIP kernels must reproduce them bit for bit.
+
 usage: python tools/make_glsl_golden.py [case ...]
+       python tools/make_glsl_golden.py --canonical [case ...]
 """
 from __future__ import annotations
 
+import hashlib
 import json
 import os
 import subprocess
@@ -52,11 +61,27 @@ CASES = {
     # radius 1e18-1e19 a path is chaotic at float precision (the 0.001 self-intersection bound is far
     # below the hit point's ULP there), and at maxDepth 4 llvmpipe and the oracle agree to 1e-6 on 0.07 % of pixels
     "extreme": dict(scene="extreme", n=7, depth=5, m=0, W=160, H=100, spp=1, md=1, oct=1, dyaw=0.0, dpitch=0.0),
-    # the bench's C3 frame itself (3840x2160, 100k spheres, depth 8); 16 of its rows are kept
+    # the bench's C3 frame itself (3840x2160, 100k spheres, depth 8); 16 of its rows are kept (the
+    # --canonical hashes cover the whole frame: c3_full)
     "c3_full_rows": dict(scene="random", n=100000, depth=8, m=0, W=3840, H=2160, spp=1, md=1, oct=1, dyaw=0.0,
                          dpitch=0.0, rows=[0, 135, 270, 405, 540, 675, 810, 945, 1080, 1215, 1350, 1485, 1620, 1755,
                                            1890, 2159]),
 }
+
+
+# --canonical only (hashes of whole frames): the bench's C3 frame; C2 at 4 samples and 8 bounces
+CANON_EXTRA = {
+    "c3_full": dict(scene="random", n=100000, depth=8, m=0, W=3840, H=2160, spp=1, md=1, oct=1, dyaw=0.0, dpitch=0.0),
+    "c2_full_spp4_d8": dict(scene="random", n=10000, depth=6, m=0, W=1920, H=1080, spp=4, md=8, oct=1, dyaw=0.0,
+                            dpitch=0.0),
+}
+PRELUDE = ROOT / "oracle" / "glsl_canonical_builtins.glsl"
+
+
+def canonical_cases():
+    cc = {k: v for k, v in CASES.items() if "rows" not in v}
+    cc.update(CANON_EXTRA)
+    return cc
 
 
 def case_inputs(c):
@@ -91,11 +116,13 @@ def write_input(path, s, t, p):
             f.write(np.ascontiguousarray(a).tobytes())
 
 
-def run_glsl(s, t, p, timing=None):
-    """The frame (H, W, 3) and the renderer line; timing (a dict) gets the draw's wall ms."""
+def run_glsl(s, t, p, timing=None, prelude=None):
+    """The frame (H, W, 3) and the renderer line; timing (a dict) gets the draw's wall ms;
+    prelude: a GLSL file glsl_run inserts after the fragment shader's #version line."""
     with tempfile.TemporaryDirectory() as d:
         write_input(f"{d}/in.bin", s, t, p)
-        r = subprocess.run([str(RUNNER), str(SHADERS), f"{d}/in.bin", f"{d}/out.bin"], capture_output=True, text=True)
+        cmd = [str(RUNNER), str(SHADERS), f"{d}/in.bin", f"{d}/out.bin"] + ([str(prelude)] if prelude else [])
+        r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise SystemExit(f"glsl_run failed: {r.stderr}")
         img = np.fromfile(f"{d}/out.bin", np.float32).reshape(p.height, p.width, 4)
@@ -107,10 +134,34 @@ def run_glsl(s, t, p, timing=None):
     return np.ascontiguousarray(img[..., :3]), next(x for x in lines if "Mesa" in x)
 
 
+def frame_sha(img):
+    return hashlib.sha256(np.ascontiguousarray(img, np.float32).tobytes()).hexdigest()
+
+
+def canonical(names):
+    import glsl_builtins_check as B
+    PRELUDE.write_text(B.prelude())
+    path = OUT / "canonical.json"
+    doc = json.loads(path.read_text()) if path.exists() else {"cases": {}}
+    doc["prelude"] = "oracle/glsl_canonical_builtins.glsl"
+    doc["prelude_sha256"] = hashlib.sha256(PRELUDE.read_bytes()).hexdigest()
+    cc = canonical_cases()
+    for name in names or list(cc):
+        t0 = time.time()
+        s, t, p = case_inputs(cc[name])
+        img, renderer = run_glsl(s, t, p, prelude=PRELUDE)
+        doc["renderer"] = renderer
+        doc["cases"][name] = dict(cc[name], sha256=frame_sha(img), n_nodes=int(t.n_nodes), n_indices=int(t.n_indices))
+        print(f"{name}: {p.width}x{p.height} canonical builtins in {time.time() - t0:.1f} s", flush=True)
+    path.write_text(json.dumps(doc, indent=1, sort_keys=True) + "\n")
+
+
 def main():
     if not RUNNER.exists():
         raise SystemExit("build the runner first: make -C oracle glsl")
     OUT.mkdir(parents=True, exist_ok=True)
+    if sys.argv[1:2] == ["--canonical"]:
+        return canonical(sys.argv[2:])
     names = sys.argv[1:] or list(CASES)
     for name in names:
         c = CASES[name]
