@@ -10,10 +10,12 @@
  * reference's buffer layout (SSBO bindings 0-6, glsl:20-46), with the canonical builtins of
  * include/ort_math.h.  Pinning: the octree input is byte-for-byte the
  * reference's own src/octree.cpp's (oracle/_ref/ref_octree, tests/golden); the pixels are
- * checked against the reference's UNMODIFIED shaders run by the image's Mesa llvmpipe
- * (oracle/glsl_run.c, tests/golden/glsl, tests/test_glsl_parity.py): within 1e-6 on >= 99.99 %
- * of a primary-ray frame's pixels, the rest on sphere silhouettes -- GLSL's builtins have a
- * few ULP of freedom, so the pin is to rounding, not to every bit.
+ * checked against the reference's own shaders run by the image's Mesa llvmpipe
+ * (oracle/glsl_run.c, tests/golden/glsl, tests/test_glsl_parity.py): with GLSL's
+ * implementation-defined builtins set to the canonical ones of include/ort_math.h
+ * (oracle/glsl_canonical_builtins.glsl), this file's frames are BIT-IDENTICAL to the shader's
+ * (12 frames, multi-bounce and the full C3 bench frame included); with llvmpipe's own builtins
+ * within 1e-6 on >= 99.99 % of a primary-ray frame's pixels.
 
  * Differences from the GLSL, all forced: node offsets are int32 instead of float-in-
  * vec4.w; FragCoord is exactly (px+0.5, py+0.5) (vertex_shader.glsl:15);
