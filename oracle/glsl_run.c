@@ -221,7 +221,13 @@ int main(int argc, char **argv) {
     GLF(PFNGLREADBUFFERPROC, glReadBuffer);
     GLF(PFNGLPIXELSTOREIPROC, glPixelStorei);
     GLF(PFNGLREADPIXELSPROC, glReadPixels);
+    GLF(PFNGLGETINTEGER64VPROC, glGetInteger64v);
     fprintf(stderr, "glsl_run: %s / %s\n", (const char *)glGetString(GL_RENDERER), (const char *)glGetString(GL_VERSION));
+    /* (llvmpipe reports a 128 MiB GL_MAX_SHADER_STORAGE_BLOCK_SIZE but reads larger buffers whole:
+     * the C3 node arrays, 175 MB each, give frames bit-identical to the oracle's) */
+    GLint64 max_ssbo = 0;
+    glGetInteger64v(GL_MAX_SHADER_STORAGE_BLOCK_SIZE, &max_ssbo);
+    fprintf(stderr, "glsl_run: GL_MAX_SHADER_STORAGE_BLOCK_SIZE %lld\n", (long long)max_ssbo);
 
     /* the reference's program */
     GLuint sh[2];
