@@ -5,8 +5,9 @@ tools/make_glsl_golden.py: as they are, and with a PRELUDE inserted after the fr
 #version line (in memory; the reference's file is never touched) that substitutes the oracle's
 canonical builtins (include/ort_math.h: double-precision sin/cos/pow with fma, the glm forms of
 normalize/dot/length/cross/reflect, min/max in the GLSL spec's (y < x) ? y : x form) for llvmpipe's, via function-like macros -- and compares both
-frames with the CPU oracle.  What the prelude cannot reach is llvmpipe's own arithmetic in the
-shader's expressions (e.g. fused multiply-adds), so the second frame still need not be bit-equal.
+frames with the CPU oracle.  (What a prelude cannot reach is llvmpipe's own arithmetic in the
+shader's expressions; measured, it changes nothing there: with the prelude every frame of
+tests/golden/glsl/canonical.json is bit-identical to the oracle's.)
 usage: LP_NUM_THREADS=8 python tools/glsl_builtins_check.py [case ...]"""
 import re
 import sys
@@ -131,17 +132,12 @@ vec3 ort_max(vec3 x, vec3 y) {{ return vec3(ort_max(x.x, y.x), ort_max(x.y, y.y)
 
 
 def run(s, t, p, pre=None):
-    import subprocess
+    """The GLSL frame, with the prelude text pre inserted (or as is)."""
+    if pre is None:
+        return M.run_glsl(s, t, p)[0]
     with tempfile.TemporaryDirectory() as d:
-        M.write_input(f"{d}/in.bin", s, t, p)
-        cmd = [str(M.RUNNER), str(M.SHADERS), f"{d}/in.bin", f"{d}/out.bin"]
-        if pre is not None:
-            Path(f"{d}/pre.glsl").write_text(pre)
-            cmd.append(f"{d}/pre.glsl")
-        r = subprocess.run(cmd, capture_output=True, text=True)
-        if r.returncode != 0:
-            raise SystemExit(f"glsl_run failed: {r.stderr[-3000:]}")
-        return np.fromfile(f"{d}/out.bin", np.float32).reshape(p.height, p.width, 4)[..., :3].copy()
+        Path(f"{d}/pre.glsl").write_text(pre)
+        return M.run_glsl(s, t, p, prelude=f"{d}/pre.glsl")[0]
 
 
 def stats(img, o):
