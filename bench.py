@@ -52,6 +52,25 @@ CONFIGS = {
 }
 
 
+def reference_frame_check(config: str, frame, host=None):
+    """SHA-256 of the bench's assembled static frame (float32 RGB, GL rows) against the frame the
+    reference's own shaders give for the same scene and camera -- run on Mesa llvmpipe with the
+    canonical builtins, tests/golden/glsl/canonical.json (tests/test_glsl_parity.py).  None when
+    no such hash exists for the config (C5: its tree is too large for llvmpipe) or no frame."""
+    cases = {"c1": "c1", "c2": "c2_full", "c3": "c3_full"}
+    path = Path(__file__).resolve().parent / "tests" / "golden" / "glsl" / "canonical.json"
+    if frame is None or config not in cases or not path.exists():
+        return None
+    ref = json.loads(path.read_text())["cases"][cases[config]]
+    W, H, N, D, M, NS, MD = CONFIGS[config]
+    assert (ref["W"], ref["H"], ref["n"], ref["depth"], ref["m"], ref["spp"], ref["md"]) == (W, H, N, D, M, NS, MD)
+    img = host if host is not None else (frame.cpu().numpy() if hasattr(frame, "cpu") else np.asarray(frame))
+    got = hashlib.sha256(np.ascontiguousarray(img, np.float32).tobytes()).hexdigest()
+    return {"frame_sha256": got, "reference_shader_frame_sha256": ref["sha256"], "bit_identical": got == ref["sha256"],
+            "reference": "the reference's shaders/octree_fragment_shader.glsl on Mesa llvmpipe with canonical "
+                         "builtins, same scene and camera (tests/golden/glsl/canonical.json, case %s)" % cases[config]}
+
+
 def default_inflight(config: str, world: int) -> int:
     """Frames in flight by default: 2 when a GPU's share of a frame is at most 40 M pixel-bounces,
     where the longest walks' drain at the end of every launch would otherwise idle much of the
@@ -448,6 +467,8 @@ def _main():
     elapsed = time.perf_counter() - t0
     # the static camera's frame (the later phases reuse the frame buffer)
     saved = frame.cpu().numpy() if (args.save and rank == 0 and frame is not None) else None
+    # the assembled static frame against the reference's own shaders (outside the timed region)
+    parity = reference_frame_check(args.config, frame, saved) if rank == 0 else None
     kern_ms = [a.elapsed_time(b) for a, b, _ in evs]       # whole per-frame pipeline (trace+shade+sort)
     latency_ms = [a.elapsed_time(c) for a, _, c in evs]    # render start -> frame gathered and assembled
     nframes0 = min(-(-args.steps // inflight), 64)          # context 0's timed frames
@@ -657,6 +678,7 @@ def _main():
             "roofline": roofline(pmc, counts, (pmc or {}).get("traversals_per_frame"), alg_bytes,
                                  float(np.mean(trace_ms)), kernels),
             "setup": setup,
+            "parity": parity,
             "build_sha": lib_sha(),
             "device_sha": device_sha(),
         }
@@ -872,7 +894,7 @@ def emulate(args, world, rank):
                           "scaling": "strong", "vs_baseline": None, "dtype": "f32",
                           "data": "EMULATION (host build of the kernel code, gloo): a control-path test, not a "
                                   "measurement", "config": {"workload": args.config, "width": W, "height": H},
-                          "frame_sha256": digest}), flush=True)
+                          "frame_sha256": digest, "parity": reference_frame_check(args.config, frame)}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

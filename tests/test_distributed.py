@@ -176,7 +176,8 @@ def test_gather_wait_is_bounded():
 def test_bench_self_launch(world):
     """`bench.py --gpus N` with no launcher starts its own N ranks (torch.distributed.run as a
     child process) and prints rank 0's line only; --emulate renders on the host and gathers
-    with gloo.  The assembled frame equals the oracle's single-process frame."""
+    with gloo.  The assembled frame equals the oracle's single-process frame and the reference
+    shaders' frame."""
     import hashlib
     import subprocess
     import sys
@@ -194,6 +195,8 @@ def test_bench_self_launch(world):
     t = ort.build_octree(s, 4, 0)
     ref = oracle.render(s, t, ort.FrameParams.default_camera(256, 256))
     assert line["frame_sha256"] == hashlib.sha256(np.ascontiguousarray(ref).tobytes()).hexdigest()
+    # ... and the reference's own shaders' frame (tests/test_glsl_parity.py), bit for bit
+    assert line["parity"]["bit_identical"] and line["parity"]["frame_sha256"] == line["frame_sha256"]
 
 
 def test_bench_group_arguments(monkeypatch):

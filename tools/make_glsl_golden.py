@@ -69,8 +69,10 @@ CASES = {
 }
 
 
-# --canonical only (hashes of whole frames): the bench's C3 frame; C2 at 4 samples and 8 bounces
+# --canonical only (hashes of whole frames): the bench's C2 and C3 frames (bench.py checks its own frame
+# against them); C2 at 4 samples and 8 bounces
 CANON_EXTRA = {
+    "c2_full": dict(scene="random", n=10000, depth=6, m=0, W=1920, H=1080, spp=1, md=1, oct=1, dyaw=0.0, dpitch=0.0),
     "c3_full": dict(scene="random", n=100000, depth=8, m=0, W=3840, H=2160, spp=1, md=1, oct=1, dyaw=0.0, dpitch=0.0),
     "c2_full_spp4_d8": dict(scene="random", n=10000, depth=6, m=0, W=1920, H=1080, spp=4, md=8, oct=1, dyaw=0.0,
                             dpitch=0.0),
