@@ -76,6 +76,13 @@ CANON_EXTRA = {
     "c3_full": dict(scene="random", n=100000, depth=8, m=0, W=3840, H=2160, spp=1, md=1, oct=1, dyaw=0.0, dpitch=0.0),
     "c2_full_spp4_d8": dict(scene="random", n=10000, depth=6, m=0, W=1920, H=1080, spp=4, md=8, oct=1, dyaw=0.0,
                             dpitch=0.0),
+    # trees deeper than 8 levels (C5's kind: depth 10, maxSpheresPerNode 1, 4 bounces) take the
+    # HIP path's deep kernels (96-bit level masks, the depth 9-10 persistent bounce walk); C5's own
+    # 239 M-node tree is too large for llvmpipe, these are not
+    "deep_d10_m1_b4": dict(scene="random", n=50000, depth=10, m=1, W=640, H=360, spp=1, md=4, oct=1, dyaw=0.0,
+                           dpitch=0.0),
+    "deep_d9_m1_spp2_b3": dict(scene="random", n=20000, depth=9, m=1, W=320, H=180, spp=2, md=3, oct=1, dyaw=15.0,
+                               dpitch=-6.0),
 }
 PRELUDE = ROOT / "oracle" / "glsl_canonical_builtins.glsl"
 
