@@ -5,8 +5,8 @@
    in place of llvmpipe's, the reference's unmodified shaders produce frames BIT-IDENTICAL to the
    oracle's -- and so to the HIP kernels' -- on every case of tests/golden/glsl/canonical.json:
    C1, the DEBUG scene, M=1, C2, the whole 1920x1080 C2 and 3840x2160 C3 bench frames, brute force at 4 bounces,
-   the prebuilt scene at 4 samples x 8 bounces, C2 at 2 x 4 and (1920x1080) 4 x 8, the sphere-root
-   edge cases.  Only SHA-256s are stored.
+   the prebuilt scene at 4 samples x 8 bounces, C2 at 2 x 4 and (1920x1080) 4 x 8, depth-9/10
+   M=1 trees with bounces (the HIP deep kernels), the sphere-root edge cases.  Only SHA-256s are stored.
 
 2. Within GLSL's tolerance, with llvmpipe's own builtins: tests/golden/glsl/*.npz are frames of
 /root/reference/shaders/{vertex_shader,octree_fragment_shader}.glsl run unmodified by a real GLSL
