@@ -1960,6 +1960,7 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     a.final_out = fuse_first ? 1 : 0;
     a.key_spread = (const uint32_t*)ctx->key_spread.p;
     // the cost order: the per-workgroup camera-ray kernels (ort_trace_compact[_deep]) only
+    bool cam_moved = false;  // the camera moved since this context's last frame (cost order on)
     if (mode == 0 && ctx->cost_order && ctx->depth >= 2) {
         if ((rc = ensure(ctx, ctx->pcost, 2 * slots))) return rc;
         const unsigned long long sig = frame_sig(ctx, p, t);
@@ -1974,8 +1975,8 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
         // correlation of 0.82 with the new walks, reprojected ones 0.05 -- profiles/r05_moving_*),
         // and raising the wrong waves costs: C3 moving frames 1.855 -> 1.798 ms without it
         // (profiles/r05_moving_shift_c3.log), static frames unchanged
-        const bool moved = std::memcmp(&ctx->prio_cam, &a.pp.cam, sizeof(ort::KCamera)) != 0;
-        a.prio_steps = moved ? 0 : ctx->heavy_prio;
+        cam_moved = std::memcmp(&ctx->prio_cam, &a.pp.cam, sizeof(ort::KCamera)) != 0;
+        a.prio_steps = cam_moved ? 0 : ctx->heavy_prio;
         if (!dcounters) ctx->prio_cam = a.pp.cam;
     }
     // split walks of the heavy camera rays (1 sample; the production kernels, bounce 0)
@@ -2006,6 +2007,13 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
         bcost = (uint16_t*)ctx->bcost.p;
         a.heavy = ctx->heavy_first;
     }
+    // ... whose classes are read only while the camera stands still (the steps are recorded
+    // always): after a move last frame's bounce walks are not this frame's, and sorting stale
+    // heavy paths first cost C5's moving frames 0.8 % (1568 -> 1556 Mrays/s, bench --opt HEAVY_FIRST=0)
+#ifndef ORT_HEAVY_FIRST_STATIC_ONLY
+#define ORT_HEAVY_FIRST_STATIC_ONLY 1
+#endif
+    const uint16_t* bcost_rd = (ORT_HEAVY_FIRST_STATIC_ONLY && cam_moved) ? nullptr : bcost;
     const int key_bits = bcost ? ort::kPathKeyBits + kHeavyKeyBits : ort::kPathKeyBits;
     const size_t lds = lds_bytes(mode, ctx->depth, false);
     const size_t lds_exact = lds_bytes(mode, ctx->depth, true);
@@ -2071,7 +2079,7 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                 {   // heavy first: record index smp * bounces + b (bounces >= 1 only)
                     const int hi = smp * bounces + b;
                     if (bcost && pb > 0 && b > 0 && hi < nbc) at.bcost_w = bcost + (size_t)hi * slots;
-                    if (bcost && fmode == 2 && hi + 1 < nbc && b + 1 < bounces) at.bcost_r = bcost + (size_t)(hi + 1) * slots;
+                    if (bcost_rd && fmode == 2 && hi + 1 < nbc && b + 1 < bounces) at.bcost_r = bcost_rd + (size_t)(hi + 1) * slots;
                 }
                 const bool do_split = split && (fmode == 1 || fmode == 2);
                 const unsigned long long fsig = do_split ? frame_sig(ctx, p, t) : 0ull;
@@ -2176,7 +2184,7 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                     a2.qnext_count = qcnt[cur ^ 1];
                     a2.qnext_keys = listsort ? (uint32_t*)ctx->skeys.p : nullptr;
                     const int hn = smp * bounces + b + 1;  // the next bounce's record
-                    if (bcost && hn < nbc) a2.bcost_r = bcost + (size_t)hn * slots;
+                    if (bcost_rd && hn < nbc) a2.bcost_r = bcost_rd + (size_t)hn * slots;
                 }
                 e = launch_shade(mode, b == 0, direct, a2, (int)blocks, s);
                 if (e != hipSuccess) return hip_fail(ctx, e, "ort_shade_kernel launch");
