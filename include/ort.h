@@ -118,8 +118,9 @@ typedef struct ort_scene_info {
                                       trace) order paths by the steps their walk at that bounce took in
                                       the previous frame of the same shape -- >= 4T first, then >= 2T,
                                       >= T, the rest, each class in coherence order -- so the longest
-                                      walks start early rather than in the launch's drain tail (same
-                                      pixels); 0: coherence order only */
+                                      walks start early rather than in the launch's drain tail -- while
+                                      the camera stands still (after a move the steps are stale); same
+                                      pixels.  0: coherence order only */
 #define ORT_OPT_HEAVY_PRIO 13      /* T > 0 (default 150): a wave of the camera-ray trace (cost order on)
                                       that holds a ray whose walk took >= T steps in the previous frame of
                                       the same shape runs at raised issue priority (s_setprio), so the
