@@ -96,6 +96,11 @@ struct PipeArgs {
     uint16_t* bcost_w;        // ORT_OPT_HEAVY_FIRST: the persistent bounce trace records each walk's steps here
     const uint16_t* bcost_r;  // ... the kernels appending the next bounce's list read that bounce's last-frame steps
     int heavy;                // ... walks of at least this many steps are heavy: they sort first
+    // ... and after a camera move (no fresh steps), the class of a path from its ray alone: the
+    // root box (lo xyz, hi xyz) and the exit-distance thresholds of classes 0-2 (geo_heavy)
+    int geo_heavy;
+    float gbox[6];
+    float gthr[3];
     int prio_steps;   // ORT_OPT_HEAVY_PRIO: a camera-ray wave holding a ray whose last walk took >= this many
                       // steps runs at raised issue priority (0: off)
     // ORT_OPT_SPLIT_HEAVY (1 sample, 1 bounce): the camera rays whose walk took >= split steps in the
@@ -663,12 +668,34 @@ static_assert(ORT_HEAVY_LEVELS >= 1 && ORT_HEAVY_LEVELS <= 7, "ORT_HEAVY_LEVELS:
 constexpr int kHeavyKeyBits = ORT_HEAVY_LEVELS > 3 ? 3 : (ORT_HEAVY_LEVELS > 1 ? 2 : 1);
 // the class sits above the path key's bits in a 32-bit radix key (sortListBounded's end bit)
 static_assert(ort::kPathKeyBits + kHeavyKeyBits <= 32, "heavy-first class bits + path key bits exceed 32");
+// Heavy first after a camera move: the class from the new ray alone -- bounce walks of rays that
+// leave the root box soon run longest (the C5 slab, bounce 1: exit within 1.2x the box's
+// smallest extent, half of the rays, 29 % of them >= 256 steps; beyond 6.8x, 0.5 %;
+// tools/bounce_texit.py).  Classes 0-2 by the thresholds gthr, 3 beyond (as light_bit's).
+__device__ __forceinline__ uint32_t geo_class_bits(const float* gb, const float* th, float4 o, float4 d) {
+    float tx = 3.0e38f;
+    const float oa[3] = {o.x, o.y, o.z}, da[3] = {d.x, d.y, d.z};
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float inv = 1.0f / da[a];  // (+-inf for a zero component: that axis never bounds)
+        const float t = fmaxf((gb[a] - oa[a]) * inv, (gb[3 + a] - oa[a]) * inv);
+        tx = fminf(tx, t);
+    }
+    const uint32_t cls = tx <= th[0] ? 0u : (tx <= th[1] ? 1u : (tx <= th[2] ? 2u : 3u));
+    return min(cls, (uint32_t)ORT_HEAVY_LEVELS) << ort::kPathKeyBits;
+}
 __device__ __forceinline__ uint32_t light_bit(const uint16_t* bcost_r, int heavy, int k) {
     if (!bcost_r) return 0u;
     const int c = bcost_r[k];
     uint32_t cls = ORT_HEAVY_LEVELS;
     for (int l = 0; l < ORT_HEAVY_LEVELS; ++l) cls -= c >= (heavy << (ORT_HEAVY_RATIO_LOG2 * l)) ? 1u : 0u;
     return cls << ort::kPathKeyBits;
+}
+// The sort key of path k (its state just stored) with its heavy-first class.
+__device__ __forceinline__ uint32_t path_key_class(const PipeArgs& A, int k) {
+    const float4 o = A.po[k], d = A.pd[k];
+    return ort::path_key(o, d, A.mp, A.key_spread) |
+           (A.geo_heavy ? geo_class_bits(A.gbox, A.gthr, o, d) : light_bit(A.bcost_r, A.heavy, k));
 }
 
 // One ray per lane over the compact layout (default): the tile-block order of the path
@@ -920,8 +947,11 @@ __device__ __forceinline__ void trace_compact_body(PipeArgs& A, unsigned char* s
         typedef __attribute__((address_space(4))) const PipeArgs KernArgs;
         KernArgs* kp = (KernArgs*)__builtin_amdgcn_kernarg_segment_ptr();
         uint32_t key = 0;
-        if (go && kp->qnext_keys)  // the state just stored
-            key = ort::path_key(kp->po[k], kp->pd[k], kp->mp, kp->key_spread) | light_bit(kp->bcost_r, kp->heavy, k);
+        if (go && kp->qnext_keys) {  // the state just stored
+            const float4 o = kp->po[k], d = kp->pd[k];
+            key = ort::path_key(o, d, kp->mp, kp->key_spread) |
+                  (kp->geo_heavy ? geo_class_bits(kp->gbox, kp->gthr, o, d) : light_bit(kp->bcost_r, kp->heavy, k));
+        }
         append_slots(go, k, key, kp->qnext, kp->qnext_keys, kp->qnext_count);
 #endif
     }
@@ -971,8 +1001,11 @@ __device__ __forceinline__ void trace_pair_body(PipeArgs& A, unsigned char* smem
 #if defined(__HIP_DEVICE_COMPILE__)
             KernArgs* kq = (KernArgs*)__builtin_amdgcn_kernarg_segment_ptr();
             uint32_t key = 0;
-            if (go && kq->qnext_keys)
-                key = ort::path_key(kq->po[k], kq->pd[k], kq->mp, kq->key_spread) | light_bit(kq->bcost_r, kq->heavy, k);
+            if (go && kq->qnext_keys) {
+                const float4 o = kq->po[k], d = kq->pd[k];
+                key = ort::path_key(o, d, kq->mp, kq->key_spread) |
+                      (kq->geo_heavy ? geo_class_bits(kq->gbox, kq->gthr, o, d) : light_bit(kq->bcost_r, kq->heavy, k));
+            }
             append_slots(go, k, key, kq->qnext, kq->qnext_keys, kq->qnext_count);
 #endif
         }
@@ -1138,7 +1171,7 @@ __global__ void __launch_bounds__(kBlock) ort_trace_split(PipeArgs A) {
                     const int q = atomicAdd(A.qnext_count, 1);
                     A.qnext[q] = k;
                     if (A.qnext_keys)
-                        A.qnext_keys[q] = ort::path_key(A.po[k], A.pd[k], A.mp, A.key_spread) | light_bit(A.bcost_r, A.heavy, k);
+                        A.qnext_keys[q] = path_key_class(A, k);
                 }
             }
         }
@@ -1213,7 +1246,7 @@ __global__ void __launch_bounds__(kBlock) ort_trace_exact(PipeArgs A) {
                 const int pos = atomicAdd(A.qnext_count, 1);
                 A.qnext[pos] = k;
                 if (A.qnext_keys)
-                    A.qnext_keys[pos] = ort::path_key(A.po[k], A.pd[k], A.mp, A.key_spread) | light_bit(A.bcost_r, A.heavy, k);
+                    A.qnext_keys[pos] = path_key_class(A, k);
             }
         } else {
             A.hit[k] = make_int2(st == ORT_TRACE_HIT ? entry : -1, __float_as_int(t));
@@ -1280,7 +1313,7 @@ __global__ void __launch_bounds__(kBlock) ort_shade_kernel(PipeArgs A) {
     if (!DIRECT && A.qnext) {
         uint32_t key = 0;
         if (go && A.qnext_keys)  // the state just stored
-            key = ort::path_key(A.po[k], A.pd[k], A.mp, A.key_spread) | light_bit(A.bcost_r, A.heavy, k);
+            key = path_key_class(A, k);
         append_slots(go, k, key, A.qnext, A.qnext_keys, A.qnext_count);
     }
 }
@@ -2014,6 +2047,21 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
 #define ORT_HEAVY_FIRST_STATIC_ONLY 1
 #endif
     const uint16_t* bcost_rd = (ORT_HEAVY_FIRST_STATIC_ONLY && cam_moved) ? nullptr : bcost;
+#ifndef ORT_GEO_HEAVY
+#define ORT_GEO_HEAVY 1
+#endif
+    if (ORT_GEO_HEAVY && bcost && !bcost_rd) {  // moved: classes from the rays themselves (geo_class_bits)
+        a.geo_heavy = 1;
+        float m = 3.0e38f;
+        for (int q = 0; q < 3; ++q) {
+            a.gbox[q] = ctx->root_lo[q];
+            a.gbox[3 + q] = ctx->root_hi[q];
+            m = std::min(m, ctx->root_hi[q] - ctx->root_lo[q]);
+        }
+        a.gthr[0] = 1.2f * m;
+        a.gthr[1] = 2.7f * m;
+        a.gthr[2] = 6.8f * m;
+    }
     const int key_bits = bcost ? ort::kPathKeyBits + kHeavyKeyBits : ort::kPathKeyBits;
     const size_t lds = lds_bytes(mode, ctx->depth, false);
     const size_t lds_exact = lds_bytes(mode, ctx->depth, true);

@@ -96,6 +96,30 @@ def test_heavy_first_frames_match_coherence_order(ort, oracle, depth):
     assert_same(got[48][2][120:128], ref, f"depth {depth} heavy first vs oracle")
 
 
+@pytest.mark.parametrize("depth", [8, 10])
+def test_heavy_first_moving_camera(ort, oracle, depth):
+    """Heavy first with the camera turning: a moved frame sorts its bounce lists by classes from
+    the rays themselves (the root-box exit distance, geo_class_bits), a frame of an unmoved
+    camera by last frame's walk steps -- the frames stay bit-identical to coherence order and to
+    the oracle, on the depth <= 8 and the depth 9-10 persistent kernel."""
+    from octreeraytracer_amd.scene import DEFAULT_YAW
+    s = ort.random_spheres(20000, 42)
+    t = ort.build_octree(s, depth, 1)
+    W, H = 320, 180
+    ps = [ort.FrameParams.default_camera(W, H, num_samples=1, max_depth=4, yaw=DEFAULT_YAW + 0.5 * j)
+          for j in (0, 0, 1, 2, 2)]  # static, moved, moved, static
+    got = {}
+    for thr in (0, 48):
+        with ort.Renderer(0) as r:
+            r.upload(s, t)
+            r.set_heavy_first(thr)
+            got[thr] = [r.render(p) for p in ps]
+    for i in range(len(ps)):
+        assert_same(got[48][i], got[0][i], f"depth {depth}, frame {i}: heavy first vs coherence order")
+    ref = oracle.render(s, t, ps[3], 0, 80, W, 8, threads=0)
+    assert_same(got[48][3][80:88], ref, f"depth {depth}, moved frame vs oracle")
+
+
 def test_heavy_first_option_range(ort):
     with ort.Renderer(0) as r:
         with pytest.raises(ort.OrtError):
