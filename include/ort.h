@@ -118,9 +118,11 @@ typedef struct ort_scene_info {
                                       trace) order paths by the steps their walk at that bounce took in
                                       the previous frame of the same shape -- >= 4T first, then >= 2T,
                                       >= T, the rest, each class in coherence order -- so the longest
-                                      walks start early rather than in the launch's drain tail -- while
-                                      the camera stands still (after a move the steps are stale); same
-                                      pixels.  0: coherence order only */
+                                      walks start early rather than in the launch's drain tail.  After a
+                                      camera move (the steps are stale) the classes come from the rays
+                                      themselves instead: the distance to the root box's exit, within
+                                      1.2 / 2.7 / 6.8 x its smallest extent.  Same pixels.  0: coherence
+                                      order only */
 #define ORT_OPT_HEAVY_PRIO 13      /* T > 0 (default 150): a wave of the camera-ray trace (cost order on)
                                       that holds a ray whose walk took >= T steps in the previous frame of
                                       the same shape runs at raised issue priority (s_setprio), so the
