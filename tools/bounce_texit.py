@@ -2,6 +2,7 @@
 bounce-b walks of a 512x256 window (ort_debug_bounce_walks) against each ray's root-box exit
 distance -- a history-free heavy-path class for moving cameras.  usage: python tools/bounce_texit.py [config] [bounce]"""
 import ctypes as C, sys, numpy as np
+import ctypes as C, sys, numpy as np
 sys.path.insert(0, '/root/repo'); sys.path.insert(0, '/root/repo/tools')
 import bench, octreeraytracer_amd as ort
 from octreeraytracer_amd import _lib as L
@@ -35,3 +36,25 @@ q = np.quantile(texit, [0.25, 0.5, 0.75, 0.9])
 for a, b in zip([-1] + list(q), list(q) + [1e30]):
     m = (texit > a) & (texit <= b)
     print('  t_exit in (%.3g, %.3g]: steps mean %.1f  share >= 256: %.3f' % (a, b, st[m].mean(), np.mean(st[m] >= 256)))
+ext = hi - lo
+F = (np.abs(d) * texit[:, None] / ext).sum(1)
+G = (np.abs(d) * np.minimum(texit, 1e9)[:, None] / ext)
+def sp(a, b):
+    return np.corrcoef(np.argsort(np.argsort(a)), np.argsort(np.argsort(b)))[0, 1]
+print(' spearman: t_exit %.3f  F=sum|d_a| t_exit/ext_a %.3f  |d.y| %.3f  Fy %.3f  Fxz %.3f' % (sp(st, texit), sp(st, F), sp(st, np.abs(d[:, 1])), sp(st, G[:, 1]), sp(st, G[:, 0] + G[:, 2])))
+q = np.quantile(F, [0.5, 0.75, 0.9])
+for a_, b_ in zip([-1] + list(q), list(q) + [1e30]):
+    m = (F > a_) & (F <= b_)
+    print('  F in (%.3g, %.3g]: steps mean %.1f  share >= 256: %.3f  share of rays %.2f' % (a_, b_, st[m].mean(), np.mean(st[m] >= 256), m.mean()))
+rate = (np.abs(d) / ext).sum(1)   # cell crossings per unit length (x 2^D)
+mext = ext.min()
+for lam in (0.25, 0.5, 1.0, 2.0, 4.0, 1e9):
+    Hf = np.minimum(texit, lam * mext) * rate
+    print('  lambda %.2g x min extent: spearman %.3f' % (lam, sp(st, Hf)))
+print('  rate alone: %.3f' % sp(st, rate))
+Hf = np.minimum(texit, mext) * rate
+qs = np.quantile(Hf, [0.25, 0.5, 0.75, 0.9])
+print('  H quantiles 25/50/75/90%:', ' '.join('%.4f' % v for v in qs))
+for a_, b_ in zip([-1] + list(qs), list(qs) + [1e30]):
+    m = (Hf > a_) & (Hf <= b_)
+    print('  H in (%.4g, %.4g]: steps mean %.1f  share >= 256: %.3f  >= 128: %.3f  rays %.2f' % (a_, b_, st[m].mean(), np.mean(st[m] >= 256), np.mean(st[m] >= 128), m.mean()))
