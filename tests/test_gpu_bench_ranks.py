@@ -52,6 +52,7 @@ def test_bench_ranks_assemble_the_c3_frame(c3_frame, world, tmp_path):
     got = image.read_pfm(out)
     assert got.shape == c3_frame.shape and got.dtype == np.float32
     assert np.array_equal(got.view(np.uint32), c3_frame.view(np.uint32))
+    assert line["parity"]["bit_identical"], line["parity"]  # ... and the reference shaders' frame
 
 
 @pytest.mark.parametrize("world,inflight", [(4, 2), (8, 0)])
@@ -70,6 +71,7 @@ def test_bench_group_rehearsal_is_bit_identical(world, inflight):
     assert len(lines) == 1, r.stdout[-2000:]
     line = json.loads(lines[0])
     assert line["frame_check"].startswith("bit-identical"), line["frame_check"]
+    assert line["parity"]["bit_identical"], line["parity"]  # the group's frame IS the reference shaders'
     assert line["n_gpus"] == world and line["config"]["devices"] == [0] * world
     assert line["config"]["rays_per_step"] == 3840 * 2160
     import bench
