@@ -102,7 +102,10 @@ def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    # untimed warm-up frames: a C3 frame keeps getting faster over the first ~15 frames of a
+    # process (the clocks ramping up, profiles/r05_c3_warm3.md): 20 by default measures the steady
+    # state (C3 +2.3 % over 5: profiles/r05_warmup_c3.log); 20 C5 frames take ~0.8 s
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
