@@ -18,9 +18,9 @@ for step in "$@"; do
         timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
             > $OUT/pytest_all.log 2>&1 || { tail -30 $OUT/pytest_all.log; exit 1; } ;;
     c3)
-        timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > $OUT/bench_c3.json 2> $OUT/bench_c3.err || exit 1 ;;
+        timeout -k 10 300 python -u bench.py > $OUT/bench_c3.json 2> $OUT/bench_c3.err || exit 1 ;;
     c5)
-        timeout -k 10 400 python -u bench.py --config c5 --steps 10 --warmup 3 --no-cpu-baseline \
+        timeout -k 10 400 python -u bench.py --config c5 --steps 10 --no-cpu-baseline \
             > $OUT/bench_c5.json 2> $OUT/bench_c5.err || exit 1 ;;
     *) echo "unknown step $step"; exit 2 ;;
     esac
