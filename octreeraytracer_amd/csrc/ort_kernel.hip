@@ -2046,7 +2046,10 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
 #ifndef ORT_HEAVY_FIRST_STATIC_ONLY
 #define ORT_HEAVY_FIRST_STATIC_ONLY 1
 #endif
-    const uint16_t* bcost_rd = (ORT_HEAVY_FIRST_STATIC_ONLY && cam_moved) ? nullptr : bcost;
+#ifndef ORT_GEO_ALWAYS
+#define ORT_GEO_ALWAYS 0  // analysis: the rays' own classes on every frame (tools/ab_stream.py)
+#endif
+    const uint16_t* bcost_rd = ((ORT_HEAVY_FIRST_STATIC_ONLY && cam_moved) || ORT_GEO_ALWAYS) ? nullptr : bcost;
 #ifndef ORT_GEO_HEAVY
 #define ORT_GEO_HEAVY 1
 #endif
