@@ -2061,9 +2061,11 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
             a.gbox[3 + q] = ctx->root_hi[q];
             m = std::min(m, ctx->root_hi[q] - ctx->root_lo[q]);
         }
-        a.gthr[0] = 1.2f * m;
-        a.gthr[1] = 2.7f * m;
-        a.gthr[2] = 6.8f * m;
+#ifndef ORT_GEO_T
+#define ORT_GEO_T 1.2f, 2.7f, 6.8f  // the class thresholds, in units of the box's smallest extent
+#endif
+        const float gt[3] = {ORT_GEO_T};
+        for (int q = 0; q < 3; ++q) a.gthr[q] = gt[q] * m;
     }
     const int key_bits = bcost ? ort::kPathKeyBits + kHeavyKeyBits : ort::kPathKeyBits;
     const size_t lds = lds_bytes(mode, ctx->depth, false);
