@@ -534,7 +534,8 @@ def _main():
     # moving camera: the cost order and heavy-first lists deal work by the previous frame's walk
     # steps, which a static camera makes exact; an interactive caller turns the camera
     # (src/main.cpp:120-163).  The same pipeline, the camera turning yaw_step degrees per frame
-    # from the static pose, so every frame's hints are one frame stale (after the main timed
+    # from the static pose, so every frame's hints are stale (by frames_in_flight frames: each
+    # context renders every frames_in_flight-th frame; after the main timed
     # region, not part of `value`)
     moving = None
     if args.moving_steps > 0:
@@ -569,7 +570,7 @@ def _main():
         moving = (float(t_mov.item()), None if mov_rays is None else float(mov_rays.item()))
         # the control: poses of the turn rendered statically, each the way the main loop renders
         # (frames in flight, a warm-up frame of the pose first: exact hints) -- moving / control
-        # isolates what one-frame-stale hints cost from what the turned view itself costs (other
+        # isolates what stale hints cost from what the turned view itself costs (other
         # geometry in view)
         ctrl = None
         if args.moving_control > 0:
@@ -668,9 +669,10 @@ def _main():
                     "ms_per_step": round(moving[2][0] / (args.control_steps * moving[2][2]) * 1e3, 4),
                     "note": "poses of the turn, each rendered statically like the main loop (frames in flight, "
                             "after warm-up frames of the pose: exact hints); moving value / this = the price of "
-                            "one-frame-stale hints alone"},
+                            "stale hints alone"},
                 "note": "the camera turns yaw_step_deg per frame (the interactive case): the per-slot walk-cost "
-                        "hints that order work are one frame stale; `value` above is the static camera of the "
+                        "hints that order work are frames_in_flight frames stale (each context renders every "
+                        "frames_in_flight-th frame); `value` above is the static camera of the "
                         "reference's saveStats runs"},
             "trace_kernels_ms_avg": round(float(np.mean(trace_ms)), 4),
             # with frames in flight: trace_kernels_ms_avg and the first-trace figures are taken over
