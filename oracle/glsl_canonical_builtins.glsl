@@ -1,5 +1,6 @@
+//@replace in vec2 FragCoord;	#define FragCoord gl_FragCoord
 
-// ---- analysis prelude: the canonical builtins of include/ort_math.h ----
+// ---- analysis prelude: the canonical builtins of include/ort_math.h (and the exact pixel centre) ----
 const double ORT_LOG2_TAB[32] = double[32](1.3989071038251366LF, -0.4843001617159575LF, 1.3403141361256545LF, -0.4225711719642514LF, 1.2864321608040201LF, -0.3633753794563512LF, 1.2367149758454106LF, -0.3065130425006747LF, 1.1906976744186046LF, -0.2518071504105397LF, 1.147982062780269LF, -0.19910010007969525LF, 1.1082251082251082LF, -0.14825095858394247LF, 1.0711297071129706LF, -0.09913319201925132LF, 1.0364372469635628LF, -0.05163276841532236LF, 1.0LF, 0.0LF, 0.9481481481481482LF, 0.07681559705083084LF, 0.8951048951048951LF, 0.1598713367783894LF, 0.847682119205298LF, 0.2384047393250789LF, 0.8050314465408805LF, 0.3128829552843553LF, 0.7664670658682635LF, 0.38370429247405213LF, 0.7314285714285714LF, 0.4512111118323288LF);
 const double ORT_EXP2_TAB[32] = double[32](1.0LF, 1.0218971486541166LF, 1.0442737824274138LF, 1.0671404006768237LF, 1.0905077326652577LF, 1.1143867425958924LF, 1.1387886347566916LF, 1.1637248587775775LF, 1.189207115002721LF, 1.215247359980469LF, 1.241857812073484LF, 1.2690509571917332LF, 1.2968395546510096LF, 1.3252366431597413LF, 1.3542555469368927LF, 1.383909881963832LF, 1.4142135623730951LF, 1.4451808069770467LF, 1.4768261459394993LF, 1.5091644275934228LF, 1.5422108254079407LF, 1.5759808451078865LF, 1.6104903319492543LF, 1.645755478153965LF, 1.681792830507429LF, 1.718619298122478LF, 1.7562521603732995LF, 1.7947090750031072LF, 1.8340080864093424LF, 1.8741676341103LF, 1.9152065613971474LF, 1.9571441241754002LF);
 const double ORT_RNE = 6755399441055744.0LF;

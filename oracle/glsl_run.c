@@ -24,7 +24,10 @@
  *   PRELUDE (analysis only, tools/glsl_builtins_check.py): GLSL text inserted after the
  *   fragment shader's #version line, in memory (the reference's file is never changed) -- used
  *   to substitute the oracle's canonical builtins for llvmpipe's and so measure how much of
- *   the remaining difference is the builtins'.
+ *   the remaining difference is the builtins'.  Its leading lines of the form
+ *   "//@replace OLD<TAB>NEW" each replace the one occurrence of OLD in the fragment shader (in
+ *   memory, before the insertion; OLD must occur exactly once) -- the canonical prelude uses one
+ *   to read the pixel centre from gl_FragCoord instead of the interpolated FragCoord varying.
  *   INPUT (little endian): int32 W, H, numSamples, maxDepth, useOctree, nSpheres, nNodes,
  *   nIndices; float32 view[16] (column-major, as glUniformMatrix4fv takes glm), cameraPosition[3],
  *   cameraZoom; then float32[nSpheres*4] x3, float32[nNodes*4] x2, int32[nNodes],
@@ -139,6 +142,24 @@ int main(int argc, char **argv) {
     char *fs_src = read_file(path, NULL);
     if (argc == 5 && fs_src) {  /* the prelude goes right after the #version line */
         char *pre = read_file(argv[4], NULL);
+        if (!pre) die("cannot read the prelude");
+        while (strncmp(pre, "//@replace ", 11) == 0) {  /* its replacement lines */
+            char *eol = strchr(pre, '\n'), *tab = strchr(pre + 11, '\t');
+            if (!eol || !tab || tab > eol) die("bad //@replace line");
+            *eol = 0;
+            *tab = 0;
+            const char *old = pre + 11, *rep = tab + 1;
+            char *at = strstr(fs_src, old);
+            if (!at || strstr(at + 1, old)) die("//@replace: OLD must occur exactly once in the fragment shader");
+            const size_t a = (size_t)(at - fs_src), lo = strlen(old), lr = strlen(rep), c = strlen(at + lo);
+            char *m = (char *)malloc(a + lr + c + 1);
+            if (!m) die("out of memory");
+            memcpy(m, fs_src, a);
+            memcpy(m + a, rep, lr);
+            memcpy(m + a + lr, at + lo, c + 1);
+            fs_src = m;
+            pre = eol + 1;
+        }
         char *nl = strchr(fs_src, '\n');
         if (!pre || !nl || strncmp(fs_src, "#version", 8) != 0) die("cannot insert the prelude");
         const size_t a = (size_t)(nl + 1 - fs_src), b = strlen(pre), c = strlen(nl + 1);

@@ -14,7 +14,9 @@
  * (oracle/glsl_run.c, tests/golden/glsl, tests/test_glsl_parity.py): with GLSL's
  * implementation-defined builtins set to the canonical ones of include/ort_math.h
  * (oracle/glsl_canonical_builtins.glsl), this file's frames are BIT-IDENTICAL to the shader's
- * (15 frames, multi-bounce, depth-10 trees and the full C2 and C3 bench frames included); with llvmpipe's own builtins
+ * (18 frames, multi-bounce, depth-9/10 trees and the full C2 and C3 bench frames included; the
+ * canonical prelude also reads the pixel centre from gl_FragCoord, exact, where llvmpipe's
+ * interpolated FragCoord varying misses it by an ulp at some frame sizes); with llvmpipe's own builtins
  * within 1e-6 on >= 99.99 % of a primary-ray frame's pixels.
 
  * Differences from the GLSL, all forced: node offsets are int32 instead of float-in-

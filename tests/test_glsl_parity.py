@@ -126,7 +126,7 @@ def test_canonical_prelude_is_ort_math():
     import glsl_builtins_check as B
     assert B.prelude() == PRELUDE.read_text()
     assert hashlib.sha256(PRELUDE.read_bytes()).hexdigest() == CANON["prelude_sha256"]
-    assert "llvmpipe" in CANON["renderer"] and len(CANON["cases"]) >= 12
+    assert "llvmpipe" in CANON["renderer"] and len(CANON["cases"]) >= 18
 
 
 @pytest.mark.parametrize("name", sorted(CANON["cases"]))
@@ -156,7 +156,7 @@ def test_fixtures_regenerate_bit_for_bit(name):
 
 
 @pytest.mark.skipif(not (RUNNER.exists() and SHADERS.exists()), reason="needs oracle/_ref/glsl_run and /root/reference")
-@pytest.mark.parametrize("name", ["c1", "prebuilt_spp4_d8", "c2_spp2_d4"])
+@pytest.mark.parametrize("name", ["c1", "prebuilt_spp4_d8", "c2_spp2_d4", "m8_d7_odd_b2"])
 def test_canonical_hashes_regenerate(name):
     """The canonical-builtin hashes are what the reference's shaders give now."""
     import sys
@@ -164,3 +164,22 @@ def test_canonical_hashes_regenerate(name):
     import make_glsl_golden as M
     img, _ = M.run_glsl(*M.case_inputs(CANON["cases"][name]), prelude=PRELUDE)
     assert frame_sha(img) == CANON["cases"][name]["sha256"]
+
+
+@pytest.mark.skipif(not (RUNNER.exists() and SHADERS.exists()), reason="needs oracle/_ref/glsl_run and /root/reference")
+def test_interpolated_pixel_centre_is_implementation_defined():
+    """Why the canonical prelude reads gl_FragCoord: at 333x177 llvmpipe's interpolated FragCoord
+    varying misses the exact pixel centre by an ulp on part of the frame, which reseeds those
+    pixels' RNG; with the builtins alone canonical (no //@replace line) the frame is not the
+    oracle's, with the exact centre it is (canonical.json)."""
+    import sys
+    import tempfile
+    sys.path.insert(0, str(RUNNER.parents[2] / "tools"))
+    import make_glsl_golden as M
+    c = CANON["cases"]["m8_d7_odd_b2"]
+    text = PRELUDE.read_text()
+    assert text.startswith("//@replace in vec2 FragCoord;\t#define FragCoord gl_FragCoord\n")
+    with tempfile.TemporaryDirectory() as d:
+        Path(f"{d}/pre.glsl").write_text(text.split("\n", 1)[1])  # the builtins without the replacement
+        img, _ = M.run_glsl(*M.case_inputs(c), prelude=f"{d}/pre.glsl")
+    assert frame_sha(img) != c["sha256"]

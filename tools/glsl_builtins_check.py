@@ -8,6 +8,8 @@ normalize/dot/length/cross/reflect, min/max in the GLSL spec's (y < x) ? y : x f
 frames with the CPU oracle.  (What a prelude cannot reach is llvmpipe's own arithmetic in the
 shader's expressions; measured, it changes nothing there: with the prelude every frame of
 tests/golden/glsl/canonical.json is bit-identical to the oracle's.)
+The prelude also reads the pixel centre from gl_FragCoord instead of the interpolated FragCoord
+varying (FRAGCOORD_REPLACE below).
 usage: LP_NUM_THREADS=8 python tools/glsl_builtins_check.py [case ...]"""
 import re
 import sys
@@ -40,11 +42,21 @@ def lit(x):
     return repr(float(x)) + "LF"
 
 
+# The pixel centre: the reference's fragment shader reads the FragCoord varying its vertex shader
+# sets to (clip xy + 1) / 2 * iResolution at the quad's corners (vertex_shader.glsl:15), i.e. the
+# exact pixel centre (x + 0.5, y + 0.5) wherever interpolation is exact -- but the precision of
+# varying interpolation is implementation-defined, and llvmpipe's plane equations miss it by an ulp
+# at some frame sizes (e.g. 344x180 or 333x177: 39-44 % of the pixels then differ, since the pixel's
+# RNG is seeded from FragCoord, octree_fragment_shader.glsl:640).  The canonical frame reads the
+# centre from gl_FragCoord, which the rasterizer gives exactly (glsl_run's //@replace line).
+FRAGCOORD_REPLACE = "//@replace in vec2 FragCoord;\t#define FragCoord gl_FragCoord\n"
+
+
 def prelude():
     c = consts()
     tab = lambda k: "double[{}]({})".format(len(c[k]), ", ".join(lit(v) for v in c[k]))  # noqa: E731
-    return f"""
-// ---- analysis prelude: the canonical builtins of include/ort_math.h ----
+    return FRAGCOORD_REPLACE + f"""
+// ---- analysis prelude: the canonical builtins of include/ort_math.h (and the exact pixel centre) ----
 const double ORT_LOG2_TAB[32] = {tab("ORT_LOG2_TAB_VALUES")};
 const double ORT_EXP2_TAB[32] = {tab("ORT_EXP2_TAB_VALUES")};
 const double ORT_RNE = 6755399441055744.0LF;

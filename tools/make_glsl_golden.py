@@ -83,6 +83,17 @@ CANON_EXTRA = {
                            dpitch=0.0),
     "deep_d9_m1_spp2_b3": dict(scene="random", n=20000, depth=9, m=1, W=320, H=180, spp=2, md=3, oct=1, dyaw=15.0,
                                dpitch=-6.0),
+    # leaves of up to 8 spheres, an odd frame size (partial tiles on both axes), 2 bounces
+    "m8_d7_odd_b2": dict(scene="random", n=30000, depth=7, m=8, W=333, H=177, spp=1, md=2, oct=1, dyaw=-25.0,
+                         dpitch=8.0),
+    # the C3 tree (depth 8) with bounces and samples: the depth <= 8 persistent bounce walk
+    "c3tree_spp3_b5": dict(scene="random", n=100000, depth=8, m=0, W=200, H=120, spp=3, md=5, oct=1, dyaw=10.0,
+                           dpitch=-20.0),
+    # a depth-9 tree subdivided to the bottom (maxSpheresPerNode 0): the deep kernels without C5's
+    # one-sphere leaves (at depth 10 such trees pass 2^24 nodes even at 2000 spheres: SURVEY F7,
+    # the reference's float offsets then name wrong children)
+    "deep_d9_m0_b2": dict(scene="random", n=10000, depth=9, m=0, W=320, H=180, spp=1, md=2, oct=1, dyaw=-8.0,
+                          dpitch=3.0),
 }
 PRELUDE = ROOT / "oracle" / "glsl_canonical_builtins.glsl"
 
