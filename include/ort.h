@@ -97,10 +97,12 @@ typedef struct ort_scene_info {
                                       frame of the same shape + 1/64 + 1024, read back asynchronously;
                                       a longer list goes on unsorted): no host wait; 1 sort every
                                       slot's key; 0 slot order */
-#define ORT_OPT_XCD_SWIZZLE 8      /* workgroup -> tile order (same pixels): 2 (default) each XCD renders
-                                      runs of consecutive raster tiles (about 1/15 of a tile row, a power
-                                      of two: 16 at 3840 px); 1: each XCD renders 128x128-pixel
-                                      super-tiles; 0: raster order (tile b on XCD b % 8) */
+#define ORT_OPT_XCD_SWIZZLE 8      /* workgroup -> tile order (same pixels): 2 each XCD renders runs of
+                                      consecutive raster tiles (about 1/15 of a tile row, a power of
+                                      two: 16 at 3840 px); 1: each XCD renders 128x128-pixel
+                                      super-tiles; 0: raster order (tile b on XCD b % 8); -1 (default):
+                                      0 for one-tile workgroups on tiles of at most 1.5 M pixels (a
+                                      C3 1/8 band at one frame in flight -3 %), 2 otherwise */
 #define ORT_OPT_KID_SKIP 9         /* 1 (default): a lane skips one-sphere leaf children holding the sphere it
                                       last rejected at a tmin <= theirs (they cannot end the walk; same
                                       pixels, kid_table.h), a node's record and kid entry loaded together

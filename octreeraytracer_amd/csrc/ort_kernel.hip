@@ -198,7 +198,7 @@ __device__ inline LdsView setup_lds(unsigned char* smem, const ort::KScene& S) {
 // to XCD b % 8, each XCD with its own L2.  ORT_OPT_XCD_SWIZZLE picks the order:
 //   0  raster: XCD x renders every 8th tile of a tile row -- neighbouring tiles, whose rays
 //      walk the same octree nodes, are spread over all 8 L2s;
-//   2  (default) within every 8*run consecutive workgroups the `run` that land on one XCD
+//   2  (default above kRasterAutoPixels) within every 8*run consecutive workgroups the `run` that land on one XCD
 //      get `run` consecutive raster tiles (run = xcd_run_log2: 16 tiles, a 256x16-pixel run,
 //      at 3840 px): c3 +2% (8-tile runs) and another +1.7% (16), c5 +2% in interleaved A/B
 //      (tools/ab_stream.py);
@@ -1357,6 +1357,12 @@ constexpr int kHeavyPrioSteps = 150;
 constexpr int kSplitAutoSteps = 200;
 constexpr long long kSplitAutoPixels = 1ll << 21;
 constexpr long long kPairsAutoPixels = kSplitAutoPixels + 1;
+// ORT_OPT_XCD_SWIZZLE -1 (auto): raster order (0) for the per-tile kernel on tiles of at most
+// this many pixels, runs (2) otherwise.  A C3 1/8 band (1 M pixels, ~2 generations of
+// workgroups) at one frame in flight: 0.307 -> 0.298 ms with raster order (its heavy region
+// spread over all 8 XCDs instead of runs of 16 tiles on one); a 1/4 band 0.492 vs 0.505 and
+// tile pairs (frames in flight) 0.224 vs 0.242 ms the other way (profiles/r05_band_swizzle.log)
+constexpr long long kRasterAutoPixels = 3ll << 19;
 struct ort_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -1377,7 +1383,7 @@ struct ort_ctx {
     void* wclock = nullptr;  // ort_debug_wave_clock (ORT_PERSIST_CLOCK analysis builds)
     long long wclock_n = 0;
 #endif
-    int xcd_swizzle = 2;  // ORT_OPT_XCD_SWIZZLE: workgroup -> tile order (block_tile)
+    int xcd_swizzle = -1;  // ORT_OPT_XCD_SWIZZLE: workgroup -> tile order (block_tile); -1 auto
     int kid_skip = 1;     // ORT_OPT_KID_SKIP: rejected-sphere skip of one-sphere leaf children (2: without nk)
     // ORT_OPT_SORT_PATHS: order of the alive paths between bounces.  2 (default): the list the
     // shade kernel appended, radix-sorted by the coherence key after reading its length back --
@@ -1959,7 +1965,7 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     a.tilesX = gridX;
     a.pair = pairs ? 1 : 0;
     a.tilesY = tilesY;
-    a.swizzle = ctx->xcd_swizzle;
+    a.swizzle = ctx->xcd_swizzle >= 0 ? ctx->xcd_swizzle : ((!pairs && (long long)pix <= kRasterAutoPixels) ? 0 : 2);
     a.xrun_log2 = xcd_run_log2(gridX);
     a.total = (int)slots;
     a.exact_only = ctx->exact_only || !ctx->ordered;
@@ -2417,7 +2423,7 @@ int ort_set_option(ort_ctx* ctx, int option, int value) {
         return ORT_OK;
     }
     if (option == ORT_OPT_XCD_SWIZZLE) {
-        if (value < 0 || value > 2) return fail(ctx, ORT_ERR_INVALID_ARG, "xcd swizzle must be 0, 1 or 2");
+        if (value < -1 || value > 2) return fail(ctx, ORT_ERR_INVALID_ARG, "xcd swizzle must be -1 (auto), 0, 1 or 2");
         ctx->xcd_swizzle = value;
         return ORT_OK;
     }

@@ -115,8 +115,9 @@ class Renderer:
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_EXACT_TRAVERSAL, int(bool(on))))
 
     def set_xcd_swizzle(self, mode: int):
-        """Workgroup -> tile order (ORT_OPT_XCD_SWIZZLE): 2 (default) runs of 8 raster tiles per
-        XCD, 1 128x128-pixel super-tiles per XCD, 0 raster; same pixels."""
+        """Workgroup -> tile order (ORT_OPT_XCD_SWIZZLE): 2 runs of raster tiles per XCD, 1
+        128x128-pixel super-tiles per XCD, 0 raster, -1 (default) raster on small one-tile-workgroup
+        tiles and runs otherwise; same pixels."""
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_XCD_SWIZZLE, int(mode)))
 
     def set_sort_paths(self, mode: int):

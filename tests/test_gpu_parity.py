@@ -303,7 +303,7 @@ def test_deep_tree_kernel_bit_exact(ort, oracle, renderer, depth, mspn):
         renderer.set_sort_paths(2)  # the default
 
 
-@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("mode", [0, 1, 2, -1])
 def test_xcd_swizzle_orders_identical(ort, oracle, renderer, scene_c2, mode):
     """Every workgroup -> tile order (ORT_OPT_XCD_SWIZZLE) renders the oracle's pixels: a
     ragged tile (partial 512/64-workgroup groups, edge super-tiles), bounces included."""
@@ -314,10 +314,13 @@ def test_xcd_swizzle_orders_identical(ort, oracle, renderer, scene_c2, mode):
         p = ort.FrameParams.default_camera(1920, 1080, num_samples=1, max_depth=3)
         tile = ort.Tile(13, 1900, 7, 1010)  # 119 x 64 tiles: ragged in both directions
         assert_same(renderer.render(p, tile), oracle.render(s, t, p, 13, 7, 1900, 1010), f"swizzle {mode}")
-        with pytest.raises(ort.OrtError):
-            renderer.set_xcd_swizzle(3)
+        small = ort.Tile(5, 1000, 3, 900)  # <= 1.5 M pixels: raster order under the auto mode
+        assert_same(renderer.render(p, small), oracle.render(s, t, p, 5, 3, 1000, 900), f"swizzle {mode}, small")
+        for bad in (3, -2):
+            with pytest.raises(ort.OrtError):
+                renderer.set_xcd_swizzle(bad)
     finally:
-        renderer.set_xcd_swizzle(2)
+        renderer.set_xcd_swizzle(-1)
 
 
 @pytest.mark.parametrize("use_octree", [1, 0])
