@@ -55,7 +55,7 @@ CONFIGS = {
 def reference_frame_check(config: str, frame, host=None):
     """SHA-256 of the bench's assembled static frame (float32 RGB, GL rows) against the frame the
     reference's own shaders give for the same scene and camera -- run on Mesa llvmpipe with the
-    canonical builtins, tests/golden/glsl/canonical.json (tests/test_glsl_parity.py).  None when
+    canonical builtins and pixel centre, tests/golden/glsl/canonical.json (tests/test_glsl_parity.py).  None when
     no such hash exists for the config (C5: its tree is too large for llvmpipe) or no frame."""
     cases = {"c1": "c1", "c2": "c2_full", "c3": "c3_full"}
     path = Path(__file__).resolve().parent / "tests" / "golden" / "glsl" / "canonical.json"
@@ -68,7 +68,8 @@ def reference_frame_check(config: str, frame, host=None):
     got = hashlib.sha256(np.ascontiguousarray(img, np.float32).tobytes()).hexdigest()
     return {"frame_sha256": got, "reference_shader_frame_sha256": ref["sha256"], "bit_identical": got == ref["sha256"],
             "reference": "the reference's shaders/octree_fragment_shader.glsl on Mesa llvmpipe with canonical "
-                         "builtins, same scene and camera (tests/golden/glsl/canonical.json, case %s)" % cases[config]}
+                         "builtins and pixel centre, same scene and camera (tests/golden/glsl/canonical.json, "
+                         "case %s)" % cases[config]}
 
 
 def default_inflight(config: str, world: int) -> int:
