@@ -2172,7 +2172,10 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                     }
                     at.hsync = hc + 8 * ctx->hpar;
                     at.hsync_next = hc + 8 * (ctx->hpar ^ 1);
-                    const int hblocks = 32;  // 1024 heavy rays in flight; more loop
+#ifndef ORT_SPLIT_BLOCKS
+#define ORT_SPLIT_BLOCKS 32
+#endif
+                    const int hblocks = ORT_SPLIT_BLOCKS;  // 1024 heavy rays in flight; more loop
                     const dim3 hg(hblocks), ht(kBlock);
                     if (ctx->depth > 8 && fmode == 1) hipLaunchKernelGGL((ort_trace_split<true, 1>), hg, ht, lds, ctx->aux_stream, at);
                     else if (ctx->depth > 8) hipLaunchKernelGGL((ort_trace_split<true, 2>), hg, ht, lds, ctx->aux_stream, at);
