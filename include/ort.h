@@ -153,6 +153,13 @@ typedef struct ort_scene_info {
 #define ORT_OPT_DEBUG_FLAGS 18     /* analysis library only (libort_analysis.so, tools/ab_stream.py): 1 records
                                       no per-launch trace-timing events, 2 scans the heavy list at the start
                                       of each split frame; libort.so: ORT_ERR_UNSUPPORTED */
+#define ORT_OPT_LAUNCH_TIMES 19    /* 1 (default): HIP events time every trace launch of a frame
+                                      (ort_last_trace_ms, ort_trace_times_ms, ort_frame_trace_times_ms);
+                                      0: only the frame's start and end are timed (ort_last_kernel_ms) --
+                                      fewer event packets on the stream: a C3 1/8 band at one frame in
+                                      flight 0.297 -> 0.291 ms; the per-launch queries then report
+                                      no newer launch (ort_last_trace_ms: an error while none was ever
+                                      timed).  Same pixels */
 /* Retired option codes, reserved (ORT_ERR_UNSUPPORTED): options that lost to the defaults in
  * A/B and were removed -- 5 the wave-level packet walk (1.2-1.35x slower),
  * 7 the wave-level block queue (1/8 band 0.83 vs 0.61 ms), 17 longest-first workgroups

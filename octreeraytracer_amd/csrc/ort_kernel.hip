@@ -1459,6 +1459,7 @@ struct ort_ctx {
     DevBuf hit, defer_list, defer_count, po, pd, pc, prng, pcol;
     int sync_set = 0;      // defer_count's counter set of the next trace launch (render_impl)
     int debug_flags = 0;   // ORT_OPT_DEBUG_FLAGS (A/B of the per-frame stream structure only)
+    int launch_times = 1;  // ORT_OPT_LAUNCH_TIMES: per-launch trace-timing events
     bool sync_ok = false;  // both sets zero except the one the last exact kernel left to zero
     DevBuf qlist, qlist2, qcount, qtemp;  // bounce >= 1 path compaction (two lists: read one, append the other)
     DevBuf skeys, skeys2, svals;  // coherence sort
@@ -2085,7 +2086,8 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     ctx->tseg[fslot] = 0;
     // the frame's start: also the start of its first trace launch when that is timed (nothing is
     // enqueued between them), which saves an event packet per frame (~1 % of a 1/8 band frame)
-    const bool start_is_tr0 = maxd > 0 && !(ctx->debug_flags & 1);
+    const bool no_times = (ctx->debug_flags & 1) || !ctx->launch_times;  // no per-launch events
+    const bool start_is_tr0 = maxd > 0 && !no_times;
     ctx->ev0_last = start_is_tr0 ? ctx->tr0[fslot][0] : ctx->ev0;
     HIPCHK(ctx, hipEventRecord(ctx->ev0_last, s));
     for (int smp = 0; smp < ns; ++smp) {
@@ -2112,7 +2114,7 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
                 const int slot = fslot;
                 const int seg = ctx->tseg[slot];
                 // every trace launch of the frame, up to kSeg (analysis flag 1: none)
-                const bool timed = seg < ort_ctx::kSeg && !(ctx->debug_flags & 1);
+                const bool timed = seg < ort_ctx::kSeg && !no_times;
                 if (timed && !ctx->tr0[slot][seg]) {
                     HIPCHK(ctx, hipEventCreate(&ctx->tr0[slot][seg]));
                     HIPCHK(ctx, hipEventCreate(&ctx->tr1[slot][seg]));
@@ -2453,6 +2455,11 @@ int ort_set_option(ort_ctx* ctx, int option, int value) {
     if (option == ORT_OPT_SPLIT_LEVEL) {
         if (value < 0 || value > ORT_COMPACT_MAX_DEPTH) return fail(ctx, ORT_ERR_INVALID_ARG, "ORT_OPT_SPLIT_LEVEL: 0 (auto) .. 10");
         ctx->split_level = value;
+        return ORT_OK;
+    }
+    if (option == ORT_OPT_LAUNCH_TIMES) {
+        if (value < 0 || value > 1) return fail(ctx, ORT_ERR_INVALID_ARG, "ORT_OPT_LAUNCH_TIMES: 0 or 1");
+        ctx->launch_times = value;
         return ORT_OK;
     }
 #if ORT_ANALYSIS

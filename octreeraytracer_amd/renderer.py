@@ -114,6 +114,11 @@ class Renderer:
         """Disable (True) / enable the sign-specialised fast walk; pixels are identical either way."""
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_EXACT_TRAVERSAL, int(bool(on))))
 
+    def set_launch_times(self, on: int):
+        """ORT_OPT_LAUNCH_TIMES: 1 (default) times every trace launch (last_trace_ms, trace_times_ms);
+        0 times only the frame (last_kernel_ms) -- fewer event packets per frame; same pixels."""
+        self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_LAUNCH_TIMES, int(on)))
+
     def set_xcd_swizzle(self, mode: int):
         """Workgroup -> tile order (ORT_OPT_XCD_SWIZZLE): 2 runs of raster tiles per XCD, 1
         128x128-pixel super-tiles per XCD, 0 raster, -1 (default) raster on small one-tile-workgroup

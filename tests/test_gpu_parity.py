@@ -367,3 +367,21 @@ def test_kernel_bit_exact_to_reference_shader(ort, renderer, name):
     s, t, p = inputs(ort, c)
     renderer.upload(s, t)
     assert frame_sha(renderer.render(p)) == c["sha256"], f"{name}: HIP frame differs from the reference shader's"
+
+
+def test_launch_times_option(ort, oracle, renderer, scene_c1):
+    """ORT_OPT_LAUNCH_TIMES 0: no per-launch events, same pixels, the frame still timed."""
+    s, t = scene_c1
+    renderer.upload(s, t)
+    p = ort.FrameParams.default_camera(96, 64, num_samples=2, max_depth=3)
+    try:
+        renderer.set_launch_times(0)
+        got = renderer.render(p)
+        assert_same(got, oracle.render(s, t, p), "launch times off")
+        assert renderer.last_kernel_ms() > 0.0
+        with pytest.raises(ort.OrtError):
+            renderer.set_launch_times(2)
+    finally:
+        renderer.set_launch_times(1)
+    renderer.render(p)
+    assert renderer.last_trace_ms() > 0.0

@@ -71,6 +71,9 @@ t1 = time.perf_counter()
 torch.cuda.synchronize()
 t2 = time.perf_counter()
 r = rs[0]
+try:  # (analysis flag 1 records no per-launch times)
+    timed = f"last frame pipeline {r.last_kernel_ms():.3f} ms, trace {r.last_trace_ms():.3f} ms"
+except ort.OrtError:
+    timed = "no per-launch times (launch times off)"
 print(f"{cfg} world={world} inflight={inflight}{' ' + ' '.join(sys.argv[6:]) if opts else ''}: enqueue {1e3 * (t1 - t0) / n:.3f} ms/frame, wall {1e3 * (t2 - t0) / n:.3f} ms/frame, "
-      f"gpu span {e0.elapsed_time(e1) / n:.3f} ms/frame, last frame pipeline {r.last_kernel_ms():.3f} ms, "
-      f"trace {r.last_trace_ms():.3f} ms")
+      f"gpu span {e0.elapsed_time(e1) / n:.3f} ms/frame, {timed}")
