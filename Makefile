@@ -33,7 +33,7 @@ $(AOBJ)/%.o: $(SRC)/%.hip $(HDRS)
 
 $(ALIB): $(HOST_OBJS) $(AOBJ)/ort_kernel.o $(OBJ)/gpu_build.o $(AOBJ)/group.o
 	@mkdir -p $(dir $(ALIB))
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -ldl -Wl,-soname,libort_analysis.so
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -ldl -Wl,-soname,libort_analysis.so -Wl,-Bsymbolic
 
 $(OBJ)/%.o: $(SRC)/%.cpp $(HDRS)
 	@mkdir -p $(OBJ)

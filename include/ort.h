@@ -160,6 +160,15 @@ typedef struct ort_scene_info {
                                       flight 0.297 -> 0.291 ms; the per-launch queries then report
                                       no newer launch (ort_last_trace_ms: an error while none was ever
                                       timed).  Same pixels */
+#define ORT_OPT_PIXEL_PATHS 20    /* whole-pixel paths: the frame in ONE launch, each lane stepping a pixel's
+                                      samples and bounces in turn (the RNG state runs on from one sample to the
+                                      next, glsl:640, so a pixel is a sequential chain) and taking the next
+                                      pixel when done -- instead of the per-sample, per-bounce pipeline (trace,
+                                      shade, list sort launches).  -1 (default): on for frames of more than one
+                                      traversal per pixel on brute force and on trees of at most 2^21 nodes
+                                      (the small scenes of the reference's sweeps, where launches and sorts
+                                      dominate); 0 off; 1 on wherever it applies (compact layout or brute
+                                      force, maxDepth >= 1, not 1 sample x 1 bounce).  Same pixels */
 /* Retired option codes, reserved (ORT_ERR_UNSUPPORTED): options that lost to the defaults in
  * A/B and were removed -- 5 the wave-level packet walk (1.2-1.35x slower),
  * 7 the wave-level block queue (1/8 band 0.83 vs 0.61 ms), 17 longest-first workgroups

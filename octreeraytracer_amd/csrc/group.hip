@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstring>
 #include <chrono>
 #include <mutex>
@@ -229,7 +230,7 @@ hipError_t query(int device, hipEvent_t e) {
 int wait_slot(ort_group* g, GroupSlot& S) {
     if (S.ticket < 0) return ORT_OK;
     const auto t0 = std::chrono::steady_clock::now();
-    for (long long spin = 0;; ++spin) {
+    for (;;) {
         const hipError_t e = query(g->dev[0], S.finished);
         if (e == hipSuccess) break;
         if (e != hipErrorNotReady) GCHK(g, e);
@@ -249,9 +250,15 @@ int wait_slot(ort_group* g, GroupSlot& S) {
                                                  std::to_string((long long)(S.ticket % (long long)g->slot.size())) +
                                                  ") not complete after " + std::to_string(ms) + " ms; pending: " + pend);
         }
-        // poll: yield first, then sleep in growing steps up to 1 ms (a frame takes 0.2-50 ms)
-        if (spin < 64) std::this_thread::yield();
-        else std::this_thread::sleep_for(std::chrono::microseconds(spin < 1024 ? 50 : 1000));
+        // poll: yield (no sleep) for twice the last frame's device time, at least 5 ms and at most
+        // 250 ms -- a synchronous render is then seen complete within a yield of its end -- and
+        // only past that window sleep, 50 us steps then 1 ms steps (a frame takes 0.2-50 ms)
+        const float lf = g->last_ms > 0.0f ? g->last_ms : 0.0f;
+        const long long busy_us = std::min(250000LL, std::max(5000LL, (long long)(2000.0f * lf)));
+        const long long us =
+            std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
+        if (us < busy_us) std::this_thread::yield();
+        else std::this_thread::sleep_for(std::chrono::microseconds(us < busy_us + 50000 ? 50 : 1000));
     }
     GCHK(g, hipSetDevice(g->dev[0]));
     const int i = (int)(S.ticket % ort_group::kMsRing);

@@ -1338,6 +1338,146 @@ __global__ void __launch_bounds__(kBlock) ort_finalize_kernel(PipeArgs A) {
     o[0] = v.x; o[1] = v.y; o[2] = v.z;
 }
 
+// ---------------------------------------------------------------------------------------
+// Whole-pixel paths (ORT_OPT_PIXEL_PATHS): main() of the fragment shader (glsl:636-664) for
+// every pixel in ONE launch -- all samples, all bounces -- instead of the wavefront pipeline's
+// per-sample, per-bounce launches (trace, exact walk, shade, list sort: ~10 launches per bounce).
+// Samples cannot be batched across launches: the RNG state runs on from one sample to the next
+// (randState, glsl:640), so a pixel's samples are a sequential chain.  Each lane therefore owns
+// a pixel and steps it one bounce at a time, regenerating the path when it ends (the pixel's
+// next sample starts in the same iteration: lanes stay on the walk code whatever sample or
+// bounce they are at), and a lane whose pixel is done takes the next pixel of its wave's chunk
+// (persistent grid, one atomic per 64-pixel chunk, pixels in the tile-block order of the path
+// slots: a chunk is an 8x8 block).  Every pixel runs exactly shade_pixel's chain (render_core.h),
+// so the frames are the pipeline's bit for bit.  MODE 0: compact octree (DEEP: depth 9-10, the
+// camera walk's 96-bit masks over the forward tables; else the bounce walk's Masks64Plain), the
+// exact walk inline for the rays the fast walk cannot take; MODE 2: brute force.
+// The grid's work cursor and done count (A.sync[1], [2]) start at zero (the counter set of the
+// launch) and the last workgroup to finish resets them.
+template <int MODE, bool DEEP>
+__device__ __forceinline__ bool pixel_trace(const PipeArgs& A, LdsView& L, const ort::Ray& r, float& t, int& entry) {
+    ort::Counters cnt;  // (not counted: counting renders take the pipeline)
+    entry = -1;
+    t = 0.0f;
+    if (MODE == 2) return ort::traverse_brute<false>(A.S, r, 0.001f, ORT_MAXFLOAT, entry, t, cnt);
+    ort::V3 inv = ort::mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+    if (!A.exact_only && ort::fast_prepare(A.S, r, inv)) {
+        using Masks = typename std::conditional<DEEP, ort::Masks96, ort::Masks64Plain>::type;
+        return ort::traverse_fast_t<false, Masks>(A.S, L.planes, L.lut, r, inv, 0.001f, ORT_MAXFLOAT, entry, t, L.fr, cnt);
+    }
+    return ort::traverse_compact<false>(A.S, L.planes, r, 0.001f, ORT_MAXFLOAT, entry, t, L.fr, cnt);
+}
+
+#ifndef ORT_PIXEL_CHUNK
+#define ORT_PIXEL_CHUNK 64  // pixels a wave takes from the cursor at a time (one 8x8 block)
+#endif
+#ifndef ORT_PIXEL_WAVES
+#define ORT_PIXEL_WAVES 4
+#endif
+
+template <int MODE, bool DEEP>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ORT_PIXEL_WAVES)))
+ort_pixel_paths(PipeArgs A) {
+    extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];  // plane tables: 1 KiB-aligned
+    LdsView L{};
+    if (MODE == 0) L = setup_lds<true>(smem, A.S);
+    const int lane = threadIdx.x & 63;
+    const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const int maxd = A.pp.maxDepth, ns = A.pp.ns;
+    int k = -1;              // the lane's path slot (pixel), -1 idle
+    int px = 0, py = 0, s = 0, b = 0;
+    ort::Ray ray;
+    ray.o = ray.d = ort::mk(0.0f, 0.0f, 0.0f);
+    ort::V3 c = ort::mk(1.0f, 1.0f, 1.0f), col = ort::mk(0.0f, 0.0f, 0.0f);
+    float importance = 1.0f;
+    ort_rng st;
+    st.x = st.y = 0.0f;
+    int next = 0, end = 0;   // wave-uniform: the rest of the wave's chunk
+    bool drained = false;    // wave-uniform: the cursor passed the last slot
+    for (;;) {
+        const unsigned long long idle = __ballot(k < 0);
+        if (idle && !drained) {  // refill: idle lanes take the chunk's next pixels
+            if (next == end) {
+                int base = 0;
+                if (lane == 0) base = atomicAdd(A.sync + 1, ORT_PIXEL_CHUNK);
+                base = __shfl(base, 0);
+                if (base >= A.total) drained = true;
+                next = base;
+                end = min(base + ORT_PIXEL_CHUNK, A.total);
+            }
+            if (!drained) {
+                const int n_idle = __popcll(idle);
+                const int take = min(n_idle, end - next);
+                if (k < 0) {
+                    const int rank = __popcll(idle & below);
+                    if (rank < take) {
+                        const int cand = next + rank;
+                        int cx, cy;
+                        if (slot_coords(A, cand, cx, cy)) {
+                            const int y = tile_row_to_y(A.tm, cy);
+                            if (y < A.pp.H) {  // a pixel: sample 0's camera ray
+                                k = cand;
+                                px = A.tm.x0 + cx;
+                                py = y;
+                                ort::pixel_rng_init(A.pp, px, py, st);
+                                s = 0;
+                                b = 0;
+                                col = ort::mk(0.0f, 0.0f, 0.0f);
+                                c = ort::mk(1.0f, 1.0f, 1.0f);
+                                importance = 1.0f;
+                                ray = ort::primary_ray(A.pp, px, py, 0, st);
+                            } else {  // a band's padding row (past the frame): zeros, as the pipeline writes
+                                float* o = A.out + 3 * ((size_t)cy * A.tm.tw + cx);
+                                o[0] = 0.0f; o[1] = 0.0f; o[2] = 0.0f;
+                            }
+                        }
+                    }
+                }
+                next += take;
+            }
+        }
+        if (!__ballot(k >= 0)) {
+            if (drained) break;
+            continue;
+        }
+        if (k >= 0) {  // one bounce of the lane's current path (radiance(), glsl:604-627)
+            float t;
+            int entry;
+            const bool hit = pixel_trace<MODE, DEEP>(A, L, ray, t, entry);
+            ort::HitRec h;
+            if (hit) h = ort::hit_record<MODE>(A.S, ray, t, entry);
+            bool ended = ort::shade_bounce(hit, h, ray, c, importance, st);
+            ++b;
+            ended = ended || b >= maxd || importance < 0.01f;
+            if (ended) {  // col += radiance(r) (glsl:655); the pixel's next sample, or its final colour
+                col = ort::add(col, c);
+                if (++s < ns) {
+                    b = 0;
+                    c = ort::mk(1.0f, 1.0f, 1.0f);
+                    importance = 1.0f;
+                    ray = ort::primary_ray(A.pp, px, py, s, st);
+                } else {
+                    int cx, cy;
+                    (void)slot_coords(A, k, cx, cy);
+                    const ort::V3 v = ort::finish_pixel(col, ns);
+                    float* o = A.out + 3 * ((size_t)cy * A.tm.tw + cx);
+                    o[0] = v.x; o[1] = v.y; o[2] = v.z;
+                    k = -1;
+                }
+            }
+        }
+    }
+    // the last workgroup out resets the cursor and the done count for the next launch
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        if (atomicAdd(A.sync + 2, 1) == (int)gridDim.x - 1) {
+            atomicExch(A.sync + 1, 0);
+            atomicExch(A.sync + 2, 0);
+        }
+    }
+}
+
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
@@ -1377,6 +1517,7 @@ struct ort_ctx {
     std::string err;
     int force_layout = -1;
     int exact_only = 0;
+    int pixel_paths = -1;  // ORT_OPT_PIXEL_PATHS: -1 auto (use_pixel_paths), 0 off, 1 on where it applies
     int refill = 16;  // ORT_OPT_REFILL: C5 (64-item chunks) 16 > 12 (-0.6 %) > 8 (-1.2 %); tools/ab_stream.py
     int persistent = 2;  // ORT_OPT_PERSISTENT: 0 off, 2 bounce >= 1 traces (default)
 #if ORT_ANALYSIS
@@ -1855,6 +1996,22 @@ int persistent_blocks(int device, bool count, bool deep, int depth, size_t lds, 
     return (int)std::max(1LL, std::min(b, needed));
 }
 
+// Whole-pixel paths (ort_pixel_paths): the frame in one launch.  Auto (ORT_OPT_PIXEL_PATHS -1):
+// frames of more than one traversal per pixel on brute force and on trees of at most
+// kPixelPathsAutoNodes nodes -- small scenes, where the pipeline's per-bounce launches and
+// sorts cost more than its coherence gains (the reference's own sweeps).
+constexpr long long kPixelPathsAutoNodes = 1ll << 21;
+bool use_pixel_paths(const ort_ctx* ctx, int mode, int ns, int maxd);
+
+template <int MODE, bool DEEP>
+int pixel_paths_blocks(int device, size_t lds, long long needed) {
+    int per_cu = 0, cus = 0;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ort_pixel_paths<MODE, DEEP>, kBlock, lds);
+    const long long b = (long long)std::max(per_cu, 1) * std::max(cus, 1);
+    return (int)std::max(1LL, std::min(b, needed));
+}
+
 // FNV-1a of the frame shape and scene: the previous-frame hints (list lengths, walk costs)
 // belong to one of these
 unsigned long long frame_sig(const ort_ctx* ctx, const ort_params* p, const ort_tile* t) {
@@ -1864,6 +2021,65 @@ unsigned long long frame_sig(const ort_ctx* ctx, const ort_params* p, const ort_
     unsigned long long sig = 1469598103934665603ull;
     for (long long x : v) sig = (sig ^ (unsigned long long)x) * 1099511628211ull;
     return sig;
+}
+
+bool use_pixel_paths(const ort_ctx* ctx, int mode, int ns, int maxd) {
+    if (mode == 1 || maxd < 1 || (ns == 1 && maxd == 1) || ctx->pixel_paths == 0) return false;
+    if (ctx->pixel_paths > 0) return true;
+    return mode == 2 || ctx->n_nodes <= kPixelPathsAutoNodes;
+}
+
+// The frame as one ort_pixel_paths launch (use_pixel_paths); dout: the frame on the device.
+int render_pixel_paths(ort_ctx* ctx, const ort_params* p, const ort_tile* t, int mode, float* dout, hipStream_t s) {
+    const int tilesX = (t->width + 15) / 16, tilesY = (t->rows + 15) / 16;
+    const long long blocks = (long long)tilesX * tilesY;
+    PipeArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.pp = pixel_params(p);
+    a.S = device_scene(ctx);
+    a.tm = {t->x0, t->width, t->y0, t->rows, t->band_height, t->band_stride};
+    a.tilesX = tilesX;
+    a.tilesY = tilesY;
+    a.total = (int)(blocks * kBlock);
+    a.exact_only = ctx->exact_only || !ctx->ordered;
+    a.out = dout;
+    // the cursor and done count: this frame's counter set (zero; the kernel's last workgroup
+    // zeroes them again, so the set stays the pipeline's next one)
+    if (!ctx->sync_ok) {
+        HIPCHK(ctx, hipMemsetAsync(ctx->defer_count.p, 0, 128, s));
+        ctx->sync_set = 0;
+        ctx->pre_ok = false;
+    }
+    ctx->sync_ok = false;
+    a.sync = (int*)ctx->defer_count.p + 16 * ctx->sync_set;
+    const bool deep = ctx->depth > 8;
+    const size_t lds = mode == 0 ? lds_bytes(0, ctx->depth, true) : 0;
+    const int g = mode == 2 ? pixel_paths_blocks<2, false>(ctx->device, lds, blocks)
+                            : (deep ? pixel_paths_blocks<0, true>(ctx->device, lds, blocks)
+                                    : pixel_paths_blocks<0, false>(ctx->device, lds, blocks));
+    const int fslot = (int)(ctx->frames % ort_ctx::kRing);
+    ctx->tseg[fslot] = 0;
+    const bool timed = !((ctx->debug_flags & 1) || !ctx->launch_times);
+    if (timed && !ctx->tr0[fslot][0]) {
+        HIPCHK(ctx, hipEventCreate(&ctx->tr0[fslot][0]));
+        HIPCHK(ctx, hipEventCreate(&ctx->tr1[fslot][0]));
+    }
+    ctx->ev0_last = timed ? ctx->tr0[fslot][0] : ctx->ev0;  // the frame's start is its trace launch's
+    HIPCHK(ctx, hipEventRecord(ctx->ev0_last, s));
+    if (mode == 2) hipLaunchKernelGGL((ort_pixel_paths<2, false>), dim3(g), dim3(kBlock), 0, s, a);
+    else if (deep) hipLaunchKernelGGL((ort_pixel_paths<0, true>), dim3(g), dim3(kBlock), lds, s, a);
+    else hipLaunchKernelGGL((ort_pixel_paths<0, false>), dim3(g), dim3(kBlock), lds, s, a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(ctx, e, "ort_pixel_paths launch");
+    if (timed) {
+        HIPCHK(ctx, hipEventRecord(ctx->tr1[fslot][0], s));
+        ctx->tseg[fslot] = 1;
+        ctx->frames += 1;
+    }
+    HIPCHK(ctx, hipEventRecord(ctx->ev1, s));
+    ctx->timed = true;
+    ctx->sync_ok = true;
+    return ORT_OK;
 }
 
 int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out, int out_is_device,
@@ -1898,6 +2114,16 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     }
     const int ns = p->num_samples, maxd = p->max_depth;
     const bool direct = (ns == 1 && maxd == 1);
+    if (!dcounters && use_pixel_paths(ctx, mode, ns, maxd)) {  // the frame in one launch
+        if ((rc = ensure(ctx, ctx->defer_count, 128)) || (rc = render_pixel_paths(ctx, p, t, mode, dout, s))) return rc;
+        if (!out_is_device) {
+            HIPCHK(ctx, hipMemcpyAsync(out, dout, 12 * pix, hipMemcpyDeviceToHost, s));
+            HIPCHK(ctx, hipStreamSynchronize(s));
+        } else if (!stream) {
+            HIPCHK(ctx, hipStreamSynchronize(s));
+        }
+        return ORT_OK;
+    }
     if ((rc = ensure(ctx, ctx->hit, 8 * slots)) || (rc = ensure(ctx, ctx->defer_list, 4 * slots)) ||
         (rc = ensure(ctx, ctx->defer_count, 128)))
         return rc;
@@ -2000,7 +2226,11 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
     a.final_out = fuse_first ? 1 : 0;
     a.key_spread = (const uint32_t*)ctx->key_spread.p;
     // the cost order: the per-workgroup camera-ray kernels (ort_trace_compact[_deep]) only
-    bool cam_moved = false;  // the camera moved since this context's last frame (cost order on)
+    // the camera moved since this context's last rendered frame (counting renders leave the
+    // record alone): heavy priority here and heavy-first's bounce classes below both gate on it,
+    // whether or not the cost order is on
+    const bool cam_moved = mode == 0 && std::memcmp(&ctx->prio_cam, &a.pp.cam, sizeof(ort::KCamera)) != 0;
+    if (mode == 0 && !dcounters) ctx->prio_cam = a.pp.cam;
     if (mode == 0 && ctx->cost_order && ctx->depth >= 2) {
         if ((rc = ensure(ctx, ctx->pcost, 2 * slots))) return rc;
         const unsigned long long sig = frame_sig(ctx, p, t);
@@ -2015,9 +2245,7 @@ int render_impl(ort_ctx* ctx, const ort_params* p, const ort_tile* t, float* out
         // correlation of 0.82 with the new walks, reprojected ones 0.05 -- profiles/r05_moving_*),
         // and raising the wrong waves costs: C3 moving frames 1.855 -> 1.798 ms without it
         // (profiles/r05_moving_shift_c3.log), static frames unchanged
-        cam_moved = std::memcmp(&ctx->prio_cam, &a.pp.cam, sizeof(ort::KCamera)) != 0;
         a.prio_steps = cam_moved ? 0 : ctx->heavy_prio;
-        if (!dcounters) ctx->prio_cam = a.pp.cam;
     }
     // split walks of the heavy camera rays (1 sample; the production kernels, bounce 0)
     const int split_steps = ctx->split_steps >= 0 ? ctx->split_steps
@@ -2455,6 +2683,11 @@ int ort_set_option(ort_ctx* ctx, int option, int value) {
     if (option == ORT_OPT_SPLIT_LEVEL) {
         if (value < 0 || value > ORT_COMPACT_MAX_DEPTH) return fail(ctx, ORT_ERR_INVALID_ARG, "ORT_OPT_SPLIT_LEVEL: 0 (auto) .. 10");
         ctx->split_level = value;
+        return ORT_OK;
+    }
+    if (option == ORT_OPT_PIXEL_PATHS) {
+        if (value < -1 || value > 1) return fail(ctx, ORT_ERR_INVALID_ARG, "ORT_OPT_PIXEL_PATHS: -1 (auto), 0 or 1");
+        ctx->pixel_paths = value;
         return ORT_OK;
     }
     if (option == ORT_OPT_LAUNCH_TIMES) {

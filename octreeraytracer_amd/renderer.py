@@ -119,6 +119,11 @@ class Renderer:
         0 times only the frame (last_kernel_ms) -- fewer event packets per frame; same pixels."""
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_LAUNCH_TIMES, int(on)))
 
+    def set_pixel_paths(self, mode: int):
+        """ORT_OPT_PIXEL_PATHS: -1 (default) auto, 0 the per-bounce pipeline, 1 whole-pixel paths in one
+        launch wherever they apply (same pixels)."""
+        self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_PIXEL_PATHS, int(mode)))
+
     def set_xcd_swizzle(self, mode: int):
         """Workgroup -> tile order (ORT_OPT_XCD_SWIZZLE): 2 runs of raster tiles per XCD, 1
         128x128-pixel super-tiles per XCD, 0 raster, -1 (default) raster on small one-tile-workgroup

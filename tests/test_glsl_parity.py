@@ -6,7 +6,10 @@
    oracle's -- and so to the HIP kernels' -- on every case of tests/golden/glsl/canonical.json:
    C1, the DEBUG scene, M=1, C2, the whole 1920x1080 C2 and 3840x2160 C3 bench frames, brute force at 4 bounces,
    the prebuilt scene at 4 samples x 8 bounces, C2 at 2 x 4 and (1920x1080) 4 x 8, depth-9/10
-   M=1 trees with bounces (the HIP deep kernels), the sphere-root edge cases.  Only SHA-256s are stored.
+   M=1 trees with bounces (the HIP deep kernels), the sphere-root edge cases, moved camera
+   positions (the DEBUG pose, inside and above the field) and zooms 1-30, and the reference's own
+   configurations (config.h's default 800x600 16 x 8, stats.csv:114, stats_maxspheres0.csv:68).
+   Only SHA-256s are stored.
 
 2. Within GLSL's tolerance, with llvmpipe's own builtins: tests/golden/glsl/*.npz are frames of
 /root/reference/shaders/{vertex_shader,octree_fragment_shader}.glsl run unmodified by a real GLSL
@@ -48,7 +51,7 @@ def load(name):
 
 
 def inputs(ort, c):
-    from octreeraytracer_amd.scene import DEFAULT_PITCH, DEFAULT_YAW
+    from octreeraytracer_amd.scene import DEFAULT_CAMERA_POSITION, DEFAULT_PITCH, DEFAULT_YAW, DEFAULT_ZOOM
     if c["scene"] == "random":
         s = ort.random_spheres(c["n"], 42)
     elif c["scene"] == "prebuilt":
@@ -59,8 +62,11 @@ def inputs(ort, c):
     else:
         s = ort.debug_spheres()
     t = ort.build_octree(s, c["depth"], c["m"])
+    # the camera: yaw/pitch offsets from main.cpp's camera; position and zoom when the case names them
     p = ort.FrameParams.default_camera(c["W"], c["H"], yaw=DEFAULT_YAW + c["dyaw"], pitch=DEFAULT_PITCH + c["dpitch"],
-                                       num_samples=c["spp"], max_depth=c["md"], use_octree=c["oct"])
+                                       num_samples=c["spp"], max_depth=c["md"], use_octree=c["oct"],
+                                       position=tuple(c.get("pos", DEFAULT_CAMERA_POSITION)),
+                                       zoom=c.get("zoom", DEFAULT_ZOOM))
     return s, t, p
 
 
@@ -126,7 +132,7 @@ def test_canonical_prelude_is_ort_math():
     import glsl_builtins_check as B
     assert B.prelude() == PRELUDE.read_text()
     assert hashlib.sha256(PRELUDE.read_bytes()).hexdigest() == CANON["prelude_sha256"]
-    assert "llvmpipe" in CANON["renderer"] and len(CANON["cases"]) >= 18
+    assert "llvmpipe" in CANON["renderer"] and len(CANON["cases"]) >= 28
 
 
 @pytest.mark.parametrize("name", sorted(CANON["cases"]))
@@ -156,7 +162,8 @@ def test_fixtures_regenerate_bit_for_bit(name):
 
 
 @pytest.mark.skipif(not (RUNNER.exists() and SHADERS.exists()), reason="needs oracle/_ref/glsl_run and /root/reference")
-@pytest.mark.parametrize("name", ["c1", "prebuilt_spp4_d8", "c2_spp2_d4", "m8_d7_odd_b2"])
+@pytest.mark.parametrize("name", ["c1", "prebuilt_spp4_d8", "c2_spp2_d4", "m8_d7_odd_b2", "debug_pose", "c2tree_zoom1",
+                                  "config_default"])
 def test_canonical_hashes_regenerate(name):
     """The canonical-builtin hashes are what the reference's shaders give now."""
     import sys

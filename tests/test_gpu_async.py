@@ -22,6 +22,7 @@ def c2_bounce(ort, scene_c2):
     s, t = scene_c2
     r = ort.Renderer(0)
     r.upload(s, t)
+    r.set_pixel_paths(0)  # the per-bounce pipeline (its options are under test)
     yield s, t, r
     r.close()
 
@@ -53,6 +54,7 @@ def test_multibounce_render_returns_before_the_frame_ends(ort, oracle, c2_bounce
     img = out.cpu().numpy()
     with ort.Renderer(0) as r0:  # slot order, synchronous: an independent path order
         r0.upload(s, t)
+        r0.set_pixel_paths(0)  # the per-bounce pipeline (its options are under test)
         r0.set_sort_paths(0)
         assert_same(img, r0.render(p), "stream-ordered list sort vs slot order")
     ref = oracle.render(s, t, p, 0, 500, W, 40, threads=0)
@@ -87,6 +89,7 @@ def test_hints_follow_the_frame_shape(ort, c2_bounce):
     for p, tl in shapes:
         with ort.Renderer(0) as fresh:
             fresh.upload(s, t)
+            fresh.set_pixel_paths(0)  # the per-bounce pipeline (its options are under test)
             want.append(fresh.render(p, tl))
     for rep in range(2):
         for (p, tl), w in zip(shapes, want):

@@ -37,6 +37,7 @@ def test_cost_order_frames_match_block_order(ort, oracle, scene_c2, ns, md):
     for on in (1, 0):
         with ort.Renderer(0) as r:
             r.upload(s, t)
+            r.set_pixel_paths(0)  # the per-bounce pipeline (its options are under test)
             r.set_cost_order(on)
             got[on] = _frames(ort, r, s, t, params, tiles)
     for i, (a, b) in enumerate(zip(got[1], got[0])):
@@ -57,6 +58,7 @@ def test_cost_order_deep_tree(ort, oracle):
     for on in (1, 0):
         with ort.Renderer(0) as r:
             r.upload(s, t)
+            r.set_pixel_paths(0)  # the per-bounce pipeline (its options are under test)
             r.set_cost_order(on)
             got[on] = [r.render(p) for _ in range(2)]
     assert_same(got[1][1], got[0][1], "depth 9, second frame: cost order vs block order")
@@ -87,6 +89,7 @@ def test_heavy_first_frames_match_coherence_order(ort, oracle, depth):
     for thr in (0, 8, 48):
         with ort.Renderer(0) as r:
             r.upload(s, t)
+            r.set_pixel_paths(0)  # the per-bounce pipeline (its options are under test)
             r.set_heavy_first(thr)
             got[thr] = [r.render(p) for _ in range(3)]
     for thr in (8, 48):
@@ -109,13 +112,19 @@ def test_heavy_first_moving_camera(ort, oracle, depth):
     ps = [ort.FrameParams.default_camera(W, H, num_samples=1, max_depth=4, yaw=DEFAULT_YAW + 0.5 * j)
           for j in (0, 0, 1, 2, 2)]  # static, moved, moved, static
     got = {}
-    for thr in (0, 48):
+    # (48, 0): heavy first with the cost order off -- the camera-moved test that gates the
+    # bounce classes must not depend on the cost order (it did until round 6)
+    for thr, cost_order in ((0, 1), (48, 1), (48, 0)):
         with ort.Renderer(0) as r:
             r.upload(s, t)
+            r.set_pixel_paths(0)  # the per-bounce pipeline (its options are under test)
+            r.set_cost_order(cost_order)
             r.set_heavy_first(thr)
-            got[thr] = [r.render(p) for p in ps]
+            got[thr, cost_order] = [r.render(p) for p in ps]
     for i in range(len(ps)):
-        assert_same(got[48][i], got[0][i], f"depth {depth}, frame {i}: heavy first vs coherence order")
+        assert_same(got[48, 1][i], got[0, 1][i], f"depth {depth}, frame {i}: heavy first vs coherence order")
+        assert_same(got[48, 0][i], got[0, 1][i], f"depth {depth}, frame {i}: heavy first, cost order off")
+    got[48] = got[48, 1]
     ref = oracle.render(s, t, ps[3], 0, 80, W, 8, threads=0)
     assert_same(got[48][3][80:88], ref, f"depth {depth}, moved frame vs oracle")
 
@@ -157,10 +166,12 @@ def test_split_heavy_frames_match(ort, oracle, scene_c2, split, level, prio, md)
     tiles = [full, full, full, full, band, band, full]
     with ort.Renderer(0) as r:
         r.upload(s, t)
+        r.set_pixel_paths(0)  # the per-bounce pipeline (its options are under test)
         _plain(r)
         want = _frames(ort, r, s, t, params, tiles)
     with ort.Renderer(0) as r:
         r.upload(s, t)
+        r.set_pixel_paths(0)  # the per-bounce pipeline (its options are under test)
         r.set_split_heavy(split)
         r.set_split_level(level)
         r.set_heavy_prio(prio)
@@ -179,10 +190,12 @@ def test_split_heavy_deep_tree(ort, oracle):
     p = ort.FrameParams.default_camera(W, H)
     with ort.Renderer(0) as r:
         r.upload(s, t)
+        r.set_pixel_paths(0)  # the per-bounce pipeline (its options are under test)
         _plain(r)
         want = [r.render(p) for _ in range(2)]
     with ort.Renderer(0) as r:
         r.upload(s, t)
+        r.set_pixel_paths(0)  # the per-bounce pipeline (its options are under test)
         r.set_split_heavy(30)
         got = [r.render(p) for _ in range(3)]
     for g in got:
@@ -210,6 +223,7 @@ def test_tile_pairs_frames_match(ort, oracle, ns, md, depth):
     for on in (1, 0):
         with ort.Renderer(0) as r:
             r.upload(s, t)
+            r.set_pixel_paths(0)  # the per-bounce pipeline (its options are under test)
             r.set_tile_pairs(on)
             r.set_heavy_prio(100)
             got[on] = _frames(ort, r, s, t, params, tiles)
@@ -229,10 +243,12 @@ def test_split_heavy_queued_list_across_other_frames(ort, oracle, scene_c2):
     full = ort.Tile(0, W, 0, H)
     with ort.Renderer(0) as r:
         r.upload(s, t)
+        r.set_pixel_paths(0)  # the per-bounce pipeline (its options are under test)
         _plain(r)
         want_band, want_full = r.render(p, band), r.render(p, full)
     with ort.Renderer(0) as r:
         r.upload(s, t)
+        r.set_pixel_paths(0)  # the per-bounce pipeline (its options are under test)
         _plain(r)
         r.set_split_heavy(30)
         got = [r.render(p, band) for _ in range(3)]

@@ -19,6 +19,21 @@ def assert_same(img, ref, what=""):
     assert bad == 0, f"{what}: {bad} pixels not bit-identical"
 
 
+class pixel_paths:
+    """ORT_OPT_PIXEL_PATHS for a block: 0 the per-bounce pipeline (the tests of its options), 1
+    whole-pixel paths in one launch; the default (-1, auto) restored after."""
+
+    def __init__(self, renderer, mode):
+        self.r, self.mode = renderer, mode
+
+    def __enter__(self):
+        self.r.set_pixel_paths(self.mode)
+        return self.r
+
+    def __exit__(self, *exc):
+        self.r.set_pixel_paths(-1)
+
+
 @pytest.mark.parametrize("layout", [0, 1])
 def test_c1_bit_exact(ort, oracle, renderer, scene_c1, layout):
     s, t = scene_c1
@@ -30,18 +45,22 @@ def test_c1_bit_exact(ort, oracle, renderer, scene_c1, layout):
     renderer.set_layout(-1)
 
 
-def test_c1_bounces_and_samples(ort, oracle, renderer, scene_c1):
+@pytest.mark.parametrize("mode", [0, 1])
+def test_c1_bounces_and_samples(ort, oracle, renderer, scene_c1, mode):
     s, t = scene_c1
     renderer.upload(s, t)
     p = ort.FrameParams.default_camera(160, 120, num_samples=4, max_depth=8)
-    assert_same(renderer.render(p), oracle.render(s, t, p), "C1 spp4 depth8")
+    with pixel_paths(renderer, mode):
+        assert_same(renderer.render(p), oracle.render(s, t, p), f"C1 spp4 depth8 pixel_paths={mode}")
 
 
-def test_brute_force_mode(ort, oracle, renderer, scene_c1):
+@pytest.mark.parametrize("mode", [0, 1])
+def test_brute_force_mode(ort, oracle, renderer, scene_c1, mode):
     s, t = scene_c1
     renderer.upload(s, t)
-    p = ort.FrameParams.default_camera(128, 128, use_octree=0, max_depth=4)
-    assert_same(renderer.render(p), oracle.render(s, None, p), "brute force")
+    p = ort.FrameParams.default_camera(128, 128, use_octree=0, max_depth=4, num_samples=2)
+    with pixel_paths(renderer, mode):
+        assert_same(renderer.render(p), oracle.render(s, None, p), f"brute force pixel_paths={mode}")
 
 
 def test_prebuilt_scene(ort, oracle, renderer):
@@ -164,6 +183,7 @@ def test_kernel_variants_identical(ort, oracle, renderer, scene_c2, persistent, 
     renderer.set_persistent(persistent)
     renderer.set_exact_traversal(exact)
     renderer.set_refill(refill)
+    renderer.set_pixel_paths(0)  # the pipeline's kernels (C2's small tree would take whole-pixel paths)
     try:
         p = ort.FrameParams.default_camera(1920, 1080, num_samples=2, max_depth=3)
         tile = ort.Tile(700, 200, 300, 120)
@@ -172,10 +192,13 @@ def test_kernel_variants_identical(ort, oracle, renderer, scene_c2, persistent, 
         assert_same(got, ref, f"variant persistent={persistent} exact={exact}")
         p1 = ort.FrameParams.default_camera(1920, 1080)
         assert_same(renderer.render(p1, tile), oracle.render(s, t, p1, 700, 300, 200, 120), "primary")
+        with pixel_paths(renderer, 1):  # and whole-pixel paths, fast or exact walk
+            assert_same(renderer.render(p, tile), ref, f"pixel paths exact={exact}")
     finally:
         renderer.set_persistent(2)  # the default
         renderer.set_exact_traversal(False)
         renderer.set_refill(16)  # the default
+        renderer.set_pixel_paths(-1)
 
 
 def test_removed_options_are_refused(ort, renderer):
@@ -205,6 +228,7 @@ def test_bounce_orders_and_skip_identical(ort, oracle, renderer, depth, mspn, so
     renderer.upload(s, t)
     renderer.set_sort_paths(sort)
     renderer.set_kid_skip(kid_skip)
+    renderer.set_pixel_paths(0)  # the pipeline's bounce lists
     try:
         p = ort.FrameParams.default_camera(960, 540, num_samples=2, max_depth=5)
         tile = ort.Tile(100, 400, 200, 96)
@@ -213,13 +237,18 @@ def test_bounce_orders_and_skip_identical(ort, oracle, renderer, depth, mspn, so
         assert_same(got, ref, f"sort={sort} kid_skip={kid_skip} d{depth}")
         with pytest.raises(ort.OrtError):
             renderer.set_kid_skip(3)
+        if sort == 2:  # whole-pixel paths, with and without the skip
+            with pixel_paths(renderer, 1):
+                assert_same(renderer.render(p, tile), ref, f"pixel paths kid_skip={kid_skip} d{depth}")
     finally:
         renderer.set_sort_paths(2)  # the defaults
         renderer.set_kid_skip(1)
+        renderer.set_pixel_paths(-1)
 
 
+@pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("ns", [1, 2])
-def test_band_padding_rows_with_bounces(ort, oracle, renderer, scene_c2, ns):
+def test_band_padding_rows_with_bounces(ort, oracle, renderer, scene_c2, ns, mode):
     """Band tiles whose rows run past the frame (the multi-GPU partition's padding) in the
     multi-bounce pipeline, where the last shading writes the final pixels itself: the padding
     rows come back as zeros and every other pixel as the oracle's."""
@@ -227,9 +256,10 @@ def test_band_padding_rows_with_bounces(ort, oracle, renderer, scene_c2, ns):
     renderer.upload(s, t)
     p = ort.FrameParams.default_camera(320, 180, num_samples=ns, max_depth=4)
     tile = ort.Tile(0, 320, 150, 64, 16, 64)  # rows y = 150 + 64 (j / 16) + j % 16: most past 180
-    got = renderer.render(p, tile)
+    with pixel_paths(renderer, mode):
+        got = renderer.render(p, tile)
     ref = oracle.render(s, t, p, 0, 150, 320, 64, band_height=16, band_stride=64)
-    assert_same(got, ref, f"band padding ns={ns}")
+    assert_same(got, ref, f"band padding ns={ns} pixel_paths={mode}")
     assert float(np.abs(got[16:]).max()) == 0.0  # rows past the frame
 
 
@@ -269,14 +299,18 @@ def test_bounce_compaction_after_larger_frames(ort, oracle, renderer, scene_c2):
     render left alive must never leak into a later, smaller tile."""
     s, t = scene_c2
     renderer.upload(s, t)
-    big = ort.FrameParams.default_camera(1920, 1080, num_samples=1, max_depth=4)
-    renderer.render(big, ort.Tile(0, 1920, 0, 256))
-    p = ort.FrameParams.default_camera(1920, 1080, num_samples=2, max_depth=5)
-    for tile in (ort.Tile(900, 70, 500, 30), ort.Tile(0, 1920, 3, 40, 8, 27)):
-        got = renderer.render(p, tile)
-        ref = oracle.render(s, t, p, tile.x0, tile.y0, tile.width, tile.rows, band_height=tile.band_height,
-                            band_stride=tile.band_stride)
-        assert_same(got, ref, f"compaction tile {tile}")
+    with pixel_paths(renderer, 0):  # the pipeline's compacted lists
+        big = ort.FrameParams.default_camera(1920, 1080, num_samples=1, max_depth=4)
+        renderer.render(big, ort.Tile(0, 1920, 0, 256))
+        p = ort.FrameParams.default_camera(1920, 1080, num_samples=2, max_depth=5)
+        for tile in (ort.Tile(900, 70, 500, 30), ort.Tile(0, 1920, 3, 40, 8, 27)):
+            got = renderer.render(p, tile)
+            ref = oracle.render(s, t, p, tile.x0, tile.y0, tile.width, tile.rows, band_height=tile.band_height,
+                                band_stride=tile.band_stride)
+            assert_same(got, ref, f"compaction tile {tile}")
+            with pixel_paths(renderer, 1):  # whole-pixel paths after pipeline frames, and back
+                assert_same(renderer.render(p, tile), ref, f"pixel paths tile {tile}")
+            renderer.set_pixel_paths(0)
 
 
 @pytest.mark.parametrize("depth,mspn", [(9, 0), (10, 1)])
@@ -292,8 +326,12 @@ def test_deep_tree_kernel_bit_exact(ort, oracle, renderer, depth, mspn):
     assert_same(renderer.render(p), oracle.render(s, t, p), f"deep d{depth} primary")
     pb = ort.FrameParams.default_camera(1280, 720, num_samples=2, max_depth=4)
     try:
-        for sort in (0, 1, 2):
-            renderer.set_sort_paths(sort)
+        for sort in (0, 1, 2, "pixel paths"):
+            if sort == "pixel paths":  # the depth 9-10 whole-pixel kernel (96-bit masks)
+                renderer.set_pixel_paths(1)
+            else:
+                renderer.set_pixel_paths(0)
+                renderer.set_sort_paths(sort)
             for tile in (ort.Tile(300, 160, 200, 96), ort.Tile(0, 1280, 5, 48, 8, 90)):
                 got = renderer.render(pb, tile)
                 ref = oracle.render(s, t, pb, tile.x0, tile.y0, tile.width, tile.rows, band_height=tile.band_height,
@@ -301,6 +339,7 @@ def test_deep_tree_kernel_bit_exact(ort, oracle, renderer, depth, mspn):
                 assert_same(got, ref, f"deep d{depth} bounces {tile} sort={sort}")
     finally:
         renderer.set_sort_paths(2)  # the default
+        renderer.set_pixel_paths(-1)
 
 
 @pytest.mark.parametrize("mode", [0, 1, 2, -1])
@@ -310,6 +349,7 @@ def test_xcd_swizzle_orders_identical(ort, oracle, renderer, scene_c2, mode):
     s, t = scene_c2
     renderer.upload(s, t)
     renderer.set_xcd_swizzle(mode)
+    renderer.set_pixel_paths(0)  # the pipeline's per-tile kernels
     try:
         p = ort.FrameParams.default_camera(1920, 1080, num_samples=1, max_depth=3)
         tile = ort.Tile(13, 1900, 7, 1010)  # 119 x 64 tiles: ragged in both directions
@@ -321,6 +361,7 @@ def test_xcd_swizzle_orders_identical(ort, oracle, renderer, scene_c2, mode):
                 renderer.set_xcd_swizzle(bad)
     finally:
         renderer.set_xcd_swizzle(-1)
+        renderer.set_pixel_paths(-1)
 
 
 @pytest.mark.parametrize("use_octree", [1, 0])
@@ -332,7 +373,10 @@ def test_extreme_sphere_roots(ort, oracle, renderer, use_octree):
     t = ort.build_octree(s, 5, 0) if use_octree else None
     renderer.upload(s, t)
     p = ort.FrameParams.default_camera(64, 40, max_depth=4, use_octree=use_octree)
-    assert_same(renderer.render(p), oracle.render(s, t, p), "extreme roots")
+    ref = oracle.render(s, t, p)
+    for mode in (0, 1):
+        with pixel_paths(renderer, mode):
+            assert_same(renderer.render(p), ref, f"extreme roots pixel_paths={mode}")
     p1 = ort.FrameParams.default_camera(64, 40, use_octree=use_octree)
     assert_same(renderer.render(p1), oracle.render(s, t, p1), "extreme roots, primary")
 
@@ -370,10 +414,30 @@ def test_kernel_bit_exact_to_reference_shader(ort, renderer, name):
 
 
 def test_launch_times_option(ort, oracle, renderer, scene_c1):
-    """ORT_OPT_LAUNCH_TIMES 0: no per-launch events, same pixels, the frame still timed."""
+    """ORT_OPT_LAUNCH_TIMES 0: no per-launch events, same pixels, the frame still timed -- and the
+    per-launch queries report no newer launch (include/ort.h): on a context never timed
+    ort_last_trace_ms is an error and ort_trace_times_ms returns nothing; after one timed frame,
+    untimed frames leave that frame's launch time the newest."""
     s, t = scene_c1
-    renderer.upload(s, t)
     p = ort.FrameParams.default_camera(96, 64, num_samples=2, max_depth=3)
+    with ort.Renderer(0) as fresh:
+        fresh.upload(s, t)
+        fresh.set_launch_times(0)
+        assert_same(fresh.render(p), oracle.render(s, t, p), "launch times off, fresh context")
+        assert fresh.last_kernel_ms() > 0.0
+        with pytest.raises(ort.OrtError):
+            fresh.last_trace_ms()
+        assert fresh.trace_times_ms(4) == []
+        fresh.set_launch_times(1)
+        fresh.render(p)  # one timed frame
+        timed = fresh.trace_times_ms(1)
+        assert len(timed) == 1 and timed[0] > 0.0 and fresh.last_trace_ms() == timed[0]
+        fresh.set_launch_times(0)
+        for _ in range(3):
+            fresh.render(p)
+        assert fresh.trace_times_ms(1) == timed and fresh.last_trace_ms() == timed[0]
+        assert len(fresh.trace_times_ms(8)) == 1
+    renderer.upload(s, t)
     try:
         renderer.set_launch_times(0)
         got = renderer.render(p)
@@ -385,3 +449,32 @@ def test_launch_times_option(ort, oracle, renderer, scene_c1):
         renderer.set_launch_times(1)
     renderer.render(p)
     assert renderer.last_trace_ms() > 0.0
+
+
+def test_pixel_paths_option_and_auto(ort, oracle, scene_c1, scene_c3):
+    """ORT_OPT_PIXEL_PATHS: -1 / 0 / 1 accepted, others refused; the auto mode renders a
+    small tree's multi-bounce frame in ONE trace launch and the C3 tree's (10.9 M nodes) with
+    the per-bounce pipeline; primary-ray frames (1 sample, 1 bounce) never take it."""
+    s, t = scene_c1
+    p = ort.FrameParams.default_camera(128, 96, num_samples=4, max_depth=6)
+    with ort.Renderer(0) as r:
+        for bad in (-2, 2):
+            with pytest.raises(ort.OrtError):
+                r.set_pixel_paths(bad)
+        r.upload(s, t)
+        ref = oracle.render(s, t, p)
+        for mode, launches in ((-1, 1), (1, 1), (0, None)):
+            r.set_pixel_paths(mode)
+            assert_same(r.render(p), ref, f"pixel_paths={mode}")
+            n = r.frame_trace_times_ms(1)[0][1]
+            assert n == launches if launches else n > 1, (mode, n)
+        r.set_pixel_paths(1)
+        p1 = ort.FrameParams.default_camera(128, 96)
+        assert_same(r.render(p1), oracle.render(s, t, p1), "primary")
+    s3, t3 = scene_c3
+    with ort.Renderer(0) as r:
+        r.upload(s3, t3)
+        pb = ort.FrameParams.default_camera(256, 144, num_samples=2, max_depth=3)
+        got = r.render(pb)
+        assert r.frame_trace_times_ms(1)[0][1] > 1  # auto: the pipeline on a large tree
+        assert_same(got, oracle.render(s3, t3, pb), "C3 tree, auto")

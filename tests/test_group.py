@@ -146,34 +146,61 @@ def test_group_submit_requires_out(ort):
 def test_group_wait_is_bounded(ort, scene_c2):
     """ort_group_set_timeout: a wait that expires returns ORT_ERR_TIMEOUT naming the frame, its
     slot and what is still pending (instead of blocking: a first multi-GPU run that stalls says
-    where); the frame stays submitted and a later wait sees it complete, bit-exact."""
+    where); the frame stays submitted and a later wait sees it complete, bit-exact.
+
+    Deterministic: rank 0's stream is held by a device-side gate the test owns
+    (hipStreamWaitValue32 on a hipMallocSignalMemory flag, enqueued ahead of the submit), so the
+    frame cannot complete before the zero-timeout poll whatever the GPU's speed; the flag is set
+    (hipStreamWriteValue32 on a stream of the test's) after the poll, and in any case before the
+    group is destroyed."""
+    import ctypes as C
     from octreeraytracer_amd.group import RenderGroup
     s, t = scene_c2
-    p = ort.FrameParams.default_camera(1920, 1080, num_samples=8, max_depth=4)  # tens of ms
+    p = ort.FrameParams.default_camera(320, 180, num_samples=2, max_depth=3)
     with ort.Renderer(0) as r:
         r.upload(s, t)
         want = r.render(p)
     torch = pytest.importorskip("torch")
-    with RenderGroup([0, 0], 1, inflight=2) as g:
-        g.upload(s, t)
-        # device output: a pageable host output makes the submit's final copy synchronous
-        out = torch.empty((1080, 1920, 3), dtype=torch.float32, device="cuda:0")
-        msgs = []
-        for _ in range(3):
-            g.set_timeout(0)  # poll once
-            tk = g.submit(p, out)
+    hip = C.CDLL("libamdhip64.so.7")  # the runtime libort.so is linked against (already loaded)
+    assert hip.hipSetDevice(0) == 0
+    flag, rel = C.c_void_p(), C.c_void_p()
+    assert hip.hipExtMallocWithFlags(C.byref(flag), C.c_size_t(64), C.c_uint(0x2)) == 0  # hipMallocSignalMemory
+    assert hip.hipStreamCreate(C.byref(rel)) == 0
+    released = []
+
+    def release():
+        if not released:  # hipStreamWriteValue32(stream, ptr, value, flags)
+            assert hip.hipStreamWriteValue32(rel, flag, C.c_uint32(1), C.c_uint(0)) == 0
+            assert hip.hipStreamSynchronize(rel) == 0
+            released.append(1)
+
+    assert hip.hipStreamWriteValue32(rel, flag, C.c_uint32(0), C.c_uint(0)) == 0
+    assert hip.hipStreamSynchronize(rel) == 0
+    try:
+        with RenderGroup([0, 0], 1, inflight=2) as g:
+            g.upload(s, t)
+            out = torch.empty((180, 320, 3), dtype=torch.float32, device="cuda:0")  # device output: no host copy
+            h = C.c_void_p()
+            assert g._lib.ort_get_stream(g.context(0), C.byref(h)) == 0 and h.value  # slot 0, rank 0
             try:
-                g.wait(tk)
-            except ort.OrtError as e:
-                assert e.code == ort.ORT_ERR_TIMEOUT
-                msgs.append(str(e))
+                # hipStreamWaitValue32(stream, ptr, value, flags = hipStreamWaitValueGte, mask)
+                assert hip.hipStreamWaitValue32(h, flag, C.c_uint32(1), C.c_uint(0), C.c_uint32(0xFFFFFFFF)) == 0
+                g.set_timeout(0)  # poll once
+                tk = g.submit(p, out)  # ticket 0: slot 0, behind the gate
+                with pytest.raises(ort.OrtError) as e:
+                    g.wait(tk)
+            finally:
+                release()
+            assert e.value.code == ort.ORT_ERR_TIMEOUT
+            msg = str(e.value)
+            assert "slot" in msg and "pending" in msg and "frame" in msg and "rank 0" in msg, msg
             g.set_timeout(120_000)
             g.wait(tk)
             assert np.array_equal(out.cpu().numpy().view(np.uint32), want.view(np.uint32))
-            if msgs:
-                break
-        assert msgs, "a 8-spp 4-bounce C2 frame completed before a zero-timeout poll"
-        assert "slot" in msgs[0] and "pending" in msgs[0] and "frame" in msgs[0], msgs[0]
+    finally:
+        release()
+        hip.hipStreamDestroy(rel)
+        hip.hipFree(flag)
 
 
 @pytest.mark.gpu

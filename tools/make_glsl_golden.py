@@ -36,7 +36,7 @@ import numpy as np
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 import octreeraytracer_amd as ort  # noqa: E402
-from octreeraytracer_amd.scene import DEFAULT_PITCH, DEFAULT_YAW  # noqa: E402
+from octreeraytracer_amd.scene import DEFAULT_CAMERA_POSITION, DEFAULT_PITCH, DEFAULT_YAW, DEFAULT_ZOOM  # noqa: E402
 
 OUT = ROOT / "tests" / "golden" / "glsl"
 RUNNER = ROOT / "oracle" / "_ref" / "glsl_run"
@@ -89,6 +89,40 @@ CANON_EXTRA = {
     # the C3 tree (depth 8) with bounces and samples: the depth <= 8 persistent bounce walk
     "c3tree_spp3_b5": dict(scene="random", n=100000, depth=8, m=0, W=200, H=120, spp=3, md=5, oct=1, dyaw=10.0,
                            dpitch=-20.0),
+    # --- camera inputs (round 6): the reference moves Position by WASD (src/opengl/camera.h:70-81)
+    # and Zoom by the scroll wheel (camera.h:106-113, clamped to [1, 45]); both reach
+    # Camera_initFromViewMatrix (glsl:176-202) as the cameraPosition / cameraZoom uniforms.
+    # The DEBUG scene from its own camera (src/main.cpp:31: Position (30, 20, -50)), bounced
+    "debug_pose": dict(scene="debug", n=3, depth=3, m=2, W=320, H=240, spp=2, md=4, oct=1, dyaw=0.0, dpitch=0.0,
+                       pos=[30.0, 20.0, -50.0]),
+    # main.cpp:33's commented "centered" pose (0, 2.5, 0): inside the C3 field
+    "c3tree_centered": dict(scene="random", n=100000, depth=8, m=0, W=320, H=180, spp=1, md=3, oct=1, dyaw=0.0,
+                            dpitch=0.0, pos=[0.0, 2.5, 0.0]),
+    # above the C2 field (half-width 30) at pitch -40 and +40 (the shader looks along -Front:
+    # w = -normalize(view row 2), glsl:181, so +40 looks down onto the field, -40 up into the sky)
+    "c2tree_above_m40": dict(scene="random", n=10000, depth=6, m=0, W=320, H=180, spp=1, md=2, oct=1, dyaw=0.0,
+                             dpitch=-40.0, pos=[5.0, 25.0, -45.0]),
+    "c2tree_above_p40": dict(scene="random", n=10000, depth=6, m=0, W=320, H=180, spp=1, md=2, oct=1, dyaw=12.0,
+                             dpitch=40.0, pos=[5.0, 25.0, -45.0]),
+    # zoom 20 and zoom 1 (the scroll clamp's lower end): narrow fields of view, tan(theta/2) of
+    # small arguments
+    "c2tree_zoom20": dict(scene="random", n=10000, depth=6, m=0, W=320, H=180, spp=2, md=3, oct=1, dyaw=0.0,
+                          dpitch=0.0, zoom=20.0),
+    "c2tree_zoom1": dict(scene="random", n=10000, depth=6, m=0, W=320, H=180, spp=1, md=2, oct=1, dyaw=3.0,
+                         dpitch=-2.0, zoom=1.0),
+    # a moved, turned and zoomed pose together
+    "c3tree_moved_zoom30": dict(scene="random", n=100000, depth=8, m=0, W=256, H=192, spp=1, md=2, oct=1,
+                                dyaw=-35.0, dpitch=12.0, pos=[-20.0, 6.0, 15.0], zoom=30.0),
+    # --- the reference's own configurations
+    # src/config.h:10-28 (the default build): 800x600, 100 spheres, depth 3, M=0, 16 spp x 8 bounces
+    "config_default": dict(scene="random", n=100, depth=3, m=0, W=800, H=600, spp=16, md=8, oct=1, dyaw=0.0,
+                           dpitch=0.0),
+    # analysis/stats.csv:114's row: 1000 spheres, depth 5, M=1, 16 x 8, 1920x1080
+    "stats114": dict(scene="random", n=1000, depth=5, m=1, W=1920, H=1080, spp=16, md=8, oct=1, dyaw=0.0,
+                     dpitch=0.0),
+    # analysis/stats_maxspheres0.csv:68's row: 2000 spheres, depth 3, M=0, 4 x 4, 800x600
+    "ms0_row68": dict(scene="random", n=2000, depth=3, m=0, W=800, H=600, spp=4, md=4, oct=1, dyaw=0.0,
+                      dpitch=0.0),
     # a depth-9 tree subdivided to the bottom (maxSpheresPerNode 0): the deep kernels without C5's
     # one-sphere leaves (at depth 10 such trees pass 2^24 nodes even at 2000 spheres: SURVEY F7,
     # the reference's float offsets then name wrong children)
@@ -116,9 +150,16 @@ def case_inputs(c):
     else:
         s = ort.debug_spheres()
     t = ort.build_octree(s, c["depth"], c["m"])
-    p = ort.FrameParams.default_camera(c["W"], c["H"], yaw=DEFAULT_YAW + c["dyaw"], pitch=DEFAULT_PITCH + c["dpitch"],
-                                       num_samples=c["spp"], max_depth=c["md"], use_octree=c["oct"])
-    return s, t, p
+    return s, t, case_params(c)
+
+
+def case_params(c):
+    """The frame of a case: size, samples, bounces and the camera -- yaw/pitch offsets from the
+    default camera and, when the case names them, the position and zoom (else main.cpp's)."""
+    return ort.FrameParams.default_camera(c["W"], c["H"], yaw=DEFAULT_YAW + c["dyaw"], pitch=DEFAULT_PITCH + c["dpitch"],
+                                          num_samples=c["spp"], max_depth=c["md"], use_octree=c["oct"],
+                                          position=tuple(c.get("pos", DEFAULT_CAMERA_POSITION)),
+                                          zoom=c.get("zoom", DEFAULT_ZOOM))
 
 
 def write_input(path, s, t, p):
