@@ -149,10 +149,10 @@ def test_group_wait_is_bounded(ort, scene_c2):
     where); the frame stays submitted and a later wait sees it complete, bit-exact.
 
     Deterministic: rank 0's stream is held by a device-side gate the test owns
-    (hipStreamWaitValue32 on a hipMallocSignalMemory flag, enqueued ahead of the submit), so the
-    frame cannot complete before the zero-timeout poll whatever the GPU's speed; the flag is set
-    (hipStreamWriteValue32 on a stream of the test's) after the poll, and in any case before the
-    group is destroyed."""
+    (hipStreamWaitValue32 on a flag in mapped, coherent host memory, enqueued ahead of the
+    submit), so the frame cannot complete before the zero-timeout poll whatever the GPU's
+    speed; the host sets the flag after the poll, and in any case before the group is destroyed
+    (a release from another stream could share the gated stream's hardware queue)."""
     import ctypes as C
     from octreeraytracer_amd.group import RenderGroup
     s, t = scene_c2
@@ -163,19 +163,15 @@ def test_group_wait_is_bounded(ort, scene_c2):
     torch = pytest.importorskip("torch")
     hip = C.CDLL("libamdhip64.so.7")  # the runtime libort.so is linked against (already loaded)
     assert hip.hipSetDevice(0) == 0
-    flag, rel = C.c_void_p(), C.c_void_p()
-    assert hip.hipExtMallocWithFlags(C.byref(flag), C.c_size_t(64), C.c_uint(0x2)) == 0  # hipMallocSignalMemory
-    assert hip.hipStreamCreate(C.byref(rel)) == 0
-    released = []
+    flag, dflag = C.c_void_p(), C.c_void_p()
+    assert hip.hipHostMalloc(C.byref(flag), C.c_size_t(64), C.c_uint(0x40000002)) == 0  # mapped | coherent
+    gate = C.c_uint32.from_address(flag.value)
+    gate.value = 0
+    assert hip.hipHostGetDevicePointer(C.byref(dflag), flag, C.c_uint(0)) == 0
 
     def release():
-        if not released:  # hipStreamWriteValue32(stream, ptr, value, flags)
-            assert hip.hipStreamWriteValue32(rel, flag, C.c_uint32(1), C.c_uint(0)) == 0
-            assert hip.hipStreamSynchronize(rel) == 0
-            released.append(1)
+        gate.value = 1
 
-    assert hip.hipStreamWriteValue32(rel, flag, C.c_uint32(0), C.c_uint(0)) == 0
-    assert hip.hipStreamSynchronize(rel) == 0
     try:
         with RenderGroup([0, 0], 1, inflight=2) as g:
             g.upload(s, t)
@@ -184,7 +180,7 @@ def test_group_wait_is_bounded(ort, scene_c2):
             assert g._lib.ort_get_stream(g.context(0), C.byref(h)) == 0 and h.value  # slot 0, rank 0
             try:
                 # hipStreamWaitValue32(stream, ptr, value, flags = hipStreamWaitValueGte, mask)
-                assert hip.hipStreamWaitValue32(h, flag, C.c_uint32(1), C.c_uint(0), C.c_uint32(0xFFFFFFFF)) == 0
+                assert hip.hipStreamWaitValue32(h, dflag, C.c_uint32(1), C.c_uint(0), C.c_uint32(0xFFFFFFFF)) == 0
                 g.set_timeout(0)  # poll once
                 tk = g.submit(p, out)  # ticket 0: slot 0, behind the gate
                 with pytest.raises(ort.OrtError) as e:
@@ -199,8 +195,8 @@ def test_group_wait_is_bounded(ort, scene_c2):
             assert np.array_equal(out.cpu().numpy().view(np.uint32), want.view(np.uint32))
     finally:
         release()
-        hip.hipStreamDestroy(rel)
-        hip.hipFree(flag)
+        assert hip.hipDeviceSynchronize() == 0
+        hip.hipHostFree(flag)
 
 
 @pytest.mark.gpu

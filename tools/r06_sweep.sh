@@ -18,10 +18,10 @@ for g in $GRIDS; do
     > "$OUT/sweep_$g.log" 2>&1
 done
 M="$R/build/ort_main"
-timeout -k 10 120 rocprofv3 --kernel-trace --stats -d "$OUT/prof_default" -o run -- \
+timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_default" -o run -- \
   "$M" --spheres 100 --depth 3 --per-node 0 --samples 16 --bounces 8 --width 800 --height 600 --frames 20 --warmup 5 \
   > "$OUT/prof_default.log" 2>&1
-timeout -k 10 120 rocprofv3 --kernel-trace --stats -d "$OUT/prof_stats114" -o run -- \
+timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_stats114" -o run -- \
   "$M" --spheres 1000 --depth 5 --per-node 1 --samples 16 --bounces 8 --width 1920 --height 1080 --frames 20 --warmup 5 \
   > "$OUT/prof_stats114.log" 2>&1
 echo sweep done
