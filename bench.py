@@ -49,7 +49,12 @@ CONFIGS = {
     "c2": (1920, 1080, 10_000, 6, 0, 1, 1),
     "c3": (3840, 2160, 100_000, 8, 0, 1, 1),
     "c5": (7680, 4320, 1_000_000, 10, 1, 1, 4),
+    # the reference's own workloads: src/config.h:10-28's default build (16 samples x 8 bounces)
+    # and analysis/stats.csv:114's sweep row -- whole-pixel paths (ORT_OPT_PIXEL_PATHS auto)
+    "ref_default": (800, 600, 100, 3, 0, 16, 8),
+    "ref_stats114": (1920, 1080, 1000, 5, 1, 16, 8),
 }
+PIXEL_PATHS_AUTO_NODES = 1 << 21  # ort_kernel.hip kPixelPathsAutoNodes
 
 
 def reference_frame_check(config: str, frame, host=None):
@@ -57,7 +62,7 @@ def reference_frame_check(config: str, frame, host=None):
     reference's own shaders give for the same scene and camera -- run on Mesa llvmpipe with the
     canonical builtins and pixel centre, tests/golden/glsl/canonical.json (tests/test_glsl_parity.py).  None when
     no such hash exists for the config (C5: its tree is too large for llvmpipe) or no frame."""
-    cases = {"c1": "c1", "c2": "c2_full", "c3": "c3_full"}
+    cases = {"c1": "c1", "c2": "c2_full", "c3": "c3_full", "ref_default": "config_default", "ref_stats114": "stats114"}
     path = Path(__file__).resolve().parent / "tests" / "golden" / "glsl" / "canonical.json"
     if (frame is None and host is None) or config not in cases or not path.exists():
         return None
@@ -854,6 +859,9 @@ def trace_kernel_names(cfg, info, maxd, ns, pixels, split_ok=True):
     options: tile pairs on tiles above 2^21 pixels, split walks of the heaviest camera rays at or
     below it, 1 sample; split_ok False: the caller turned the split walks off, tile pairs)."""
     deep = info["tree_depth"] > 8
+    if not (maxd == 1 and ns == 1) and info["n_nodes"] <= PIXEL_PATHS_AUTO_NODES:
+        return ["ort_pixel_paths<0, %s> (whole-pixel paths: every sample and bounce of the frame in one launch)"
+                % str(deep).lower()]
     pairs = pixels > SPLIT_AUTO_PIXELS or not split_ok
     tile = ("ort_trace_pair%s<false, %d> (two tiles per workgroup: camera rays + walk + %s)" if pairs else
             "ort_trace_compact%s<false, true, %d> (camera rays + walk + %s)")

@@ -88,8 +88,11 @@ def test_sample_rows_spans_the_frame(height):
 def test_trace_kernel_names_follow_the_tile_rules(pixels, split_ok, pairs, split):
     """The roofline's kernel list names what render_impl launches by default (tile pairs above
     2^21 px or with split walks off, split walks at or below it)."""
-    names = bench.trace_kernel_names("c3", {"tree_depth": 8}, 1, 1, pixels, split_ok=split_ok)
+    names = bench.trace_kernel_names("c3", {"tree_depth": 8, "n_nodes": 10_953_681}, 1, 1, pixels, split_ok=split_ok)
     assert names[0].startswith("ort_trace_pair<" if pairs else "ort_trace_compact<")
     assert any(n.startswith("ort_trace_split<false, 1>") for n in names) == split
-    deep = bench.trace_kernel_names("c5", {"tree_depth": 10}, 4, 1, 7680 * 4320)
+    deep = bench.trace_kernel_names("c5", {"tree_depth": 10, "n_nodes": 239_220_401}, 4, 1, 7680 * 4320)
     assert deep[0].startswith("ort_trace_pair_deep<false, 2>") and deep[-1].startswith("ort_trace_persistent<false, true>")
+    # the reference's default config (a 585-node tree, 16 x 8): whole-pixel paths, one kernel
+    small = bench.trace_kernel_names("ref_default", {"tree_depth": 3, "n_nodes": 585}, 8, 16, 800 * 600)
+    assert small == [small[0]] and small[0].startswith("ort_pixel_paths<0, false>")
