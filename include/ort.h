@@ -169,6 +169,9 @@ typedef struct ort_scene_info {
                                       (the small scenes of the reference's sweeps, where launches and sorts
                                       dominate); 0 off; 1 on wherever it applies (compact layout or brute
                                       force, maxDepth >= 1, not 1 sample x 1 bounce).  Same pixels */
+#define ORT_OPT_PIXEL_LDS_SCENE 21 /* 1 (default): whole-pixel paths on scenes whose node records and leaf
+                                      spheres fit 32 KB (depth <= 8) copy them into each workgroup's LDS and
+                                      walk them there; 0: from global memory.  Same pixels */
 /* Retired option codes, reserved (ORT_ERR_UNSUPPORTED): options that lost to the defaults in
  * A/B and were removed -- 5 the wave-level packet walk (1.2-1.35x slower),
  * 7 the wave-level block queue (1/8 band 0.83 vs 0.61 ms), 17 longest-first workgroups

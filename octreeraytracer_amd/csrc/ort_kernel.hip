@@ -113,6 +113,9 @@ struct PipeArgs {
     int* hsync_next;  // the other pair: ort_trace_split zeroes it for the next frame's scan
     int hcap;
     int split_level;
+    // ort_pixel_paths with an LDS-resident scene: byte offset of nk[] in the dynamic LDS (leaf
+    // spheres at lds_sph_off), their sizes in 16-byte chunks
+    int lds_nk_off, lds_sph_off, lds_nk_n16, lds_sph_n16;
 #if ORT_ANALYSIS
     ulonglong4* wclock;  // analysis builds only (ORT_PERSIST_CLOCK, ort_debug_wave_clock): per wave a timeline record
     int wclock_n;
@@ -1354,18 +1357,20 @@ __global__ void __launch_bounds__(kBlock) ort_finalize_kernel(PipeArgs A) {
 // exact walk inline for the rays the fast walk cannot take; MODE 2: brute force.
 // The grid's work cursor and done count (A.sync[1], [2]) start at zero (the counter set of the
 // launch) and the last workgroup to finish resets them.
-template <int MODE, bool DEEP>
-__device__ __forceinline__ bool pixel_trace(const PipeArgs& A, LdsView& L, const ort::Ray& r, float& t, int& entry) {
+template <int MODE, bool DEEP, bool LDS>
+__device__ __forceinline__ bool pixel_trace(const PipeArgs& A, const ort::KScene& S, LdsView& L, const ort::Ray& r,
+                                            float& t, int& entry) {
     ort::Counters cnt;  // (not counted: counting renders take the pipeline)
     entry = -1;
     t = 0.0f;
-    if (MODE == 2) return ort::traverse_brute<false>(A.S, r, 0.001f, ORT_MAXFLOAT, entry, t, cnt);
+    if (MODE == 2) return ort::traverse_brute<false>(S, r, 0.001f, ORT_MAXFLOAT, entry, t, cnt);
     ort::V3 inv = ort::mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
-    if (!A.exact_only && ort::fast_prepare(A.S, r, inv)) {
-        using Masks = typename std::conditional<DEEP, ort::Masks96, ort::Masks64Plain>::type;
-        return ort::traverse_fast_t<false, Masks>(A.S, L.planes, L.lut, r, inv, 0.001f, ORT_MAXFLOAT, entry, t, L.fr, cnt);
+    if (!A.exact_only && ort::fast_prepare(S, r, inv)) {
+        using Masks = typename std::conditional<DEEP, ort::Masks96,
+                                                typename std::conditional<LDS, ort::Masks64PlainLds, ort::Masks64Plain>::type>::type;
+        return ort::traverse_fast_t<false, Masks>(S, L.planes, L.lut, r, inv, 0.001f, ORT_MAXFLOAT, entry, t, L.fr, cnt);
     }
-    return ort::traverse_compact<false>(A.S, L.planes, r, 0.001f, ORT_MAXFLOAT, entry, t, L.fr, cnt);
+    return ort::traverse_compact<false>(S, L.planes, r, 0.001f, ORT_MAXFLOAT, entry, t, L.fr, cnt);
 }
 
 #ifndef ORT_PIXEL_CHUNK
@@ -1375,11 +1380,25 @@ __device__ __forceinline__ bool pixel_trace(const PipeArgs& A, LdsView& L, const
 #define ORT_PIXEL_WAVES 4
 #endif
 
-template <int MODE, bool DEEP>
+// LDS: small scenes (depth <= 8) walk the workgroup's copies of nk[] and leaf_sph[] in LDS
+// (ds_read, ~50 cycles) instead of global memory: the kernel waits on memory for most of its
+// cycles (SQ_WAIT_ANY 0.64 at config.h's default scene, profiles/r06/), and a walk is a chain
+// of dependent record loads.
+template <int MODE, bool DEEP, bool LDS>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ORT_PIXEL_WAVES)))
 ort_pixel_paths(PipeArgs A) {
     extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];  // plane tables: 1 KiB-aligned
     LdsView L{};
+    ort::KScene S = A.S;
+    if (LDS) {  // before setup_lds's barrier
+        uint4* dn = reinterpret_cast<uint4*>(smem + A.lds_nk_off);
+        uint4* ds = reinterpret_cast<uint4*>(smem + A.lds_sph_off);
+        const uint4* sl = reinterpret_cast<const uint4*>(A.S.leaf_sph);
+        for (int i = threadIdx.x; i < A.lds_nk_n16; i += kBlock) dn[i] = A.S.nk[i];
+        for (int i = threadIdx.x; i < A.lds_sph_n16; i += kBlock) ds[i] = sl[i];
+        S.lds_nk = (uint32_t)(size_t)(const __attribute__((address_space(3))) unsigned char*)(smem + A.lds_nk_off);
+        S.lds_sph = (uint32_t)(size_t)(const __attribute__((address_space(3))) unsigned char*)(smem + A.lds_sph_off);
+    }
     if (MODE == 0) L = setup_lds<true>(smem, A.S);
     const int lane = threadIdx.x & 63;
     const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -1443,7 +1462,7 @@ ort_pixel_paths(PipeArgs A) {
         if (k >= 0) {  // one bounce of the lane's current path (radiance(), glsl:604-627)
             float t;
             int entry;
-            const bool hit = pixel_trace<MODE, DEEP>(A, L, ray, t, entry);
+            const bool hit = pixel_trace<MODE, DEEP, LDS>(A, S, L, ray, t, entry);
             ort::HitRec h;
             if (hit) h = ort::hit_record<MODE>(A.S, ray, t, entry);
             bool ended = ort::shade_bounce(hit, h, ray, c, importance, st);
@@ -1518,6 +1537,7 @@ struct ort_ctx {
     int force_layout = -1;
     int exact_only = 0;
     int pixel_paths = -1;  // ORT_OPT_PIXEL_PATHS: -1 auto (use_pixel_paths), 0 off, 1 on where it applies
+    int pixel_lds_scene = 1;  // ORT_OPT_PIXEL_LDS_SCENE: small scenes in LDS for whole-pixel paths
     int refill = 16;  // ORT_OPT_REFILL: C5 (64-item chunks) 16 > 12 (-0.6 %) > 8 (-1.2 %); tools/ab_stream.py
     int persistent = 2;  // ORT_OPT_PERSISTENT: 0 off, 2 bounce >= 1 traces (default)
 #if ORT_ANALYSIS
@@ -2001,13 +2021,17 @@ int persistent_blocks(int device, bool count, bool deep, int depth, size_t lds, 
 // kPixelPathsAutoNodes nodes -- small scenes, where the pipeline's per-bounce launches and
 // sorts cost more than its coherence gains (the reference's own sweeps).
 constexpr long long kPixelPathsAutoNodes = 1ll << 21;
+#ifndef ORT_PIXEL_LDS_SCENE_BYTES
+#define ORT_PIXEL_LDS_SCENE_BYTES 32768
+#endif
+constexpr int kPixelLdsSceneBytes = ORT_PIXEL_LDS_SCENE_BYTES;  // LDS-resident scene budget (ort_pixel_paths)
 bool use_pixel_paths(const ort_ctx* ctx, int mode, int ns, int maxd);
 
-template <int MODE, bool DEEP>
+template <int MODE, bool DEEP, bool LDS = false>
 int pixel_paths_blocks(int device, size_t lds, long long needed) {
     int per_cu = 0, cus = 0;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ort_pixel_paths<MODE, DEEP>, kBlock, lds);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ort_pixel_paths<MODE, DEEP, LDS>, kBlock, lds);
     const long long b = (long long)std::max(per_cu, 1) * std::max(cus, 1);
     return (int)std::max(1LL, std::min(b, needed));
 }
@@ -2053,10 +2077,23 @@ int render_pixel_paths(ort_ctx* ctx, const ort_params* p, const ort_tile* t, int
     ctx->sync_ok = false;
     a.sync = (int*)ctx->defer_count.p + 16 * ctx->sync_set;
     const bool deep = ctx->depth > 8;
-    const size_t lds = mode == 0 ? lds_bytes(0, ctx->depth, true) : 0;
+    size_t lds = mode == 0 ? lds_bytes(0, ctx->depth, true) : 0;
+    // an LDS-resident scene: node records + kid entries (16 B per node) and the leaf spheres
+    // (16 B per entry: objectIndices, then the per-sphere tail), when they fit the budget
+    const size_t nk_b = 16 * (size_t)ctx->n_nodes, sph_b = 16 * ((size_t)ctx->n_indices + (size_t)ctx->n_spheres);
+    const bool lds_scene = mode == 0 && !deep && a.S.nk && ctx->pixel_lds_scene &&
+                           nk_b + sph_b <= (size_t)kPixelLdsSceneBytes;
+    if (lds_scene) {
+        a.lds_nk_off = (int)align16(lds);
+        a.lds_sph_off = (int)(a.lds_nk_off + nk_b);
+        a.lds_nk_n16 = (int)(nk_b / 16);
+        a.lds_sph_n16 = (int)(sph_b / 16);
+        lds = (size_t)a.lds_sph_off + sph_b;
+    }
     const int g = mode == 2 ? pixel_paths_blocks<2, false>(ctx->device, lds, blocks)
                             : (deep ? pixel_paths_blocks<0, true>(ctx->device, lds, blocks)
-                                    : pixel_paths_blocks<0, false>(ctx->device, lds, blocks));
+                                    : (lds_scene ? pixel_paths_blocks<0, false, true>(ctx->device, lds, blocks)
+                                                 : pixel_paths_blocks<0, false>(ctx->device, lds, blocks)));
     const int fslot = (int)(ctx->frames % ort_ctx::kRing);
     ctx->tseg[fslot] = 0;
     const bool timed = !((ctx->debug_flags & 1) || !ctx->launch_times);
@@ -2066,9 +2103,10 @@ int render_pixel_paths(ort_ctx* ctx, const ort_params* p, const ort_tile* t, int
     }
     ctx->ev0_last = timed ? ctx->tr0[fslot][0] : ctx->ev0;  // the frame's start is its trace launch's
     HIPCHK(ctx, hipEventRecord(ctx->ev0_last, s));
-    if (mode == 2) hipLaunchKernelGGL((ort_pixel_paths<2, false>), dim3(g), dim3(kBlock), 0, s, a);
-    else if (deep) hipLaunchKernelGGL((ort_pixel_paths<0, true>), dim3(g), dim3(kBlock), lds, s, a);
-    else hipLaunchKernelGGL((ort_pixel_paths<0, false>), dim3(g), dim3(kBlock), lds, s, a);
+    if (mode == 2) hipLaunchKernelGGL((ort_pixel_paths<2, false, false>), dim3(g), dim3(kBlock), 0, s, a);
+    else if (deep) hipLaunchKernelGGL((ort_pixel_paths<0, true, false>), dim3(g), dim3(kBlock), lds, s, a);
+    else if (lds_scene) hipLaunchKernelGGL((ort_pixel_paths<0, false, true>), dim3(g), dim3(kBlock), lds, s, a);
+    else hipLaunchKernelGGL((ort_pixel_paths<0, false, false>), dim3(g), dim3(kBlock), lds, s, a);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(ctx, e, "ort_pixel_paths launch");
     if (timed) {
@@ -2688,6 +2726,11 @@ int ort_set_option(ort_ctx* ctx, int option, int value) {
     if (option == ORT_OPT_PIXEL_PATHS) {
         if (value < -1 || value > 1) return fail(ctx, ORT_ERR_INVALID_ARG, "ORT_OPT_PIXEL_PATHS: -1 (auto), 0 or 1");
         ctx->pixel_paths = value;
+        return ORT_OK;
+    }
+    if (option == ORT_OPT_PIXEL_LDS_SCENE) {
+        if (value < 0 || value > 1) return fail(ctx, ORT_ERR_INVALID_ARG, "ORT_OPT_PIXEL_LDS_SCENE: 0 or 1");
+        ctx->pixel_lds_scene = value;
         return ORT_OK;
     }
     if (option == ORT_OPT_LAUNCH_TIMES) {

@@ -108,6 +108,9 @@ struct KScene {
     const uint4* nk;         // per node: {record, kid entry} interleaved (one 16-byte load), or null
     uint32_t nk_bytes;
     uint32_t tail_base;      // = n_indices: a one-sphere leaf's objectsOffset is tail_base + sphere
+    // walks with Masks::kLdsScene (ort_pixel_paths on small scenes): LDS byte addresses of
+    // workgroup copies of nk[] and leaf_sph[] (set inside the kernel)
+    uint32_t lds_nk, lds_sph;
     // explicit (reference) layout
     const float4* nodeA;     // min.xyz, int bits of childrenOffset (binding 3)
     const float4* nodeB;     // max.xyz, int bits of objectsOffset  (binding 4)
@@ -696,6 +699,7 @@ ORT_FN float plane_at(const float* base, int idx) { return base[idx]; }
 
 // Rank-reversed level masks (see above).  pop() returns hb = 8L + 7 - rank.
 struct Masks64 {  // levels 0..7: trees of depth <= 8
+    static constexpr bool kLdsScene = false;  // records / leaf spheres from global memory
     // test the leaf children of a LEAFKIDS node inline (fast_step); pays for its registers on
     // depth <= 8 trees (all leaves at the bottom level with maxSpheresPerNode 0), not deeper
     static constexpr bool kInlineLeaves = true;
@@ -742,6 +746,7 @@ struct Masks64 {  // levels 0..7: trees of depth <= 8
     }
 };
 struct Masks96 {  // levels 0..9 (ORT_COMPACT_MAX_DEPTH 10)
+    static constexpr bool kLdsScene = false;
     // a leaf-children node's leaves tested inline (as in the depth <= 8 walk): C5 camera rays
     // 14.11 -> 14.86 ms (the rejected-sphere skip already drops most of them): off
 #ifndef ORT_INLINE_LEAVES_DEEP
@@ -914,6 +919,11 @@ struct Masks64Plain : Masks64 {
     static constexpr bool kPreMid = false;
     static constexpr bool kKidSkip = true;
 };
+// ... reading node records and leaf spheres from the workgroup's LDS copies of nk[] / leaf_sph[]
+// (KScene::lds_nk / lds_sph): whole-pixel paths on scenes that fit (ort_pixel_paths)
+struct Masks64PlainLds : Masks64Plain {
+    static constexpr bool kLdsScene = true;
+};
 
 // The split walk's level masks (traverse_split): no leaf children tested inline (the lanes
 // must pop every level-`level` node themselves, to count it) and no rejected-sphere skip (each
@@ -934,8 +944,19 @@ struct Masks96Split : Masks96 {
 #ifndef ORT_NODE_KID
 #define ORT_NODE_KID 1
 #endif
+#if defined(__HIP_DEVICE_COMPILE__)
+ORT_FN uint4 lds_u4(uint32_t a) { return *(const __attribute__((address_space(3))) uint4*)(size_t)a; }
+#endif
 template <class Masks>
 ORT_FN void fetch_rec(const KScene& S, int i, bool kid, FastStateT<Masks>& st) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (Masks::kLdsScene) {  // the workgroup's copy of nk[] (ort_pixel_paths)
+        const uint4 v = lds_u4(S.lds_nk + 16u * (uint32_t)i);
+        st.rec = make_uint2(v.x, v.y);
+        st.kd = make_uint2(v.z, v.w);
+        return;
+    }
+#endif
     if (ORT_NODE_KID && Masks::kKidSkip && kid && S.nk) {
         const uint4 v = fetch_nk(S, i);
         st.rec = make_uint2(v.x, v.y);
@@ -1033,7 +1054,17 @@ ORT_FN bool leaf_tests(const KScene& S, FastStateT<Masks>& st, int off, int n, f
     const Ray r = st.ray();
     const float a = dot(r.d, r.d);  // as fast_begin computed it
     for (int i = 0; i < n; ++i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+        float4 sp;
+        if constexpr (Masks::kLdsScene) {
+            const uint4 v = lds_u4(S.lds_sph + 16u * (uint32_t)(off + i));
+            sp = make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+        } else {
+            sp = fetch_sphere(S, off + i);
+        }
+#else
         const float4 sp = fetch_sphere(S, off + i);
+#endif
         if (COUNT) cnt.v[2] += 1;
         float t;
         if (sphere_hit_fast(r, a, st.ya, sp, ntmin, st.closest, t)) {

@@ -124,6 +124,10 @@ class Renderer:
         launch wherever they apply (same pixels)."""
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_PIXEL_PATHS, int(mode)))
 
+    def set_pixel_lds_scene(self, on: int):
+        """ORT_OPT_PIXEL_LDS_SCENE: 1 (default) small scenes walked from LDS copies in whole-pixel paths."""
+        self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_PIXEL_LDS_SCENE, int(on)))
+
     def set_xcd_swizzle(self, mode: int):
         """Workgroup -> tile order (ORT_OPT_XCD_SWIZZLE): 2 runs of raster tiles per XCD, 1
         128x128-pixel super-tiles per XCD, 0 raster, -1 (default) raster on small one-tile-workgroup

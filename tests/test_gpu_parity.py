@@ -478,3 +478,22 @@ def test_pixel_paths_option_and_auto(ort, oracle, scene_c1, scene_c3):
         got = r.render(pb)
         assert r.frame_trace_times_ms(1)[0][1] > 1  # auto: the pipeline on a large tree
         assert_same(got, oracle.render(s3, t3, pb), "C3 tree, auto")
+
+
+@pytest.mark.parametrize("n,depth,mspn", [(100, 3, 0), (60, 5, 1), (10, 1, 1)])
+def test_pixel_paths_lds_scene(ort, oracle, n, depth, mspn):
+    """Whole-pixel paths on scenes small enough for the LDS-resident copy (ORT_OPT_PIXEL_LDS_SCENE):
+    config.h's default scene, a depth-5 M=1 tree (the rejected-sphere skip from the LDS kid
+    entries) and runner.py's 10-sphere tree -- LDS on and off, against the oracle."""
+    s = ort.random_spheres(n, 42)
+    t = ort.build_octree(s, depth, mspn)
+    assert 16 * (t.n_nodes + t.n_indices + s.n) <= 32768
+    p = ort.FrameParams.default_camera(200, 150, num_samples=4, max_depth=8)
+    ref = oracle.render(s, t, p)
+    with ort.Renderer(0) as r:
+        r.upload(s, t)
+        for on in (1, 0):
+            r.set_pixel_lds_scene(on)
+            assert_same(r.render(p), ref, f"n{n} d{depth} lds_scene={on}")
+        with pytest.raises(ort.OrtError):
+            r.set_pixel_lds_scene(2)
