@@ -1494,6 +1494,31 @@ ORT_FN bool traverse_brute(const KScene& S, const Ray& r, float t_min, float t_m
     const float a = dot(r.d, r.d);
     bool hit = false;
     float closest = t_max;
+#ifndef ORT_BRUTE_FAST
+#define ORT_BRUTE_FAST 1
+#endif
+#if defined(__HIP_DEVICE_COMPILE__) && ORT_BRUTE_FAST
+    // the fast walk's sphere test (per-ray correctly rounded 1/a, Markstein quotient, guarded
+    // sqrt: the same roots) whenever its preconditions hold for the wave, and the spheres read
+    // with scalar loads -- every lane tests sphere i at once, so the address is wave-uniform
+    if (!COUNT && !any_lane(!(t_min == kFastTMin && a_in_qdiv_range(a)))) {
+        const float ya = 1.0f / a;
+        typedef __attribute__((address_space(4))) const float4 ConstF4;
+        ConstF4* sph = (ConstF4*)S.sph_cr;
+        for (int i = 0; i < S.n_spheres; ++i) {
+            const float4 s4 = sph[i];
+            float t;
+            // (radius^2 as sphere_hit_t computes it: one rounded product)
+            if (sphere_hit_fast(r, a, ya, make_float4(s4.x, s4.y, s4.z, s4.w * s4.w), t_min, closest, t)) {
+                hit = true;
+                closest = t;
+                hitSphere = i;
+            }
+        }
+        hitT = closest;
+        return hit;
+    }
+#endif
     for (int i = 0; i < S.n_spheres; ++i) {
         float t;
         if (COUNT) cnt.v[2] += 1;
