@@ -54,7 +54,7 @@ CONFIGS = {
     "ref_default": (800, 600, 100, 3, 0, 16, 8),
     "ref_stats114": (1920, 1080, 1000, 5, 1, 16, 8),
 }
-PIXEL_PATHS_AUTO_NODES = 1 << 21  # ort_kernel.hip kPixelPathsAutoNodes
+PIXEL_PATHS_AUTO_NODES = (1 << 19, 1 << 23)  # ort_kernel.hip kPixelPathsAutoNodes(Multi): 1 sample, several
 
 
 def reference_frame_check(config: str, frame, host=None):
@@ -871,7 +871,7 @@ def trace_kernel_names(cfg, info, maxd, ns, pixels, split_ok=True):
     options: tile pairs on tiles above 2^21 pixels, split walks of the heaviest camera rays at or
     below it, 1 sample; split_ok False: the caller turned the split walks off, tile pairs)."""
     deep = info["tree_depth"] > 8
-    if not (maxd == 1 and ns == 1) and info["n_nodes"] <= PIXEL_PATHS_AUTO_NODES:
+    if not (maxd == 1 and ns == 1) and info["n_nodes"] <= PIXEL_PATHS_AUTO_NODES[ns > 1]:
         return ["ort_pixel_paths<0, %s> (whole-pixel paths: every sample and bounce of the frame in one launch)"
                 % str(deep).lower()]
     pairs = pixels > SPLIT_AUTO_PIXELS or not split_ok

@@ -2017,10 +2017,12 @@ int persistent_blocks(int device, bool count, bool deep, int depth, size_t lds, 
 }
 
 // Whole-pixel paths (ort_pixel_paths): the frame in one launch.  Auto (ORT_OPT_PIXEL_PATHS -1):
-// frames of more than one traversal per pixel on brute force and on trees of at most
-// kPixelPathsAutoNodes nodes -- small scenes, where the pipeline's per-bounce launches and
-// sorts cost more than its coherence gains (the reference's own sweeps).
-constexpr long long kPixelPathsAutoNodes = 1ll << 21;
+// frames of more than one traversal per pixel on brute force, on trees of at most
+// kPixelPathsAutoNodesMulti nodes with several samples and kPixelPathsAutoNodes with one --
+// where the pipeline's per-bounce launches and sorts cost more than its coherence gains (the
+// reference's own sweeps and the threshold A/B).
+constexpr long long kPixelPathsAutoNodes = 1ll << 19;       // 1 sample per pixel
+constexpr long long kPixelPathsAutoNodesMulti = 1ll << 23;  // 2 or more
 #ifndef ORT_PIXEL_LDS_SCENE_BYTES
 #define ORT_PIXEL_LDS_SCENE_BYTES 32768
 #endif
@@ -2050,7 +2052,12 @@ unsigned long long frame_sig(const ort_ctx* ctx, const ort_params* p, const ort_
 bool use_pixel_paths(const ort_ctx* ctx, int mode, int ns, int maxd) {
     if (mode == 1 || maxd < 1 || (ns == 1 && maxd == 1) || ctx->pixel_paths == 0) return false;
     if (ctx->pixel_paths > 0) return true;
-    return mode == 2 || ctx->n_nodes <= kPixelPathsAutoNodes;
+    // several samples: the pipeline pays its launches and sorts ns x maxd times, whole-pixel
+    // paths win up to trees of 8.3 M nodes (1080p, 4 x 8: 1.65x at 209 k nodes, 1.40x at 1.5 M,
+    // 1.17x at 8.3 M; the C3 tree of 11 M nodes at 3 x 5: 0.87x); one sample: the pipeline's
+    // sorted bounce rays win from about 2 M nodes on (4K, 1 x 4: 0.54x at 1.9 M and at 11 M
+    // nodes, 1.05x at 209 k) -- profiles/r06/pixel_paths_threshold.log
+    return mode == 2 || ctx->n_nodes <= (ns > 1 ? kPixelPathsAutoNodesMulti : kPixelPathsAutoNodes);
 }
 
 // The frame as one ort_pixel_paths launch (use_pixel_paths); dout: the frame on the device.

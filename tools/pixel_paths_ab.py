@@ -30,6 +30,12 @@ CASES = {
     "c2_spp1_d4": (10000, 6, 0, 1920, 1080, 1, 4, 1),
     "c3tree_spp1_d4": (100000, 8, 0, 3840, 2160, 1, 4, 1),
     "c3tree_spp3_d5": (100000, 8, 0, 1920, 1080, 3, 5, 1),
+    # trees between C2's (209 k nodes) and C3's (11 M): where the auto rule's 2^21-node line sits
+    "mid_30k_d7_spp4_d8": (30000, 7, 0, 1920, 1080, 4, 8, 1),     # 1.48 M nodes
+    "mid_100k_d7_spp4_d8": (100000, 7, 0, 1920, 1080, 4, 8, 1),   # 1.94 M nodes
+    "mid_20k_d8_spp4_d8": (20000, 8, 0, 1920, 1080, 4, 8, 1),     # 5.07 M nodes
+    "mid_50k_d8_spp4_d8": (50000, 8, 0, 1920, 1080, 4, 8, 1),     # 8.26 M nodes
+    "mid_100k_d7_spp1_d4": (100000, 7, 0, 3840, 2160, 1, 4, 1),   # 1.94 M nodes, C3's frame shape
 }
 
 
