@@ -173,6 +173,12 @@ typedef struct ort_scene_info {
 #define ORT_OPT_PIXEL_LDS_SCENE 21 /* 1 (default): whole-pixel paths on scenes whose node records and leaf
                                       spheres fit 32 KB (depth <= 8) copy them into each workgroup's LDS and
                                       walk them there; 0: from global memory.  Same pixels */
+#define ORT_OPT_PIXEL_HEAVY_FIRST 22 /* whole-pixel paths: the frame's 8x8 blocks taken in the order of the
+                                      previous frame's cost (bounces per sample, 32 classes, heaviest first)
+                                      when that frame had the same shape and scene, so the longest pixel
+                                      chains start first and do not trail the frame; tile order otherwise.
+                                      -1 (default): on for frames of 2 or more samples; 0 off; 1 on.  Same
+                                      pixels (the order changes which lane traces a pixel, not its chain) */
 /* Retired option codes, reserved (ORT_ERR_UNSUPPORTED): options that lost to the defaults in
  * A/B and were removed -- 5 the wave-level packet walk (1.2-1.35x slower),
  * 7 the wave-level block queue (1/8 band 0.83 vs 0.61 ms), 17 longest-first workgroups

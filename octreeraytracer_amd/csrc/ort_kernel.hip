@@ -116,6 +116,16 @@ struct PipeArgs {
     // ort_pixel_paths with an LDS-resident scene: byte offset of nk[] in the dynamic LDS (leaf
     // spheres at lds_sph_off), their sizes in 16-byte chunks
     int lds_nk_off, lds_sph_off, lds_nk_n16, lds_sph_n16;
+    // ort_pixel_paths, heavy blocks first: the 8x8 blocks in kPixelClasses cost classes (last
+    // frame of this shape, read: pl_r / pl_rcnt, or null = tile order) and this frame's classes
+    // for the next (pl_w / pl_wcnt; pl_cost: per block {bounces, slots done}); pl_stride blocks
+    // per class segment
+    const int* pl_r;
+    int* pl_rcnt;
+    int* pl_w;
+    int* pl_wcnt;
+    unsigned long long* pl_cost;
+    int pl_stride;
 #if ORT_ANALYSIS
     ulonglong4* wclock;  // analysis builds only (ORT_PERSIST_CLOCK, ort_debug_wave_clock): per wave a timeline record
     int wclock_n;
@@ -1373,9 +1383,27 @@ __device__ __forceinline__ bool pixel_trace(const PipeArgs& A, const ort::KScene
     return ort::traverse_compact<false>(S, L.planes, r, 0.001f, ORT_MAXFLOAT, entry, t, L.fr, cnt);
 }
 
-#ifndef ORT_PIXEL_CHUNK
-#define ORT_PIXEL_CHUNK 64  // pixels a wave takes from the cursor at a time (one 8x8 block)
+#ifndef ORT_PIXEL_LPT
+#define ORT_PIXEL_LPT 1  // whole-pixel paths take last frame's heaviest 8x8 blocks first
 #endif
+constexpr int kPixelClasses = 32;  // cost classes of a block: mean bounces per sample in quarters
+// Accounts one slot of a block (a finished pixel and the bounces it traced, or a slot that is no
+// pixel): the block's last slot files the block under its cost class for the next frame and
+// clears its accumulator (cost in the high word, slots in the low word).
+__device__ __forceinline__ void block_account(const PipeArgs& A, int slot, int bounces) {
+    unsigned long long* acc = A.pl_cost + (slot >> 6);
+    const unsigned long long add = ((unsigned long long)min(bounces, 1 << 24) << 32) | 1ull;
+    const unsigned long long old = atomicAdd(acc, add);
+    if ((unsigned)(old & 0xffffffffu) == 63u) {
+        const unsigned long long cost = (old >> 32) + (unsigned long long)min(bounces, 1 << 24);
+        *acc = 0;
+        const unsigned long long quarters = cost / (16ull * (unsigned long long)A.pp.ns);
+        const int q = kPixelClasses - 1 - (int)min(quarters, (unsigned long long)(kPixelClasses - 1));
+        const int pos = atomicAdd(A.pl_wcnt + q, 1);
+        A.pl_w[(size_t)q * A.pl_stride + pos] = slot >> 6;
+    }
+}
+
 #ifndef ORT_PIXEL_WAVES
 #define ORT_PIXEL_WAVES 4
 #endif
@@ -1403,7 +1431,22 @@ ort_pixel_paths(PipeArgs A) {
     const int lane = threadIdx.x & 63;
     const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const int maxd = A.pp.maxDepth, ns = A.pp.ns;
+    // the work items: 8x8 blocks, last frame's heaviest class first (a longest-first list
+    // schedule: a frame ends with its longest pixels -- a pixel's samples run one after another --
+    // and a block keeps its pixels' rays coherent), else in tile order.  Lane q < 32 holds the
+    // inclusive prefix of the class counts.
+    const int n_blocks = A.total >> 6;
+    int cls_end = 0;
+    if (ORT_PIXEL_LPT && A.pl_r) {
+        cls_end = lane < kPixelClasses ? A.pl_rcnt[lane] : 0;
+        for (int d = 1; d < kPixelClasses; d <<= 1) {
+            const int v = __shfl_up(cls_end, d);
+            if (lane >= d) cls_end += v;
+        }
+    }
+    const bool listed = ORT_PIXEL_LPT && A.pl_r && __shfl(cls_end, kPixelClasses - 1) == n_blocks;
     int k = -1;              // the lane's path slot (pixel), -1 idle
+    int nb = 0;              // bounces traced for the lane's pixel so far (its cost class)
     int px = 0, py = 0, s = 0, b = 0;
     ort::Ray ray;
     ray.o = ray.d = ort::mk(0.0f, 0.0f, 0.0f);
@@ -1411,18 +1454,28 @@ ort_pixel_paths(PipeArgs A) {
     float importance = 1.0f;
     ort_rng st;
     st.x = st.y = 0.0f;
-    int next = 0, end = 0;   // wave-uniform: the rest of the wave's chunk
+    int next = 0, end = 0;   // wave-uniform: the rest of the wave's block
     bool drained = false;    // wave-uniform: the cursor passed the last slot
     for (;;) {
         const unsigned long long idle = __ballot(k < 0);
         if (idle && !drained) {  // refill: idle lanes take the chunk's next pixels
-            if (next == end) {
-                int base = 0;
-                if (lane == 0) base = atomicAdd(A.sync + 1, ORT_PIXEL_CHUNK);
-                base = __shfl(base, 0);
-                if (base >= A.total) drained = true;
-                next = base;
-                end = min(base + ORT_PIXEL_CHUNK, A.total);
+            if (next == end) {  // the next block
+                int j = 0;
+                if (lane == 0) j = atomicAdd(A.sync + 1, 1);
+                j = __shfl(j, 0);
+                if (j >= n_blocks) {
+                    drained = true;
+                } else {
+                    int blk = j;
+                    if (listed) {  // item j of the class lists: class q = the first with j < its prefix end
+                        const unsigned long long in = __ballot(lane < kPixelClasses && j < cls_end);
+                        const int q = __builtin_ctzll(in);
+                        const int before = q ? __shfl(cls_end, q - 1) : 0;
+                        blk = A.pl_r[(size_t)q * A.pl_stride + (j - before)];
+                    }
+                    next = blk << 6;
+                    end = next + 64;
+                }
             }
             if (!drained) {
                 const int n_idle = __popcll(idle);
@@ -1431,11 +1484,13 @@ ort_pixel_paths(PipeArgs A) {
                     const int rank = __popcll(idle & below);
                     if (rank < take) {
                         const int cand = next + rank;
+                        bool pixel = false;
                         int cx, cy;
                         if (slot_coords(A, cand, cx, cy)) {
                             const int y = tile_row_to_y(A.tm, cy);
                             if (y < A.pp.H) {  // a pixel: sample 0's camera ray
                                 k = cand;
+                                nb = 0;
                                 px = A.tm.x0 + cx;
                                 py = y;
                                 ort::pixel_rng_init(A.pp, px, py, st);
@@ -1445,11 +1500,13 @@ ort_pixel_paths(PipeArgs A) {
                                 c = ort::mk(1.0f, 1.0f, 1.0f);
                                 importance = 1.0f;
                                 ray = ort::primary_ray(A.pp, px, py, 0, st);
+                                pixel = true;
                             } else {  // a band's padding row (past the frame): zeros, as the pipeline writes
                                 float* o = A.out + 3 * ((size_t)cy * A.tm.tw + cx);
                                 o[0] = 0.0f; o[1] = 0.0f; o[2] = 0.0f;
                             }
                         }
+                        if (ORT_PIXEL_LPT && A.pl_w && !pixel) block_account(A, cand, 0);
                     }
                 }
                 next += take;
@@ -1467,6 +1524,7 @@ ort_pixel_paths(PipeArgs A) {
             if (hit) h = ort::hit_record<MODE>(A.S, ray, t, entry);
             bool ended = ort::shade_bounce(hit, h, ray, c, importance, st);
             ++b;
+            ++nb;
             ended = ended || b >= maxd || importance < 0.01f;
             if (ended) {  // col += radiance(r) (glsl:655); the pixel's next sample, or its final colour
                 col = ort::add(col, c);
@@ -1481,6 +1539,7 @@ ort_pixel_paths(PipeArgs A) {
                     const ort::V3 v = ort::finish_pixel(col, ns);
                     float* o = A.out + 3 * ((size_t)cy * A.tm.tw + cx);
                     o[0] = v.x; o[1] = v.y; o[2] = v.z;
+                    if (ORT_PIXEL_LPT && A.pl_w) block_account(A, k, nb);  // its block's cost for the next frame
                     k = -1;
                 }
             }
@@ -1493,6 +1552,9 @@ ort_pixel_paths(PipeArgs A) {
         if (atomicAdd(A.sync + 2, 1) == (int)gridDim.x - 1) {
             atomicExch(A.sync + 1, 0);
             atomicExch(A.sync + 2, 0);
+            // the class counts read this frame become the next frame's write counts
+            if (ORT_PIXEL_LPT && A.pl_rcnt)
+                for (int q = 0; q < kPixelClasses; ++q) atomicExch(A.pl_rcnt + q, 0);
         }
     }
 }
@@ -1538,6 +1600,7 @@ struct ort_ctx {
     int exact_only = 0;
     int pixel_paths = -1;  // ORT_OPT_PIXEL_PATHS: -1 auto (use_pixel_paths), 0 off, 1 on where it applies
     int pixel_lds_scene = 1;  // ORT_OPT_PIXEL_LDS_SCENE: small scenes in LDS for whole-pixel paths
+    int pixel_heavy_first = -1;  // ORT_OPT_PIXEL_HEAVY_FIRST: -1 auto (2+ samples), 0 off, 1 on
     int refill = 16;  // ORT_OPT_REFILL: C5 (64-item chunks) 16 > 12 (-0.6 %) > 8 (-1.2 %); tools/ab_stream.py
     int persistent = 2;  // ORT_OPT_PERSISTENT: 0 off, 2 bounce >= 1 traces (default)
 #if ORT_ANALYSIS
@@ -1572,6 +1635,12 @@ struct ort_ctx {
     // cleared when the frame shape or scene changes (cost_sig)
     int cost_order = 1;
     DevBuf pcost;
+    // whole-pixel paths, heavy blocks first: two {kPixelClasses segments of block lists} buffers
+    // and their counts, the blocks' cost accumulators, the parity of the next frame's write
+    // buffer, and the shape the read buffer's lists belong to (0: none)
+    DevBuf pplist, ppcnt, ppcost;
+    int pp_par = 0;
+    unsigned long long pp_sig = 0;
     unsigned long long cost_sig = 0;
     // ORT_OPT_HEAVY_FIRST: threshold in walk steps (0 off); bcost holds, per bounce >= 1 of the
     // first kCostBounces of a frame, every slot's last walk steps (cleared with cost_sig)
@@ -2080,9 +2149,38 @@ int render_pixel_paths(ort_ctx* ctx, const ort_params* p, const ort_tile* t, int
         HIPCHK(ctx, hipMemsetAsync(ctx->defer_count.p, 0, 128, s));
         ctx->sync_set = 0;
         ctx->pre_ok = false;
+        ctx->pp_sig = 0;  // (the class lists' counts re-zeroed below)
     }
     ctx->sync_ok = false;
     a.sync = (int*)ctx->defer_count.p + 16 * ctx->sync_set;
+    // heavy blocks first (ORT_OPT_PIXEL_HEAVY_FIRST; auto: several samples -- a pixel's chain is
+    // then long enough for the frame's tail to matter, while one-sample frames keep tile order's
+    // locality: 1080p 1 x 4 on 10k spheres 0.89x in heavy-first order, profiles/r06/ab_blk_*)
+    const bool heavy_first = ctx->pixel_heavy_first > 0 || (ctx->pixel_heavy_first < 0 && p->num_samples > 1);
+    if (ORT_PIXEL_LPT && !heavy_first) ctx->pp_sig = 0;
+    if (ORT_PIXEL_LPT && heavy_first) {  // last frame's class lists (same shape) and this frame's
+        const size_t nb = (size_t)blocks * (kBlock / 64), cnt_b = 2 * kPixelClasses * sizeof(int);
+        int rc;
+        if ((rc = ensure(ctx, ctx->pplist, 2 * kPixelClasses * 4 * nb)) || (rc = ensure(ctx, ctx->ppcnt, cnt_b)) ||
+            (rc = ensure(ctx, ctx->ppcost, 8 * nb)))
+            return rc;
+        const unsigned long long sig = frame_sig(ctx, p, t);
+        if (ctx->pp_sig == 0 || ctx->pp_sig != sig) {  // no lists of this shape: zero counts and accumulators
+            HIPCHK(ctx, hipMemsetAsync(ctx->ppcnt.p, 0, cnt_b, s));
+            HIPCHK(ctx, hipMemsetAsync(ctx->ppcost.p, 0, 8 * nb, s));
+        }
+        const int w = ctx->pp_par, r = w ^ 1;
+        int* lists = (int*)ctx->pplist.p;
+        int* cnt = (int*)ctx->ppcnt.p;
+        a.pl_stride = (int)nb;
+        a.pl_w = lists + (size_t)w * kPixelClasses * nb;
+        a.pl_wcnt = cnt + kPixelClasses * w;
+        a.pl_rcnt = cnt + kPixelClasses * r;
+        a.pl_cost = (unsigned long long*)ctx->ppcost.p;
+        a.pl_r = (ctx->pp_sig == sig) ? lists + (size_t)r * kPixelClasses * nb : nullptr;
+        ctx->pp_par = r;
+        ctx->pp_sig = sig;
+    }
     const bool deep = ctx->depth > 8;
     size_t lds = mode == 0 ? lds_bytes(0, ctx->depth, true) : 0;
     // an LDS-resident scene: node records + kid entries (16 B per node) and the leaf spheres
@@ -2655,7 +2753,7 @@ int ort_destroy(ort_ctx* ctx) {
     free_buf(ctx->counters);
     DevBuf* pipe[] = {&ctx->hit, &ctx->defer_list, &ctx->defer_count, &ctx->po, &ctx->pd, &ctx->pc, &ctx->prng, &ctx->pcol,
                       &ctx->qlist, &ctx->qlist2, &ctx->qcount, &ctx->qtemp, &ctx->skeys, &ctx->skeys2, &ctx->svals, &ctx->key_spread,
-                      &ctx->pcost, &ctx->bcost, &ctx->hbits, &ctx->hlist, &ctx->hcnt};
+                      &ctx->pcost, &ctx->bcost, &ctx->hbits, &ctx->hlist, &ctx->hcnt, &ctx->pplist, &ctx->ppcnt, &ctx->ppcost};
     for (DevBuf* b : pipe) free_buf(*b);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
@@ -2733,6 +2831,11 @@ int ort_set_option(ort_ctx* ctx, int option, int value) {
     if (option == ORT_OPT_PIXEL_PATHS) {
         if (value < -1 || value > 1) return fail(ctx, ORT_ERR_INVALID_ARG, "ORT_OPT_PIXEL_PATHS: -1 (auto), 0 or 1");
         ctx->pixel_paths = value;
+        return ORT_OK;
+    }
+    if (option == ORT_OPT_PIXEL_HEAVY_FIRST) {
+        if (value < -1 || value > 1) return fail(ctx, ORT_ERR_INVALID_ARG, "ORT_OPT_PIXEL_HEAVY_FIRST: -1 (auto), 0 or 1");
+        ctx->pixel_heavy_first = value;
         return ORT_OK;
     }
     if (option == ORT_OPT_PIXEL_LDS_SCENE) {

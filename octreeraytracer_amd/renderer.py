@@ -128,6 +128,11 @@ class Renderer:
         """ORT_OPT_PIXEL_LDS_SCENE: 1 (default) small scenes walked from LDS copies in whole-pixel paths."""
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_PIXEL_LDS_SCENE, int(on)))
 
+    def set_pixel_heavy_first(self, mode: int):
+        """ORT_OPT_PIXEL_HEAVY_FIRST: whole-pixel paths take the previous frame's heaviest 8x8
+        blocks first; -1 (default) for frames of 2+ samples, 0 off, 1 on."""
+        self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_PIXEL_HEAVY_FIRST, int(mode)))
+
     def set_xcd_swizzle(self, mode: int):
         """Workgroup -> tile order (ORT_OPT_XCD_SWIZZLE): 2 runs of raster tiles per XCD, 1
         128x128-pixel super-tiles per XCD, 0 raster, -1 (default) raster on small one-tile-workgroup

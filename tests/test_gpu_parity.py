@@ -510,3 +510,32 @@ def test_pixel_paths_lds_scene(ort, oracle, n, depth, mspn):
             assert_same(r.render(p), ref, f"n{n} d{depth} lds_scene={on}")
         with pytest.raises(ort.OrtError):
             r.set_pixel_lds_scene(2)
+
+
+def test_pixel_heavy_first(ort, oracle, scene_c2):
+    """ORT_OPT_PIXEL_HEAVY_FIRST: whole-pixel paths taking the previous frame's heaviest 8x8
+    blocks first.  Runs of frames of one shape (the second and later read the lists the one
+    before wrote), shape changes (lists discarded), an odd frame size (slots past the tile) and a
+    band tile with padding rows (slots past the frame) -- every frame the oracle's, in each mode."""
+    s, t = scene_c2
+    p = ort.FrameParams.default_camera(200, 150, num_samples=4, max_depth=6)
+    p2 = ort.FrameParams.default_camera(136, 100, num_samples=2, max_depth=5)
+    p3 = ort.FrameParams.default_camera(320, 180, num_samples=2, max_depth=4)
+    p1 = ort.FrameParams.default_camera(200, 150, num_samples=1, max_depth=4)
+    band = ort.Tile(0, 320, 150, 64, 16, 64)
+    refs = {"p": oracle.render(s, t, p), "p2": oracle.render(s, t, p2), "p1": oracle.render(s, t, p1),
+            "band": oracle.render(s, t, p3, 0, 150, 320, 64, band_height=16, band_stride=64)}
+    frames = {"p": (p, None), "p2": (p2, None), "p1": (p1, None), "band": (p3, band)}
+    with ort.Renderer(0) as r:
+        for bad in (-2, 2):
+            with pytest.raises(ort.OrtError):
+                r.set_pixel_heavy_first(bad)
+        r.upload(s, t)
+        with pixel_paths(r, 1):
+            for mode in (-1, 1, 0):
+                r.set_pixel_heavy_first(mode)
+                for name in ("p", "p", "p", "p2", "p2", "p", "band", "band", "band", "p1", "p1", "p"):
+                    fp, tile = frames[name]
+                    got = r.render(fp, tile) if tile else r.render(fp)
+                    assert_same(got, refs[name], f"heavy_first={mode} {name}")
+            r.set_pixel_heavy_first(-1)

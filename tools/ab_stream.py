@@ -3,7 +3,7 @@ GPU, device output, each build's frames back to back on its own stream (no host 
 frame), builds alternating in blocks of --block frames in ABBA order so clock and thermal
 drift hit every build alike.  Also checks that every build writes bit-identical frames.
 usage: python tools/ab_stream.py LIB_A LIB_B [...] [--config c3] [--rounds 12] [--block 10]
-       [--world N] [--max-depth D] [--yaw-step DEG]
+       [--world N] [--max-depth D] [--samples S] [--spheres N] [--tree-depth D] [--yaw-step DEG]
 A build may carry options: path@option=value,... with option one of the Renderer setters
 (e.g. build/ab/libA.so@xcd_swizzle=0).
 
@@ -36,7 +36,14 @@ def morton_order(s):
     return SphereSet(s.center_radius[o].copy(), s.mat_albedo[o].copy(), s.fuzz_ri[o].copy())
 
 
-def worker(spec, config, block, max_depth=0, world=1, yaw_step=0.0):
+def config_shape(args):
+    """The config's (W, H, N, D, M, NS, MD) with the command line's overrides."""
+    import bench
+    W, H, N, D, M, NS, MD = bench.CONFIGS[args.config]
+    return (W, H, args.spheres or N, args.tree_depth or D, M, args.samples or NS, args.max_depth or MD)
+
+
+def worker(spec, shape, block, world=1, yaw_step=0.0):
     import ctypes as C
 
     import torch
@@ -45,8 +52,7 @@ def worker(spec, config, block, max_depth=0, world=1, yaw_step=0.0):
     import octreeraytracer_amd as ort
     from octreeraytracer_amd import _lib as L
 
-    W, H, N, D, M, NS, MD = bench.CONFIGS[config]
-    MD = max_depth or MD
+    W, H, N, D, M, NS, MD = shape
     path, _, opts = spec.partition("@")
     lib = C.CDLL(str(Path(path).resolve()), mode=C.RTLD_LOCAL)
     L._declare(lib, debug="present")
@@ -93,19 +99,22 @@ def main():
     ap.add_argument("--rounds", type=int, default=12)
     ap.add_argument("--block", type=int, default=10)
     ap.add_argument("--max-depth", type=int, default=0, help="override the config's ray bounce depth")
+    ap.add_argument("--samples", type=int, default=0, help="override the config's samples per pixel")
+    ap.add_argument("--spheres", type=int, default=0, help="override the config's sphere count")
+    ap.add_argument("--tree-depth", type=int, default=0, help="override the config's octree depth")
     ap.add_argument("--world", type=int, default=1, help="time rank 0's band tile of this many GPUs")
     ap.add_argument("--yaw-step", type=float, default=0.0, help="moving camera: degrees of yaw per frame")
     ap.add_argument("--worker", action="store_true")
     args = ap.parse_args()
     if args.worker:
-        return worker(args.libs[0], args.config, args.block, args.max_depth, args.world, args.yaw_step)
-    import bench
-    W, H, N, D, M, NS, MD = bench.CONFIGS[args.config]
-    MD = args.max_depth or MD
+        return worker(args.libs[0], config_shape(args), args.block, args.world, args.yaw_step)
+    W, H, N, D, M, NS, MD = config_shape(args)
     procs = []
     for spec in args.libs:
         procs.append(subprocess.Popen([sys.executable, "-u", __file__, spec, "--worker", "--config", args.config,
                                        "--block", str(args.block), "--max-depth", str(args.max_depth),
+                                       "--samples", str(args.samples), "--spheres", str(args.spheres),
+                                       "--tree-depth", str(args.tree_depth),
                                        "--world", str(args.world), "--yaw-step", str(args.yaw_step)], stdin=subprocess.PIPE, stdout=subprocess.PIPE,
                                       text=True, cwd=str(ROOT)))
         while procs[-1].stdout.readline().strip() != "ready":
