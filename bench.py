@@ -54,7 +54,11 @@ CONFIGS = {
     "ref_default": (800, 600, 100, 3, 0, 16, 8),
     "ref_stats114": (1920, 1080, 1000, 5, 1, 16, 8),
 }
-PIXEL_PATHS_AUTO_NODES = (1 << 19, 1 << 23)  # ort_kernel.hip kPixelPathsAutoNodes(Multi): 1 sample, several
+def pixel_paths_auto(n_nodes, ns, maxd):
+    """ort_kernel.hip use_pixel_paths' auto rule on a tree (kPixelPathsAutoNodes, ...5, ...8)."""
+    if maxd < 1 or (ns == 1 and maxd == 1):
+        return False
+    return n_nodes <= (1 << 24 if maxd >= 8 else 1 << 23 if maxd >= 5 else 1 << 19)
 
 
 def reference_frame_check(config: str, frame, host=None):
@@ -871,7 +875,7 @@ def trace_kernel_names(cfg, info, maxd, ns, pixels, split_ok=True):
     options: tile pairs on tiles above 2^21 pixels, split walks of the heaviest camera rays at or
     below it, 1 sample; split_ok False: the caller turned the split walks off, tile pairs)."""
     deep = info["tree_depth"] > 8
-    if not (maxd == 1 and ns == 1) and info["n_nodes"] <= PIXEL_PATHS_AUTO_NODES[ns > 1]:
+    if pixel_paths_auto(info["n_nodes"], ns, maxd):
         return ["ort_pixel_paths<0, %s> (whole-pixel paths: every sample and bounce of the frame in one launch)"
                 % str(deep).lower()]
     pairs = pixels > SPLIT_AUTO_PIXELS or not split_ok

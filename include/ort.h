@@ -165,10 +165,10 @@ typedef struct ort_scene_info {
                                       next, glsl:640, so a pixel is a sequential chain) and taking the next
                                       pixel when done -- instead of the per-sample, per-bounce pipeline (trace,
                                       shade, list sort launches).  -1 (default): on for frames of more than one
-                                      traversal per pixel on brute force, on trees of at most 2^23 nodes with
-                                      2 or more samples and of at most 2^19 with one (the reference's sweeps:
-                                      launches and sorts dominate; larger trees keep the pipeline's sorted
-                                      bounce rays); 0 off; 1 on wherever it applies (compact layout or brute
+                                      traversal per pixel on brute force, on trees of at most 2^19 nodes,
+                                      2^23 with maxDepth 5-7 and 2^24 with maxDepth 8 or more (the
+                                      reference's sweeps: launches and sorts dominate, more so the more
+                                      bounces; larger trees keep the pipeline's sorted bounce rays); 0 off; 1 on wherever it applies (compact layout or brute
                                       force, maxDepth >= 1, not 1 sample x 1 bounce).  Same pixels */
 #define ORT_OPT_PIXEL_LDS_SCENE 21 /* 1 (default): whole-pixel paths on scenes whose node records and leaf
                                       spheres fit 32 KB (depth <= 8) copy them into each workgroup's LDS and

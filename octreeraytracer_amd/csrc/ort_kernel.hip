@@ -2086,12 +2086,15 @@ int persistent_blocks(int device, bool count, bool deep, int depth, size_t lds, 
 }
 
 // Whole-pixel paths (ort_pixel_paths): the frame in one launch.  Auto (ORT_OPT_PIXEL_PATHS -1):
-// frames of more than one traversal per pixel on brute force, on trees of at most
-// kPixelPathsAutoNodesMulti nodes with several samples and kPixelPathsAutoNodes with one --
-// where the pipeline's per-bounce launches and sorts cost more than its coherence gains (the
-// reference's own sweeps and the threshold A/B).
-constexpr long long kPixelPathsAutoNodes = 1ll << 19;       // 1 sample per pixel
-constexpr long long kPixelPathsAutoNodesMulti = 1ll << 23;  // 2 or more
+// frames of more than one traversal per pixel on brute force, and on trees of at most
+// kPixelPathsAutoNodes nodes, kPixelPathsAutoNodes5 with 5+ bounces, kPixelPathsAutoNodes8 with
+// 8+ -- where the pipeline's per-bounce launches and sorts cost more than its coherence gains.
+// The crossover follows the bounces: the pipeline pays a launch, a sort and a copy per bounce
+// even when few paths are left, whole-pixel paths only the paths' own work (1080p grid over
+// 1.5-11 M nodes x 1-4 samples x 4-16 bounces, profiles/r06/grid/).
+constexpr long long kPixelPathsAutoNodes = 1ll << 19;   // any bounce depth
+constexpr long long kPixelPathsAutoNodes5 = 1ll << 23;  // maxDepth 5-7
+constexpr long long kPixelPathsAutoNodes8 = 1ll << 24;  // maxDepth 8+ (measured to 11 M nodes)
 #ifndef ORT_PIXEL_LDS_SCENE_BYTES
 #define ORT_PIXEL_LDS_SCENE_BYTES 32768
 #endif
@@ -2121,12 +2124,11 @@ unsigned long long frame_sig(const ort_ctx* ctx, const ort_params* p, const ort_
 bool use_pixel_paths(const ort_ctx* ctx, int mode, int ns, int maxd) {
     if (mode == 1 || maxd < 1 || (ns == 1 && maxd == 1) || ctx->pixel_paths == 0) return false;
     if (ctx->pixel_paths > 0) return true;
-    // several samples: the pipeline pays its launches and sorts ns x maxd times, whole-pixel
-    // paths win up to trees of 8.3 M nodes (1080p, 4 x 8: 1.65x at 209 k nodes, 1.40x at 1.5 M,
-    // 1.17x at 8.3 M; the C3 tree of 11 M nodes at 3 x 5: 0.87x); one sample: the pipeline's
-    // sorted bounce rays win from about 2 M nodes on (4K, 1 x 4: 0.54x at 1.9 M and at 11 M
-    // nodes, 1.05x at 209 k) -- profiles/r06/pixel_paths_threshold.log
-    return mode == 2 || ctx->n_nodes <= (ns > 1 ? kPixelPathsAutoNodesMulti : kPixelPathsAutoNodes);
+    // 1080p, whole-pixel paths over the pipeline: 8 bounces 1.02-1.50x from 1.5 to 11 M nodes
+    // (1 to 4 samples), 5 bounces 1.09-1.10x to 5 M, 1.00x at 8.3 M, 0.95x at 11 M; 4 bounces
+    // 0.74-1.02x from 1.5 M nodes on, 1.09x at 209 k (profiles/r06/grid/)
+    const long long limit = maxd >= 8 ? kPixelPathsAutoNodes8 : (maxd >= 5 ? kPixelPathsAutoNodes5 : kPixelPathsAutoNodes);
+    return mode == 2 || ctx->n_nodes <= limit;
 }
 
 // The frame as one ort_pixel_paths launch (use_pixel_paths); dout: the frame on the device.

@@ -478,19 +478,19 @@ def test_pixel_paths_option_and_auto(ort, oracle, scene_c1, scene_c3):
         got = r.render(pb)
         assert r.frame_trace_times_ms(1)[0][1] > 1  # auto: the pipeline on a large tree
         assert_same(got, oracle.render(s3, t3, pb), "C3 tree, auto")
-    # a 1.48 M-node tree: whole-pixel paths with 2 samples (<= 2^23 nodes), the pipeline with 1
-    # (> 2^19 nodes) -- the rule's two regimes (profiles/r06/pixel_paths_threshold.log)
+    # a 1.48 M-node tree (> 2^19): whole-pixel paths with 5 or 8 bounces, the pipeline with 3,
+    # whatever the samples -- the rule's regimes (profiles/r06/grid/)
     sm = ort.random_spheres(30_000, 42)
     tm = ort.build_octree(sm, 7, 0)
     assert 2**19 < tm.n_nodes <= 2**23
     with ort.Renderer(0) as r:
         r.upload(sm, tm)
-        for ns, one_launch in ((2, True), (1, False)):
-            pm = ort.FrameParams.default_camera(192, 108, num_samples=ns, max_depth=3)
+        for ns, maxd, one_launch in ((2, 3, False), (1, 3, False), (2, 5, True), (1, 8, True)):
+            pm = ort.FrameParams.default_camera(192, 108, num_samples=ns, max_depth=maxd)
             got = r.render(pm)
             n = r.frame_trace_times_ms(1)[0][1]
-            assert (n == 1) == one_launch, (ns, n)
-            assert_same(got, oracle.render(sm, tm, pm), f"1.48 M-node tree, {ns} samples, auto")
+            assert (n == 1) == one_launch, (ns, maxd, n)
+            assert_same(got, oracle.render(sm, tm, pm), f"1.48 M-node tree, {ns} x {maxd}, auto")
 
 
 @pytest.mark.parametrize("n,depth,mspn", [(100, 3, 0), (60, 5, 1), (10, 1, 1)])
