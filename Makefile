@@ -37,7 +37,7 @@ $(ALIB): $(HOST_OBJS) $(AOBJ)/ort_kernel.o $(OBJ)/gpu_build.o $(AOBJ)/group.o
 
 $(OBJ)/%.o: $(SRC)/%.cpp $(HDRS)
 	@mkdir -p $(OBJ)
-	$(CXX) $(CXXFLAGS) -c $< -o $@
+	$(CXX) $(CXXFLAGS) -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ -c $< -o $@
 
 $(OBJ)/ort_kernel.o: $(SRC)/ort_kernel.hip $(HDRS)
 	@mkdir -p $(OBJ)

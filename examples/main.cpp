@@ -3,7 +3,7 @@
 // can write the last frame as a PPM (--ppm) and appends the saveStats CSV row (--stats).
 //   build: make examples   ->  build/ort_main
 //   run:   build/ort_main --spheres 1000 --depth 5 --samples 4 --bounces 4 --width 800
-//          --height 600 --frames 10 --stats stats.csv [--stats-ext] --ppm frame.ppm
+//          --height 600 --frames 10 --stats stats.csv [--stats-ext] [--readback] --ppm frame.ppm
 // tools/sweep.py drives it over the reference's experiment grid (analysis/runner.py:99-192).
 #include <cstdio>
 #include <cstdlib>
@@ -44,6 +44,7 @@ int main(int argc, char** argv) {
         }
         else if (!std::strcmp(argv[i], "--stats")) { cfg.collectStats = true; cfg.outputFile = next(); }
         else if (!std::strcmp(argv[i], "--stats-ext")) cfg.extendedStats = true;  // + 5 throughput columns
+        else if (!std::strcmp(argv[i], "--readback")) cfg.readback = true;  // timed frames copied to the host
         else if (!std::strcmp(argv[i], "--ppm")) ppm = next();
         else { std::fprintf(stderr, "unknown argument %s\n", argv[i]); return 2; }
     }

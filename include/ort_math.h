@@ -122,6 +122,11 @@ ORT_HD float ort__inff(void) { uint32_t u = 0x7f800000u; float f; __builtin_memc
  * Reduction by pi/2 in double with a two-part constant and fma: r = x - k*pi/2 to ~2^-100
  * absolute for |x| < 2^24 (beyond that the results stay deterministic, not accurate). */
 ORT_HD void ort_sincosf(float xf, float* sn, float* cs) {
+#if ORT_NATIVE_TRIG && defined(__HIP_DEVICE_COMPILE__)
+    *sn = __builtin_amdgcn_sinf(xf * 0.15915494309189535f);
+    *cs = __builtin_amdgcn_cosf(xf * 0.15915494309189535f);
+    return;
+#endif
     if (!(xf == xf) || xf == ort__inff() || xf == -ort__inff()) {
         *sn = ort__nanf();
         *cs = ort__nanf();
@@ -141,7 +146,7 @@ ORT_HD void ort_sincosf(float xf, float* sn, float* cs) {
     *cs = (float)(((q + 1) & 2) ? -cv : cv);
 }
 ORT_HD float ort_sinf(float xf) {
-#if ORT_NATIVE_TRIG
+#if ORT_NATIVE_TRIG && defined(__HIP_DEVICE_COMPILE__)
     return __builtin_amdgcn_sinf(xf * 0.15915494309189535f);
 #endif
     float s, c;
@@ -149,7 +154,7 @@ ORT_HD float ort_sinf(float xf) {
     return s;
 }
 ORT_HD float ort_cosf(float xf) {
-#if ORT_NATIVE_TRIG
+#if ORT_NATIVE_TRIG && defined(__HIP_DEVICE_COMPILE__)
     return __builtin_amdgcn_cosf(xf * 0.15915494309189535f);
 #endif
     float s, c;
@@ -199,7 +204,7 @@ ORT_HD float ort__exp2_f(double t) {
 }
 /* GLSL pow(x, y): undefined for x < 0 (we return NaN, as exp2(y*log2(x)) would). */
 ORT_HD float ort_powf(float x, float y) {
-#if ORT_NATIVE_POW
+#if ORT_NATIVE_POW && defined(__HIP_DEVICE_COMPILE__)
     return __builtin_amdgcn_exp2f(y * __builtin_amdgcn_logf(x));
 #endif
     if (!(x == x) || !(y == y)) return ort__nanf();

@@ -9,6 +9,8 @@
 
 #include <sched.h>
 
+#include <hip/hip_runtime_api.h>
+
 #include "scene.h"
 
 Raytracer::Raytracer() : Raytracer(RaytracerConfig()) {}
@@ -101,6 +103,8 @@ void Raytracer::setupBuffers() {
 }
 
 void Raytracer::cleanupBuffers() {
+    if (dframe) (void)hipFree(dframe);
+    dframe = nullptr;
     if (ctx) ort_destroy(ctx);
     if (group) ort_group_destroy(group);
     ctx = nullptr;
@@ -157,11 +161,21 @@ void Raytracer::run() {
     setupScene();
     setupBuffers();
     if (!sceneReady) return;
-    frame.assign((size_t)width * height * 3, 0.0f);
-    for (int i = 0; i < cfg.warmupFrames; i++) render(camera, frame.data());
+    const size_t frameBytes = sizeof(float) * 3 * (size_t)width * height;
+    if (cfg.readback) {
+        frame.assign((size_t)width * height * 3, 0.0f);
+    } else if (!dframe) {  // on the device that renders (a group: devices[0], where it assembles)
+        const int dev = cfg.devices.size() > 1 ? cfg.devices[0] : cfg.device;
+        if (hipSetDevice(dev) != hipSuccess || hipMalloc((void**)&dframe, frameBytes) != hipSuccess) {
+            dframe = nullptr;
+            std::cerr << "run: no device frame buffer of " << frameBytes << " bytes" << std::endl;
+            return;
+        }
+    }
+    for (int i = 0; i < cfg.warmupFrames; i++) renderRun();
     for (int i = 0; i < cfg.frames; i++) {
         const auto frameStart = std::chrono::steady_clock::now();
-        if (render(camera, frame.data()) != ORT_OK) {
+        if (renderRun() != ORT_OK) {
             std::cerr << "render failed: " << lastError() << std::endl;
             break;
         }
@@ -175,6 +189,18 @@ void Raytracer::run() {
         if (cfg.extendedStats && !countWork()) std::cerr << "counting the frame's work failed: " << lastError() << std::endl;
         saveStats();
     }
+}
+
+// A synchronous frame either way (ort_render / ort_group_render on the context's own stream
+// return once the frame is complete).
+int Raytracer::renderRun() {
+    if (!dframe) return render(camera, frame.data());
+    if (group) {
+        const ort_params p = frameParams(camera);
+        return ort_group_render(group, &p, dframe, 1);
+    }
+    const ort_tile t{0, width, 0, height, 0, 0};
+    return render(camera, t, dframe, true, nullptr);
 }
 
 // saveStats (src/raytracer.cpp:359-449): 2.5-sigma z-score filter, one ';' row.

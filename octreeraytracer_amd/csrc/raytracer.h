@@ -46,6 +46,9 @@ struct RaytracerConfig {
                                    // of Octree::build on the host; getOctree() then stays empty
     bool extendedStats = false;    // saveStats appends 5 throughput columns to the reference's 15
                                    // (see StatsWork / Raytracer::statsRow)
+    bool readback = false;         // run(): copy every frame to host memory; default off: the frames
+                                   // stay in a device buffer, as the reference's stay in its GL
+                                   // framebuffer (src/raytracer.cpp:476-519 never reads them back)
 };
 
 // Work of one frame for the extended stats columns: ort_count_traffic over the full frame
@@ -112,6 +115,8 @@ private:
     int frameCount;
     std::vector<double> renderTimes;
     std::vector<float> frame;
+    float* dframe = nullptr;       // run()'s device frame (readback off), on the context's device
+    int renderRun();               // one frame of run(): into dframe, or into `frame` with readback
     double gpuBuildSeconds = 0.0;
     StatsWork work;               // counted after the timed frames when cfg.extendedStats
 

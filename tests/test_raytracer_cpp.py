@@ -22,12 +22,15 @@ def test_example_binary_built():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("gpu_build", [False, True])
-def test_main_renders_and_writes_stats(ort, oracle, tmp_path, gpu_build):
+@pytest.mark.parametrize("gpu_build,readback", [(False, False), (True, False), (False, True)])
+def test_main_renders_and_writes_stats(ort, oracle, tmp_path, gpu_build, readback):
+    """run()'s timed frames into a device frame (default: the reference's frames stay in its GL
+    framebuffer) or copied to the host (--readback); then the --ppm frame against the oracle."""
     csv, ppm = tmp_path / "stats.csv", tmp_path / "frame.ppm"
     cmd = [str(EXE), "--spheres", "100", "--depth", "4", "--samples", "1", "--bounces", "1", "--width", "64",
            "--height", "48", "--frames", "3", "--warmup", "1", "--stats", str(csv), "--ppm", str(ppm)]
     cmd += ["--gpu-build"] if gpu_build else []
+    cmd += ["--readback"] if readback else []
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     row = csv.read_text().strip().split(";")

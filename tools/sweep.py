@@ -82,7 +82,7 @@ GRIDS = {"runner": grid_runner, "maxspheres0": grid_maxspheres0, "bench": grid_b
 
 
 def command(exp: dict, out: str, frames: int, warmup: int, gpu_build: bool, devices: str, extended: bool,
-            exe: Path = EXE) -> list[str]:
+            exe: Path = EXE, readback: bool = False) -> list[str]:
     """The ort_main command line of one experiment (the config.h edit + rebuild of runner.py:16-72)."""
     cmd = [str(exe)]
     for k, flag in FLAGS.items():
@@ -101,6 +101,8 @@ def command(exp: dict, out: str, frames: int, warmup: int, gpu_build: bool, devi
         cmd.append("--gpu-build")
     if devices:
         cmd += ["--devices", devices]
+    if readback:
+        cmd.append("--readback")
     return cmd
 
 
@@ -148,6 +150,9 @@ def main(argv=None):
     ap.add_argument("--timeout", type=float, default=500, help="seconds per run (runner.py:184)")
     ap.add_argument("--gpu-build", action="store_true", help="build each octree with ort_build_scene")
     ap.add_argument("--devices", default="", help="e.g. 0,1,2,3,4,5,6,7: render every point on an ort_group")
+    ap.add_argument("--readback", action="store_true",
+                    help="time every frame with its copy to host memory (default: frames stay on the device, "
+                         "as the reference's stay in its GL framebuffer)")
     ap.add_argument("--reference-columns", action="store_true", help="write the reference's 15 columns only")
     ap.add_argument("--dry-run", action="store_true", help="print the commands, run nothing")
     ap.add_argument("--limit", type=int, default=0, help="run only the first N points")
@@ -159,7 +164,7 @@ def main(argv=None):
     failed = 0
     for i, exp in enumerate(exps):
         cmd = command(exp, args.out, args.frames, args.warmup, args.gpu_build, args.devices,
-                      not args.reference_columns)
+                      not args.reference_columns, readback=args.readback)
         print(f"Experiment {i + 1}/{len(exps)}: {' '.join(cmd[1:])}", flush=True)
         if args.dry_run:
             continue

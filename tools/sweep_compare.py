@@ -3,8 +3,9 @@ same configuration (analysis/stats.csv -- runner.py's grid -- and analysis/stats
 
 The reference's rows are wall-clock frame times of its GL window loop (src/raytracer.cpp:476-519)
 on the authors' GPU, synchronised to the display: frames at 6.9 ms are its 144 Hz vsync cap, not
-the shader's cost.  Ours are Raytracer::render's wall time per frame (one frame in flight, host
-output read back).
+the shader's cost.  Ours are Raytracer::run's wall time per frame (one frame in flight, the
+frame left in a device buffer as the reference's is left in its framebuffer; `tools/sweep.py
+--readback` times each frame with its copy to host memory as well: profiles/r06/*_readback*).
 
 usage: python tools/sweep_compare.py OURS.csv REFERENCE.csv > table.md
 """
