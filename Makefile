@@ -84,7 +84,7 @@ san: build/san/san_check
 
 $(SANOBJ)/%.o: $(SRC)/%.cpp $(HDRS)
 	@mkdir -p $(SANOBJ)
-	$(CLANGXX) $(SAN) -std=c++17 -ffp-contract=off -fno-fast-math -c $< -o $@
+	$(CLANGXX) $(SAN) -std=c++17 -ffp-contract=off -fno-fast-math -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ -c $< -o $@
 
 $(SANOBJ)/%.o: $(SRC)/%.hip $(HDRS) $(SRC)/gpu_build.h $(SRC)/group_map.h
 	@mkdir -p $(SANOBJ)

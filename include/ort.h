@@ -179,6 +179,16 @@ typedef struct ort_scene_info {
                                       chains start first and do not trail the frame; tile order otherwise.
                                       -1 (default): on for frames of 2 or more samples; 0 off; 1 on.  Same
                                       pixels (the order changes which lane traces a pixel, not its chain) */
+#define ORT_OPT_PIXEL_SPECULATE 23 /* whole-pixel paths, 2+ samples: from the second frame of a shape on,
+                                      a pixel's samples are traced as 4 chunks in parallel, chunk c
+                                      starting from the RNG state chunk c-1 ended with in the previous
+                                      frame (it only depends on how many draws the paths took); a pixel
+                                      whose chunk ends in another state than last frame's has its later
+                                      samples re-traced from the true state, and every pixel's samples
+                                      are summed in order: same pixels, and a frame no longer waits for
+                                      its longest pixel's chain.  -1 (default) and 1: on while the
+                                      buffers (12 B per sample and path slot, 16 B per chunk) fit 8 GiB;
+                                      0: off */
 /* Retired option codes, reserved (ORT_ERR_UNSUPPORTED): options that lost to the defaults in
  * A/B and were removed -- 5 the wave-level packet walk (1.2-1.35x slower),
  * 7 the wave-level block queue (1/8 band 0.83 vs 0.61 ms), 17 longest-first workgroups

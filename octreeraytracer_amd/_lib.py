@@ -45,6 +45,7 @@ ORT_OPT_LAUNCH_TIMES = 19
 ORT_OPT_PIXEL_PATHS = 20
 ORT_OPT_PIXEL_LDS_SCENE = 21
 ORT_OPT_PIXEL_HEAVY_FIRST = 22
+ORT_OPT_PIXEL_SPECULATE = 23
 ORT_OPT_RETIRED = (5, 7, 17)  # include/ort.h ORT_OPT_IS_RETIRED: ORT_ERR_UNSUPPORTED
 ORT_LAYOUT_COMPACT_EXACT_EMULATION = 2
 ORT_COUNT_N = 6

@@ -36,13 +36,13 @@
 // ORT_ANALYSIS (Makefile `analysis`: octreeraytracer_amd/lib/libort_analysis.so) adds the
 // test/analysis surface: the ort_debug_* entry points (host emulation of the kernel's per-pixel
 // code for the CPU suite, walk statistics for tools/), ORT_OPT_DEBUG_FLAGS, and the per-wave
-// timeline builds (ORT_TILE_CLOCK, ORT_PERSIST_CLOCK, ORT_PERSIST_STATS).  The product library
+// timeline builds (ORT_TILE_CLOCK, ORT_PERSIST_CLOCK, ORT_PERSIST_STATS, ORT_PIXEL_CLOCK).  The product library
 // libort.so is built without it and exports only include/ort.h.
 #ifndef ORT_ANALYSIS
 #define ORT_ANALYSIS 0
 #endif
 #if !ORT_ANALYSIS && ((defined(ORT_TILE_CLOCK) && ORT_TILE_CLOCK) || (defined(ORT_PERSIST_CLOCK) && ORT_PERSIST_CLOCK) || \
-                      (defined(ORT_PERSIST_STATS) && ORT_PERSIST_STATS))
+                      (defined(ORT_PERSIST_STATS) && ORT_PERSIST_STATS) || (defined(ORT_PIXEL_CLOCK) && ORT_PIXEL_CLOCK))
 #error "per-wave timeline builds are analysis builds: add -DORT_ANALYSIS=1"
 #endif
 
@@ -126,6 +126,23 @@ struct PipeArgs {
     int* pl_wcnt;
     unsigned long long* pl_cost;
     int pl_stride;
+    // whole-pixel paths, samples in parallel (ORT_OPT_PIXEL_SPECULATE): a pixel's samples in
+    // sp_nch chunks of sp_chunk; per chunk c and slot k (index c * total + k) the RNG state the
+    // chunk ends with -- sp_prev last frame's (chunk c+1 of this frame starts from sp_prev[c]),
+    // sp_cur this frame's -- and per sample s the radiance (sp_col: three planes of ns * total
+    // floats, index s * total + k).  A whole-pixel launch with sp_cur records its chunks' end
+    // states; one with fx_slot runs the fixup list: pixel fx_slot[i] from sample fx_s0[i] with
+    // state fx_st[i] and the colour sum of its earlier samples fx_col (three planes of total
+    // floats), *fx_n entries
+    const float2* sp_prev;
+    float2* sp_cur;
+    float* sp_col;
+    int sp_chunk, sp_nch;  // samples per SPEC item (a chunk of a pixel's samples), chunks per pixel
+    int* fx_n;
+    int* fx_slot;
+    int* fx_s0;
+    float2* fx_st;
+    float* fx_col;
 #if ORT_ANALYSIS
     ulonglong4* wclock;  // analysis builds only (ORT_PERSIST_CLOCK, ort_debug_wave_clock): per wave a timeline record
     int wclock_n;
@@ -1408,13 +1425,28 @@ __device__ __forceinline__ void block_account(const PipeArgs& A, int slot, int b
 #define ORT_PIXEL_WAVES 4
 #endif
 
+
 // LDS: small scenes (depth <= 8) walk the workgroup's copies of nk[] and leaf_sph[] in LDS
 // (ds_read, ~50 cycles) instead of global memory: the kernel waits on memory for most of its
 // cycles (SQ_WAIT_ANY 0.64 at config.h's default scene, profiles/r06/), and a walk is a chain
 // of dependent record loads.
-template <int MODE, bool DEEP, bool LDS>
+// SPEC: samples in parallel.  A pixel's samples form a chain only through the RNG state, and
+// the state a sample ends with depends on the path only through how many draws it took -- so
+// with a static or slowly moving camera it repeats from frame to frame.  SPEC launches take
+// (8x8 block, sample s) items: sample s >= 1 starts from the state sample s-1 ended with LAST
+// frame (sp_prev), writes its radiance and end state, and flags the pixel when its end state
+// differs from last frame's -- the samples after it then started from a wrong state.
+// ort_sample_resolve sums each pixel's samples in order up to the first flagged one and lists
+// the pixels that need the rest; a whole-pixel launch over that list (fx_*) continues them
+// from the true state.  Every pixel's samples are thus the sequential chain's, summed in the
+// chain's order: the frames stay bit-identical, and a frame is no longer as long as its longest
+// pixel's chain (16 samples x 8 bounces at config.h's default).
+// PM: 0 whole pixels, 1 SPEC samples, 2 whole pixels that record their samples' end states or
+// run the fixup list (kept apart from 0: its registers are the ones-sample frames' too)
+template <int MODE, bool DEEP, bool LDS, int PM = 0>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ORT_PIXEL_WAVES)))
 ort_pixel_paths(PipeArgs A) {
+    constexpr bool SPEC = PM == 1;
     extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];  // plane tables: 1 KiB-aligned
     LdsView L{};
     ort::KScene S = A.S;
@@ -1433,18 +1465,21 @@ ort_pixel_paths(PipeArgs A) {
     const int maxd = A.pp.maxDepth, ns = A.pp.ns;
     // the work items: 8x8 blocks, last frame's heaviest class first (a longest-first list
     // schedule: a frame ends with its longest pixels -- a pixel's samples run one after another --
-    // and a block keeps its pixels' rays coherent), else in tile order.  Lane q < 32 holds the
-    // inclusive prefix of the class counts.
+    // and a block keeps its pixels' rays coherent), else in tile order; SPEC: (block, sample)
+    // pairs, a block's samples one after another; the fixup list: 64 of its entries at a time.
+    // Lane q < 32 holds the inclusive prefix of the class counts.
+    const bool fixup = PM == 2 && A.fx_slot;
     const int n_blocks = A.total >> 6;
+    const int n_items = SPEC ? n_blocks * A.sp_nch : (fixup ? (*A.fx_n + 63) >> 6 : n_blocks);
     int cls_end = 0;
-    if (ORT_PIXEL_LPT && A.pl_r) {
+    if (ORT_PIXEL_LPT && !SPEC && A.pl_r) {
         cls_end = lane < kPixelClasses ? A.pl_rcnt[lane] : 0;
         for (int d = 1; d < kPixelClasses; d <<= 1) {
             const int v = __shfl_up(cls_end, d);
             if (lane >= d) cls_end += v;
         }
     }
-    const bool listed = ORT_PIXEL_LPT && A.pl_r && __shfl(cls_end, kPixelClasses - 1) == n_blocks;
+    const bool listed = ORT_PIXEL_LPT && !SPEC && !fixup && A.pl_r && __shfl(cls_end, kPixelClasses - 1) == n_blocks;
     int k = -1;              // the lane's path slot (pixel), -1 idle
     int nb = 0;              // bounces traced for the lane's pixel so far (its cost class)
     int px = 0, py = 0, s = 0, b = 0;
@@ -1454,17 +1489,40 @@ ort_pixel_paths(PipeArgs A) {
     float importance = 1.0f;
     ort_rng st;
     st.x = st.y = 0.0f;
-    int next = 0, end = 0;   // wave-uniform: the rest of the wave's block
-    bool drained = false;    // wave-uniform: the cursor passed the last slot
+    int next = 0, end = 0;   // wave-uniform: the rest of the wave's block (or fixup entries)
+    int item_s = 0;          // wave-uniform, SPEC: the sample of those slots
+    bool drained = false;    // wave-uniform: the cursor passed the last item
+#if ORT_PIXEL_CLOCK  // analysis: per wave the cycles of the refill, the walk and the shading, and the walk's lanes
+    unsigned long long ck_refill = 0, ck_trace = 0, ck_shade = 0, ck_iter = 0, ck_lanes = 0, ck_t = 0;
+    const unsigned long long ck_rt0 = __builtin_amdgcn_s_memrealtime();
+#define ORT_CK_MARK(acc)                                            \
+    do {                                                            \
+        const unsigned long long now = __builtin_amdgcn_s_memtime(); \
+        acc += now - ck_t;                                          \
+        ck_t = now;                                                 \
+    } while (0)
+#else
+#define ORT_CK_MARK(acc) do { } while (0)
+#endif
     for (;;) {
+#if ORT_PIXEL_CLOCK
+        ck_t = __builtin_amdgcn_s_memtime();
+#endif
         const unsigned long long idle = __ballot(k < 0);
-        if (idle && !drained) {  // refill: idle lanes take the chunk's next pixels
-            if (next == end) {  // the next block
+        if (idle && !drained) {  // refill: idle lanes take the item's next pixels
+            if (next == end) {  // the next item
                 int j = 0;
                 if (lane == 0) j = atomicAdd(A.sync + 1, 1);
                 j = __shfl(j, 0);
-                if (j >= n_blocks) {
+                if (j >= n_items) {
                     drained = true;
+                } else if (SPEC) {  // block j / nch, its pixels' chunk j % nch
+                    next = (j / A.sp_nch) << 6;
+                    end = next + 64;
+                    item_s = j % A.sp_nch;
+                } else if (fixup) {
+                    next = j << 6;
+                    end = min(next + 64, *A.fx_n);
                 } else {
                     int blk = j;
                     if (listed) {  // item j of the class lists: class q = the first with j < its prefix end
@@ -1483,51 +1541,94 @@ ort_pixel_paths(PipeArgs A) {
                 if (k < 0) {
                     const int rank = __popcll(idle & below);
                     if (rank < take) {
-                        const int cand = next + rank;
+                        const int cand = fixup ? A.fx_slot[next + rank] : next + rank;
                         bool pixel = false;
                         int cx, cy;
                         if (slot_coords(A, cand, cx, cy)) {
                             const int y = tile_row_to_y(A.tm, cy);
-                            if (y < A.pp.H) {  // a pixel: sample 0's camera ray
+                            if (y < A.pp.H) {  // a pixel: its first sample's camera ray
                                 k = cand;
                                 nb = 0;
                                 px = A.tm.x0 + cx;
                                 py = y;
-                                ort::pixel_rng_init(A.pp, px, py, st);
-                                s = 0;
                                 b = 0;
-                                col = ort::mk(0.0f, 0.0f, 0.0f);
                                 c = ort::mk(1.0f, 1.0f, 1.0f);
                                 importance = 1.0f;
-                                ray = ort::primary_ray(A.pp, px, py, 0, st);
+                                if (SPEC) {  // chunk item_s from last frame's end state of chunk item_s - 1
+                                    s = item_s * A.sp_chunk;
+                                    if (item_s == 0) {
+                                        ort::pixel_rng_init(A.pp, px, py, st);
+                                    } else {
+                                        const float2 v = A.sp_prev[(size_t)(item_s - 1) * A.total + k];
+                                        st.x = v.x;
+                                        st.y = v.y;
+                                    }
+                                } else if (fixup) {  // the rest of the pixel's chain from its true state
+                                    const int e = next + rank;
+                                    s = A.fx_s0[e];
+                                    const float2 v = A.fx_st[e];
+                                    st.x = v.x;
+                                    st.y = v.y;
+                                    col = ort::mk(A.fx_col[e], A.fx_col[(size_t)A.total + e], A.fx_col[2 * (size_t)A.total + e]);
+                                } else {
+                                    ort::pixel_rng_init(A.pp, px, py, st);
+                                    s = 0;
+                                    col = ort::mk(0.0f, 0.0f, 0.0f);
+                                }
+                                ray = ort::primary_ray(A.pp, px, py, s, st);
                                 pixel = true;
-                            } else {  // a band's padding row (past the frame): zeros, as the pipeline writes
+                            } else if (!SPEC) {  // a band's padding row (past the frame): zeros, as the pipeline writes
                                 float* o = A.out + 3 * ((size_t)cy * A.tm.tw + cx);
                                 o[0] = 0.0f; o[1] = 0.0f; o[2] = 0.0f;
                             }
                         }
-                        if (ORT_PIXEL_LPT && A.pl_w && !pixel) block_account(A, cand, 0);
+                        if (ORT_PIXEL_LPT && !SPEC && A.pl_w && !pixel) block_account(A, cand, 0);
                     }
                 }
                 next += take;
             }
         }
+        ORT_CK_MARK(ck_refill);
         if (!__ballot(k >= 0)) {
             if (drained) break;
             continue;
         }
+#if ORT_PIXEL_CLOCK
+        ck_iter += 1;
+        ck_lanes += __popcll(__ballot(k >= 0));
+#endif
         if (k >= 0) {  // one bounce of the lane's current path (radiance(), glsl:604-627)
             float t;
             int entry;
             const bool hit = pixel_trace<MODE, DEEP, LDS>(A, S, L, ray, t, entry);
+#if ORT_PIXEL_CLOCK
+            __builtin_amdgcn_wave_barrier();
+#endif
+            ORT_CK_MARK(ck_trace);
             ort::HitRec h;
             if (hit) h = ort::hit_record<MODE>(A.S, ray, t, entry);
             bool ended = ort::shade_bounce(hit, h, ray, c, importance, st);
             ++b;
             ++nb;
             ended = ended || b >= maxd || importance < 0.01f;
-            if (ended) {  // col += radiance(r) (glsl:655); the pixel's next sample, or its final colour
+            if (ended && SPEC) {  // the sample's radiance; the chunk's next sample, or its end state
+                const size_t i = (size_t)s * A.total + k;
+                A.sp_col[i] = c.x;
+                A.sp_col[(size_t)ns * A.total + i] = c.y;
+                A.sp_col[2 * (size_t)ns * A.total + i] = c.z;
+                if (++s < ns && s % A.sp_chunk != 0) {
+                    b = 0;
+                    c = ort::mk(1.0f, 1.0f, 1.0f);
+                    importance = 1.0f;
+                    ray = ort::primary_ray(A.pp, px, py, s, st);
+                } else {
+                    A.sp_cur[(size_t)((s - 1) / A.sp_chunk) * A.total + k] = make_float2(st.x, st.y);
+                    k = -1;
+                }
+            } else if (ended) {  // col += radiance(r) (glsl:655); the pixel's next sample, or its final colour
                 col = ort::add(col, c);
+                if (PM == 2 && A.sp_cur && ((s + 1) % A.sp_chunk == 0 || s + 1 == ns))  // a chunk's end state, for SPEC
+                    A.sp_cur[(size_t)(s / A.sp_chunk) * A.total + k] = make_float2(st.x, st.y);
                 if (++s < ns) {
                     b = 0;
                     c = ort::mk(1.0f, 1.0f, 1.0f);
@@ -1544,19 +1645,94 @@ ort_pixel_paths(PipeArgs A) {
                 }
             }
         }
+        ORT_CK_MARK(ck_shade);
     }
-    // the last workgroup out resets the cursor and the done count for the next launch
+#if ORT_PIXEL_CLOCK
+    {
+        const int gw = (int)(blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6));
+        if (A.wclock && lane == 0 && !fixup && 2 * gw + 1 < A.wclock_n) {  // (the fixup launch keeps none)
+            A.wclock[2 * gw] = make_ulonglong4(ck_refill, ck_trace, ck_shade, ck_iter);
+            A.wclock[2 * gw + 1] = make_ulonglong4(ck_lanes, ck_rt0, __builtin_amdgcn_s_memrealtime(), 1ull);
+        }
+    }
+#endif
+#undef ORT_CK_MARK
+    // the last workgroup out resets the cursor and the done count for the next launch (and the
+    // fixup list's length, read by every wave at its start)
     __syncthreads();
     if (threadIdx.x == 0) {
         __threadfence();
         if (atomicAdd(A.sync + 2, 1) == (int)gridDim.x - 1) {
             atomicExch(A.sync + 1, 0);
             atomicExch(A.sync + 2, 0);
+            if (fixup) atomicExch(A.fx_n, 0);
             // the class counts read this frame become the next frame's write counts
             if (ORT_PIXEL_LPT && A.pl_rcnt)
                 for (int q = 0; q < kPixelClasses; ++q) atomicExch(A.pl_rcnt + q, 0);
         }
     }
+}
+
+// SPEC frames: per slot, the pixel's samples summed in order up to the end of the first chunk
+// whose end state differs from last frame's (all of them when none does: every chunk started
+// from its true state) -> the final pixel, or an entry of the fixup list (the pixel's next
+// sample, its true start state, the sum so far).  Padding rows: zeros.
+__global__ void __launch_bounds__(256) ort_sample_resolve(PipeArgs A) {
+    const int k = (int)(blockIdx.x * 256 + threadIdx.x);
+    if (k >= A.total) return;
+    int cx, cy;
+    if (!slot_coords(A, k, cx, cy)) return;
+    float* o = A.out + 3 * ((size_t)cy * A.tm.tw + cx);
+    if (tile_row_to_y(A.tm, cy) >= A.pp.H) {
+        o[0] = 0.0f; o[1] = 0.0f; o[2] = 0.0f;
+        return;
+    }
+    const int ns = A.pp.ns;
+    int bad = A.sp_nch - 1;  // the first chunk whose end state moved (the last: none did)
+    for (int c = 0; c < A.sp_nch - 1; ++c) {
+        const size_t i = (size_t)c * A.total + k;
+        const float2 u = A.sp_cur[i], v = A.sp_prev[i];
+        if (__float_as_uint(u.x) != __float_as_uint(v.x) || __float_as_uint(u.y) != __float_as_uint(v.y)) {
+            bad = c;
+            break;
+        }
+    }
+    const int last = min((bad + 1) * A.sp_chunk, ns) - 1;  // samples 0..last are the chain's
+    const size_t plane = (size_t)ns * A.total;
+    ort::V3 col = ort::mk(0.0f, 0.0f, 0.0f);
+    for (int s = 0; s <= last; ++s) {
+        const size_t i = (size_t)s * A.total + k;
+        col = ort::add(col, ort::mk(A.sp_col[i], A.sp_col[plane + i], A.sp_col[2 * plane + i]));
+    }
+    if (last == ns - 1) {
+        const ort::V3 v = ort::finish_pixel(col, ns);
+        o[0] = v.x; o[1] = v.y; o[2] = v.z;
+        return;
+    }
+    const int e = atomicAdd(A.fx_n, 1);
+    A.fx_slot[e] = k;
+    A.fx_s0[e] = last + 1;
+    A.fx_st[e] = A.sp_cur[(size_t)bad * A.total + k];
+    A.fx_col[e] = col.x;
+    A.fx_col[(size_t)A.total + e] = col.y;
+    A.fx_col[2 * (size_t)A.total + e] = col.z;
+}
+
+// A frame that ran the pixels' chains whole (recording their chunk end states): the pixels whose
+// chunk end states differ from last frame's -- the ones a SPEC frame would have re-traced -- into
+// *count (the camera or the scene moved: the next frame then does not speculate).
+__global__ void __launch_bounds__(256) ort_sample_moved(PipeArgs A, int* count) {
+    const int k = (int)(blockIdx.x * 256 + threadIdx.x);
+    bool moved = false;
+    int cx, cy;
+    if (k < A.total && slot_coords(A, k, cx, cy) && tile_row_to_y(A.tm, cy) < A.pp.H)
+        for (int c = 0; c < A.sp_nch - 1 && !moved; ++c) {
+            const size_t i = (size_t)c * A.total + k;
+            const float2 u = A.sp_cur[i], v = A.sp_prev[i];
+            moved = __float_as_uint(u.x) != __float_as_uint(v.x) || __float_as_uint(u.y) != __float_as_uint(v.y);
+        }
+    const unsigned long long m = __ballot(moved);
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(count, __popcll(m));
 }
 
 struct DevBuf {
@@ -1639,6 +1815,21 @@ struct ort_ctx {
     // and their counts, the blocks' cost accumulators, the parity of the next frame's write
     // buffer, and the shape the read buffer's lists belong to (0: none)
     DevBuf pplist, ppcnt, ppcost;
+    // samples in parallel (ORT_OPT_PIXEL_SPECULATE): the two per-chunk end-state buffers (spst,
+    // which one is last frame's: sp_par), the samples' radiance, the fixup list and its length,
+    // and the shape the recorded states belong to (0: none)
+    DevBuf spst, spcol, spfix, spfixn;
+    int sp_par = 0;
+    unsigned long long sp_sig = 0;
+    // the pixels the last measured frame found moved (re-traced by a SPEC frame, or counted by
+    // ort_sample_moved), copied to pinned memory behind sp_ev; the next frame speculates only
+    // while at most 1/kSpecMovedMax of the pixels moved (a moving camera: the re-traced pixels'
+    // chains would set the frame's length again)
+    int* sp_moved_host = nullptr;
+    hipEvent_t sp_ev = nullptr;
+    bool sp_pending = false;
+    long long sp_moved = 0;
+    int pixel_spec = -1;  // ORT_OPT_PIXEL_SPECULATE: -1 auto, 0 off, 1 on
     int pp_par = 0;
     unsigned long long pp_sig = 0;
     unsigned long long cost_sig = 0;
@@ -2099,15 +2290,52 @@ constexpr long long kPixelPathsAutoNodes8 = 1ll << 24;  // maxDepth 8+ (measured
 #define ORT_PIXEL_LDS_SCENE_BYTES 32768
 #endif
 constexpr int kPixelLdsSceneBytes = ORT_PIXEL_LDS_SCENE_BYTES;  // LDS-resident scene budget (ort_pixel_paths)
+// samples in parallel: device bytes of the per-sample buffers (two end states, the radiance) and
+// the per-slot ones (flags, fixup list); frames above the budget run the pixels' chains whole
+constexpr size_t kSpecBudget = size_t(8) << 30;
+#ifndef ORT_PIXEL_SPEC_CHUNKS
+#define ORT_PIXEL_SPEC_CHUNKS 4
+#endif
+// a pixel's samples in (about) this many chunks: a SPEC item is one chunk of a block's pixels --
+// shorter chains with more chunks, but each item starts with a load of its state
+constexpr int kSpecChunks = ORT_PIXEL_SPEC_CHUNKS;
+inline int spec_chunk(int ns) { return (ns + kSpecChunks - 1) / kSpecChunks; }
+inline int spec_nch(int ns) { return (ns + spec_chunk(ns) - 1) / spec_chunk(ns); }
+#ifndef ORT_PIXEL_SPEC_MOVED_MAX
+#define ORT_PIXEL_SPEC_MOVED_MAX 1000
+#endif
+constexpr long long kSpecMovedMax = ORT_PIXEL_SPEC_MOVED_MAX;
+inline size_t spec_bytes(size_t slots, int ns) { return slots * ((size_t)spec_nch(ns) * 16 + (size_t)ns * 12 + 28); }
 bool use_pixel_paths(const ort_ctx* ctx, int mode, int ns, int maxd);
 
-template <int MODE, bool DEEP, bool LDS = false>
+template <int MODE, bool DEEP, bool LDS, int PM>
 int pixel_paths_blocks(int device, size_t lds, long long needed) {
     int per_cu = 0, cus = 0;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ort_pixel_paths<MODE, DEEP, LDS>, kBlock, lds);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ort_pixel_paths<MODE, DEEP, LDS, PM>, kBlock, lds);
     const long long b = (long long)std::max(per_cu, 1) * std::max(cus, 1);
     return (int)std::max(1LL, std::min(b, needed));
+}
+
+// One ort_pixel_paths launch (the variant of the scene's walk) over a persistent grid sized by
+// the variant's occupancy, at most `needed` workgroups.
+template <int PM>
+hipError_t launch_pixel_paths(const ort_ctx* ctx, int mode, bool deep, bool lds_scene, size_t lds, long long needed,
+                              const PipeArgs& a, hipStream_t s) {
+    if (mode == 2) {
+        const int g = pixel_paths_blocks<2, false, false, PM>(ctx->device, 0, needed);
+        hipLaunchKernelGGL((ort_pixel_paths<2, false, false, PM>), dim3(g), dim3(kBlock), 0, s, a);
+    } else if (deep) {
+        const int g = pixel_paths_blocks<0, true, false, PM>(ctx->device, lds, needed);
+        hipLaunchKernelGGL((ort_pixel_paths<0, true, false, PM>), dim3(g), dim3(kBlock), lds, s, a);
+    } else if (lds_scene) {
+        const int g = pixel_paths_blocks<0, false, true, PM>(ctx->device, lds, needed);
+        hipLaunchKernelGGL((ort_pixel_paths<0, false, true, PM>), dim3(g), dim3(kBlock), lds, s, a);
+    } else {
+        const int g = pixel_paths_blocks<0, false, false, PM>(ctx->device, lds, needed);
+        hipLaunchKernelGGL((ort_pixel_paths<0, false, false, PM>), dim3(g), dim3(kBlock), lds, s, a);
+    }
+    return hipGetLastError();
 }
 
 // FNV-1a of the frame shape and scene: the previous-frame hints (list lengths, walk costs)
@@ -2155,18 +2383,64 @@ int render_pixel_paths(ort_ctx* ctx, const ort_params* p, const ort_tile* t, int
     }
     ctx->sync_ok = false;
     a.sync = (int*)ctx->defer_count.p + 16 * ctx->sync_set;
+#if ORT_ANALYSIS
+    a.wclock = (ulonglong4*)ctx->wclock;  // ORT_PIXEL_CLOCK builds (tools/pixel_clock.py)
+    a.wclock_n = (int)ctx->wclock_n;
+#endif
+    const unsigned long long sig = frame_sig(ctx, p, t);
+    // samples in parallel (ORT_OPT_PIXEL_SPECULATE, ort_pixel_paths<..., SPEC>): from the second
+    // frame of a shape on, when the per-sample state buffers fit kSpecBudget; the first frame
+    // runs the pixels' chains whole and records their samples' end states
+    const int ns = p->num_samples;
+    const size_t slots = (size_t)a.total;
+    const bool spec_on = ctx->pixel_spec != 0 && ns > 1 && spec_bytes(slots, ns) <= kSpecBudget;
+    const int nch = spec_nch(ns);
+    if (!spec_on) ctx->sp_sig = 0;
+    bool spec_frame = false;
+    float2 *sp_prev = nullptr, *sp_cur = nullptr;
+    if (spec_on) {
+        const void* had = ctx->spst.p;
+        int rc;
+        if ((rc = ensure(ctx, ctx->spst, 2 * sizeof(float2) * (size_t)nch * slots)) ||
+            (rc = ensure(ctx, ctx->spcol, 3 * sizeof(float) * (size_t)ns * slots)) ||
+            (rc = ensure(ctx, ctx->spfix, (2 * sizeof(int) + sizeof(float2) + 3 * sizeof(float)) * slots)) ||
+            (rc = ensure(ctx, ctx->spfixn, 64)))
+            return rc;
+        if (ctx->spst.p != had) ctx->sp_sig = 0;  // reallocated: no recorded states
+        if (!ctx->sp_moved_host) {
+            HIPCHK(ctx, hipHostMalloc((void**)&ctx->sp_moved_host, 64, hipHostMallocDefault));
+            HIPCHK(ctx, hipEventCreateWithFlags(&ctx->sp_ev, hipEventDisableTiming));
+        }
+        if (ctx->sp_pending && hipEventQuery(ctx->sp_ev) == hipSuccess) {  // the last measurement, once it landed
+            ctx->sp_moved = ((volatile int*)ctx->sp_moved_host)[0];
+            ctx->sp_pending = false;
+        }
+        if (ctx->sp_sig != sig) {  // a fresh start: an empty fixup list, nothing measured
+            HIPCHK(ctx, hipMemsetAsync(ctx->spfixn.p, 0, 64, s));
+            ctx->sp_moved = 0;
+            ctx->sp_pending = false;
+        }
+        const long long pixels = (long long)t->width * t->rows;
+        spec_frame = ctx->sp_sig == sig && ctx->sp_moved * kSpecMovedMax <= pixels;
+        float2* st0 = (float2*)ctx->spst.p;
+        sp_prev = ctx->sp_par ? st0 + (size_t)nch * slots : st0;
+        sp_cur = ctx->sp_par ? st0 : st0 + (size_t)nch * slots;
+        a.sp_chunk = spec_chunk(ns);
+        a.sp_nch = nch;
+    }
     // heavy blocks first (ORT_OPT_PIXEL_HEAVY_FIRST; auto: several samples -- a pixel's chain is
     // then long enough for the frame's tail to matter, while one-sample frames keep tile order's
-    // locality: 1080p 1 x 4 on 10k spheres 0.89x in heavy-first order, profiles/r06/ab_blk_*)
-    const bool heavy_first = ctx->pixel_heavy_first > 0 || (ctx->pixel_heavy_first < 0 && p->num_samples > 1);
-    if (ORT_PIXEL_LPT && !heavy_first) ctx->pp_sig = 0;
+    // locality: 1080p 1 x 4 on 10k spheres 0.89x in heavy-first order, profiles/r06/ab_blk_*);
+    // not in a frame of parallel samples (nothing there is as long as a pixel's chain)
+    const bool heavy_first = !spec_frame &&
+                             (ctx->pixel_heavy_first > 0 || (ctx->pixel_heavy_first < 0 && p->num_samples > 1));
+    if (ORT_PIXEL_LPT && !heavy_first && !spec_frame) ctx->pp_sig = 0;
     if (ORT_PIXEL_LPT && heavy_first) {  // last frame's class lists (same shape) and this frame's
         const size_t nb = (size_t)blocks * (kBlock / 64), cnt_b = 2 * kPixelClasses * sizeof(int);
         int rc;
         if ((rc = ensure(ctx, ctx->pplist, 2 * kPixelClasses * 4 * nb)) || (rc = ensure(ctx, ctx->ppcnt, cnt_b)) ||
             (rc = ensure(ctx, ctx->ppcost, 8 * nb)))
             return rc;
-        const unsigned long long sig = frame_sig(ctx, p, t);
         if (ctx->pp_sig == 0 || ctx->pp_sig != sig) {  // no lists of this shape: zero counts and accumulators
             HIPCHK(ctx, hipMemsetAsync(ctx->ppcnt.p, 0, cnt_b, s));
             HIPCHK(ctx, hipMemsetAsync(ctx->ppcost.p, 0, 8 * nb, s));
@@ -2197,28 +2471,68 @@ int render_pixel_paths(ort_ctx* ctx, const ort_params* p, const ort_tile* t, int
         a.lds_sph_n16 = (int)(sph_b / 16);
         lds = (size_t)a.lds_sph_off + sph_b;
     }
-    const int g = mode == 2 ? pixel_paths_blocks<2, false>(ctx->device, lds, blocks)
-                            : (deep ? pixel_paths_blocks<0, true>(ctx->device, lds, blocks)
-                                    : (lds_scene ? pixel_paths_blocks<0, false, true>(ctx->device, lds, blocks)
-                                                 : pixel_paths_blocks<0, false>(ctx->device, lds, blocks)));
     const int fslot = (int)(ctx->frames % ort_ctx::kRing);
     ctx->tseg[fslot] = 0;
     const bool timed = !((ctx->debug_flags & 1) || !ctx->launch_times);
-    if (timed && !ctx->tr0[fslot][0]) {
-        HIPCHK(ctx, hipEventCreate(&ctx->tr0[fslot][0]));
-        HIPCHK(ctx, hipEventCreate(&ctx->tr1[fslot][0]));
-    }
+    const int nseg = spec_frame ? 3 : 1;  // SPEC: the samples, the resolve, the fixup list
+    for (int j = 0; timed && j < nseg; ++j)
+        if (!ctx->tr0[fslot][j]) {
+            HIPCHK(ctx, hipEventCreate(&ctx->tr0[fslot][j]));
+            HIPCHK(ctx, hipEventCreate(&ctx->tr1[fslot][j]));
+        }
     ctx->ev0_last = timed ? ctx->tr0[fslot][0] : ctx->ev0;  // the frame's start is its trace launch's
     HIPCHK(ctx, hipEventRecord(ctx->ev0_last, s));
-    if (mode == 2) hipLaunchKernelGGL((ort_pixel_paths<2, false, false>), dim3(g), dim3(kBlock), 0, s, a);
-    else if (deep) hipLaunchKernelGGL((ort_pixel_paths<0, true, false>), dim3(g), dim3(kBlock), lds, s, a);
-    else if (lds_scene) hipLaunchKernelGGL((ort_pixel_paths<0, false, true>), dim3(g), dim3(kBlock), lds, s, a);
-    else hipLaunchKernelGGL((ort_pixel_paths<0, false, false>), dim3(g), dim3(kBlock), lds, s, a);
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return hip_fail(ctx, e, "ort_pixel_paths launch");
+    if (!spec_frame) {  // every pixel's whole chain (recording its samples' end states when spec_on)
+        a.sp_cur = sp_cur;
+        const hipError_t e = spec_on ? launch_pixel_paths<2>(ctx, mode, deep, lds_scene, lds, blocks, a, s)
+                                     : launch_pixel_paths<0>(ctx, mode, deep, lds_scene, lds, blocks, a, s);
+        if (e != hipSuccess) return hip_fail(ctx, e, "ort_pixel_paths launch");
+        if (timed) HIPCHK(ctx, hipEventRecord(ctx->tr1[fslot][0], s));
+        if (spec_on && ctx->sp_sig == sig) {  // how many pixels moved since last frame
+            int* cnt = (int*)ctx->spfixn.p + 1;
+            a.sp_prev = sp_prev;
+            HIPCHK(ctx, hipMemsetAsync(cnt, 0, sizeof(int), s));
+            hipLaunchKernelGGL(ort_sample_moved, dim3((unsigned)((slots + 255) / 256)), dim3(256), 0, s, a, cnt);
+            hipError_t e2;
+            if ((e2 = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e2, "ort_sample_moved launch");
+            HIPCHK(ctx, hipMemcpyAsync(ctx->sp_moved_host, cnt, sizeof(int), hipMemcpyDeviceToHost, s));
+            HIPCHK(ctx, hipEventRecord(ctx->sp_ev, s));
+            ctx->sp_pending = true;
+        }
+    } else {
+        int* fx = (int*)ctx->spfix.p;
+        a.sp_prev = sp_prev;
+        a.sp_cur = sp_cur;
+        a.sp_col = (float*)ctx->spcol.p;
+        a.fx_n = (int*)ctx->spfixn.p;
+        a.fx_slot = fx;
+        a.fx_s0 = fx + slots;
+        a.fx_st = (float2*)(fx + 2 * slots);
+        a.fx_col = (float*)(fx + 4 * slots);
+        PipeArgs as = a;  // the samples: no fixup list
+        as.fx_slot = nullptr;
+        hipError_t e = launch_pixel_paths<1>(ctx, mode, deep, lds_scene, lds, blocks * nch, as, s);
+        if (e != hipSuccess) return hip_fail(ctx, e, "ort_pixel_paths (samples) launch");
+        if (timed) HIPCHK(ctx, hipEventRecord(ctx->tr1[fslot][0], s));
+        if (timed) HIPCHK(ctx, hipEventRecord(ctx->tr0[fslot][1], s));
+        hipLaunchKernelGGL(ort_sample_resolve, dim3((unsigned)((slots + 255) / 256)), dim3(256), 0, s, a);
+        if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "ort_sample_resolve launch");
+        if (timed) HIPCHK(ctx, hipEventRecord(ctx->tr1[fslot][1], s));
+        // the fixup list's length = the pixels that moved (before the fixup launch zeroes it)
+        HIPCHK(ctx, hipMemcpyAsync(ctx->sp_moved_host, a.fx_n, sizeof(int), hipMemcpyDeviceToHost, s));
+        HIPCHK(ctx, hipEventRecord(ctx->sp_ev, s));
+        ctx->sp_pending = true;
+        if (timed) HIPCHK(ctx, hipEventRecord(ctx->tr0[fslot][2], s));
+        e = launch_pixel_paths<2>(ctx, mode, deep, lds_scene, lds, blocks, a, s);  // the fixup list
+        if (e != hipSuccess) return hip_fail(ctx, e, "ort_pixel_paths (fixup) launch");
+        if (timed) HIPCHK(ctx, hipEventRecord(ctx->tr1[fslot][2], s));
+    }
+    if (spec_on) {  // this frame's end states are the next frame's
+        ctx->sp_par ^= 1;
+        ctx->sp_sig = sig;
+    }
     if (timed) {
-        HIPCHK(ctx, hipEventRecord(ctx->tr1[fslot][0], s));
-        ctx->tseg[fslot] = 1;
+        ctx->tseg[fslot] = nseg;
         ctx->frames += 1;
     }
     HIPCHK(ctx, hipEventRecord(ctx->ev1, s));
@@ -2755,7 +3069,7 @@ int ort_destroy(ort_ctx* ctx) {
     free_buf(ctx->counters);
     DevBuf* pipe[] = {&ctx->hit, &ctx->defer_list, &ctx->defer_count, &ctx->po, &ctx->pd, &ctx->pc, &ctx->prng, &ctx->pcol,
                       &ctx->qlist, &ctx->qlist2, &ctx->qcount, &ctx->qtemp, &ctx->skeys, &ctx->skeys2, &ctx->svals, &ctx->key_spread,
-                      &ctx->pcost, &ctx->bcost, &ctx->hbits, &ctx->hlist, &ctx->hcnt, &ctx->pplist, &ctx->ppcnt, &ctx->ppcost};
+                      &ctx->pcost, &ctx->bcost, &ctx->hbits, &ctx->hlist, &ctx->hcnt, &ctx->pplist, &ctx->ppcnt, &ctx->ppcost, &ctx->spst, &ctx->spcol, &ctx->spfix, &ctx->spfixn};
     for (DevBuf* b : pipe) free_buf(*b);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
@@ -2766,6 +3080,8 @@ int ort_destroy(ort_ctx* ctx) {
         }
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->alive_host) (void)hipHostFree(ctx->alive_host);
+    if (ctx->sp_moved_host) (void)hipHostFree(ctx->sp_moved_host);
+    if (ctx->sp_ev) (void)hipEventDestroy(ctx->sp_ev);
     for (hipEvent_t ev : ctx->hint_ev)
         if (ev) (void)hipEventDestroy(ev);
     if (ctx->aux_stream) {
@@ -2833,6 +3149,11 @@ int ort_set_option(ort_ctx* ctx, int option, int value) {
     if (option == ORT_OPT_PIXEL_PATHS) {
         if (value < -1 || value > 1) return fail(ctx, ORT_ERR_INVALID_ARG, "ORT_OPT_PIXEL_PATHS: -1 (auto), 0 or 1");
         ctx->pixel_paths = value;
+        return ORT_OK;
+    }
+    if (option == ORT_OPT_PIXEL_SPECULATE) {
+        if (value < -1 || value > 1) return fail(ctx, ORT_ERR_INVALID_ARG, "ORT_OPT_PIXEL_SPECULATE: -1 (auto), 0 or 1");
+        ctx->pixel_spec = value;
         return ORT_OK;
     }
     if (option == ORT_OPT_PIXEL_HEAVY_FIRST) {

@@ -128,6 +128,12 @@ class Renderer:
         """ORT_OPT_PIXEL_LDS_SCENE: 1 (default) small scenes walked from LDS copies in whole-pixel paths."""
         self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_PIXEL_LDS_SCENE, int(on)))
 
+    def set_pixel_speculate(self, mode: int):
+        """ORT_OPT_PIXEL_SPECULATE: whole-pixel paths trace a pixel's samples in parallel from last
+        frame's per-sample RNG end states (checked, re-traced where they moved); -1 (default) / 1
+        on, 0 off."""
+        self._check(self._lib.ort_set_option(self._ctx, L.ORT_OPT_PIXEL_SPECULATE, int(mode)))
+
     def set_pixel_heavy_first(self, mode: int):
         """ORT_OPT_PIXEL_HEAVY_FIRST: whole-pixel paths take the previous frame's heaviest 8x8
         blocks first; -1 (default) for frames of 2+ samples, 0 off, 1 on."""

@@ -95,4 +95,7 @@ def test_trace_kernel_names_follow_the_tile_rules(pixels, split_ok, pairs, split
     assert deep[0].startswith("ort_trace_pair_deep<false, 2>") and deep[-1].startswith("ort_trace_persistent<false, true>")
     # the reference's default config (a 585-node tree, 16 x 8): whole-pixel paths, one kernel
     small = bench.trace_kernel_names("ref_default", {"tree_depth": 3, "n_nodes": 585}, 8, 16, 800 * 600)
-    assert small == [small[0]] and small[0].startswith("ort_pixel_paths<0, false>")
+    assert len(small) == 3 and small[0].startswith("ort_pixel_paths<0, false, ..., 1>")  # samples in parallel
+    assert small[1].startswith("ort_sample_resolve") and small[2].startswith("ort_pixel_paths<0, false, ..., 2>")
+    one = bench.trace_kernel_names("c2", {"tree_depth": 6, "n_nodes": 209_000}, 4, 1, 1920 * 1080)
+    assert one == [one[0]] and one[0].startswith("ort_pixel_paths<0, false>")  # one sample: whole pixels

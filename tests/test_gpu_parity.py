@@ -463,7 +463,9 @@ def test_pixel_paths_option_and_auto(ort, oracle, scene_c1, scene_c3):
                 r.set_pixel_paths(bad)
         r.upload(s, t)
         ref = oracle.render(s, t, p)
-        for mode, launches in ((-1, 1), (1, 1), (0, None)):
+        # the first whole-pixel frame of a shape: one launch; the next: samples in parallel
+        # (ORT_OPT_PIXEL_SPECULATE), a resolve and the fixup list -- three
+        for mode, launches in ((-1, 1), (1, 3), (0, None)):
             r.set_pixel_paths(mode)
             assert_same(r.render(p), ref, f"pixel_paths={mode}")
             n = r.frame_trace_times_ms(1)[0][1]
@@ -510,6 +512,66 @@ def test_pixel_paths_lds_scene(ort, oracle, n, depth, mspn):
             assert_same(r.render(p), ref, f"n{n} d{depth} lds_scene={on}")
         with pytest.raises(ort.OrtError):
             r.set_pixel_lds_scene(2)
+
+
+@pytest.mark.parametrize("scene", ["c2", "lds", "deep", "brute"])
+def test_pixel_speculate(ort, oracle, scene_c2, scene):
+    """ORT_OPT_PIXEL_SPECULATE: from a shape's second frame on, every (pixel, sample) traced in
+    parallel from last frame's per-sample RNG end states, checked, and the pixels whose states
+    moved re-traced from the first moved sample on.  Static frames (every state holds), a camera
+    turning by small and large steps (some / most pixels re-traced), shape changes, a band tile
+    with padding rows, the LDS-resident and the depth-10 walks and brute force -- every frame the
+    oracle's, with the option on and off."""
+    if scene == "c2":
+        s, t = scene_c2
+    elif scene == "lds":
+        s = ort.random_spheres(100, 42)
+        t = ort.build_octree(s, 3, 0)
+    else:  # deep; brute force over the same 1000 spheres (the uploaded tree unused)
+        s = ort.random_spheres(1000, 42)
+        t = ort.build_octree(s, 10, 1)
+    bf = scene == "brute"
+    t_up, t = t, (None if bf else t)
+
+    def cam(W, H, ns, md, yaw=0.0):
+        from octreeraytracer_amd.scene import DEFAULT_YAW
+        return ort.FrameParams.default_camera(W, H, num_samples=ns, max_depth=md, yaw=DEFAULT_YAW + yaw,
+                                              use_octree=0 if bf else 1)
+
+    W, H = (96, 64) if bf else (160, 120)
+    shots = [(cam(W, H, 8, 6), None)] * 3                                   # static (4 chunks of 2 samples)
+    shots += [(cam(W, H, 8, 6, 0.3 * j), None) for j in (1, 2, 3)]          # small turns
+    shots += [(cam(W, H, 8, 6, 25.0), None), (cam(W, H, 8, 6, -40.0), None)]  # large jumps
+    shots += [(cam(W, H, 3, 4), None)] * 2                                  # another shape
+    shots += [(cam(320, 180, 2, 4), ort.Tile(0, 320, 150, 64, 16, 64))] * 2  # band padding
+    with ort.Renderer(0) as r:
+        for bad in (-2, 2):
+            with pytest.raises(ort.OrtError):
+                r.set_pixel_speculate(bad)
+        r.upload(s, t_up)
+        with pixel_paths(r, 1):
+            for mode in (-1, 0):
+                r.set_pixel_speculate(mode)
+                for i, (fp, tile) in enumerate(shots):
+                    if tile is None:
+                        got, ref = r.render(fp), oracle.render(s, t, fp)
+                    else:
+                        got = r.render(fp, tile)
+                        ref = oracle.render(s, t, fp, tile.x0, tile.y0, tile.width, tile.rows,
+                                            band_height=tile.band_height, band_stride=tile.band_stride)
+                    assert_same(got, ref, f"{scene} speculate={mode} frame {i}")
+                    # launches: 3 speculating, 1 running whole chains -- the first frame of a
+                    # shape (0, 8, 10) and, while pixels move (frames 4-7: the camera turns; the
+                    # frames are synchronous, so each one knows what the one before measured),
+                    # frames after one that found moved pixels
+                    n = r.frame_trace_times_ms(1)[0][1]
+                    if mode == 0 or i in (0, 8, 10):
+                        assert n == 1, (scene, mode, i, n)
+                    elif i in (1, 2, 3, 9, 11):
+                        assert n == 3, (scene, mode, i, n)
+                    else:
+                        assert n in (1, 3), (scene, mode, i, n)
+            r.set_pixel_speculate(-1)
 
 
 def test_pixel_heavy_first(ort, oracle, scene_c2):

@@ -18,7 +18,8 @@ src, dst, cfg = Path(args[0]), Path(args[1]), args[2]
 record = "--no-record" not in sys.argv
 # the production trace kernels (COUNT false): per-tile camera kernels (one or two tiles per
 # workgroup), the persistent bounce kernel, the split walks (no COUNT variant)
-TRACE_RE = re.compile(r"ort_trace_((compact_deep|compact|pair_deep|pair|persistent|kernel)<(false|0)|split<)|ort_pixel_paths<")
+TRACE_RE = re.compile(r"ort_trace_((compact_deep|compact|pair_deep|pair|persistent|kernel)<(false|0)|split<)|ort_pixel_paths<|"
+                      r"ort_sample_resolve")
 
 
 def short(name):
