@@ -876,7 +876,7 @@ def trace_kernel_names(cfg, info, maxd, ns, pixels, split_ok=True):
     below it, 1 sample; split_ok False: the caller turned the split walks off, tile pairs)."""
     deep = info["tree_depth"] > 8
     if pixel_paths_auto(info["n_nodes"], ns, maxd):
-        if ns > 1:  # the steady state: samples in parallel (ORT_OPT_PIXEL_SPECULATE), resolve, fixup list
+        if ns > 4:  # the steady state: samples in parallel (ORT_OPT_PIXEL_SPECULATE: 2+ chunks of 4+), resolve, fixup list
             return ["ort_pixel_paths<0, %s, ..., 1> (whole-pixel paths, every (pixel, sample) in parallel from last "
                     "frame's per-sample RNG end states)" % str(deep).lower(),
                     "ort_sample_resolve (each pixel's samples summed in order; pixels whose states moved listed)",

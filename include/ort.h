@@ -179,8 +179,9 @@ typedef struct ort_scene_info {
                                       chains start first and do not trail the frame; tile order otherwise.
                                       -1 (default): on for frames of 2 or more samples; 0 off; 1 on.  Same
                                       pixels (the order changes which lane traces a pixel, not its chain) */
-#define ORT_OPT_PIXEL_SPECULATE 23 /* whole-pixel paths, 2+ samples: from the second frame of a shape on,
-                                      a pixel's samples are traced as 4 chunks in parallel, chunk c
+#define ORT_OPT_PIXEL_SPECULATE 23 /* whole-pixel paths, 5+ samples: from the second frame of a shape on,
+                                      a pixel's samples are traced as up to 4 chunks (of 4 or more
+                                      samples) in parallel, chunk c
                                       starting from the RNG state chunk c-1 ended with in the previous
                                       frame (it only depends on how many draws the paths took); a pixel
                                       whose chunk ends in another state than last frame's has its later

@@ -1826,6 +1826,14 @@ struct ort_ctx {
     // while at most 1/kSpecMovedMax of the pixels moved (a moving camera: the re-traced pixels'
     // chains would set the frame's length again)
     int* sp_moved_host = nullptr;
+    // ORT_OPT_PIXEL_SPECULATE auto (-1): per shape, the first whole-chain frame's time (frame
+    // slot sp_tslot[0]) against the first speculating frame's (sp_tslot[1]) decides sp_use
+    // 0 fresh, 1 first frame done, 2 first speculating frame done (warm-up of both), 3 whole-chain
+    // frame measured, 4 speculating frame measured, 5 decided
+    int sp_tune = 0;
+    int sp_tslot[2] = {0, 0};
+    long long sp_tframe = 0;  // ctx->frames when the whole-chain side was measured
+    bool sp_use = true;
     hipEvent_t sp_ev = nullptr;
     bool sp_pending = false;
     long long sp_moved = 0;
@@ -2296,15 +2304,20 @@ constexpr size_t kSpecBudget = size_t(8) << 30;
 #ifndef ORT_PIXEL_SPEC_CHUNKS
 #define ORT_PIXEL_SPEC_CHUNKS 4
 #endif
-// a pixel's samples in (about) this many chunks: a SPEC item is one chunk of a block's pixels --
-// shorter chains with more chunks, but each item starts with a load of its state
+// a pixel's samples in (about) this many chunks of at least kSpecMinChunk samples: a SPEC item
+// is one chunk of a block's pixels -- shorter chains with more chunks, but each item starts with
+// a load of its state and a refill (one-sample chunks: 4 x 4 on 10 spheres at 1080p 0.55 ->
+// 1.69 ms; config.h's 16 x 8 in 2 / 4 / 8 chunks: 1.46 / 1.77 / 1.60x, profiles/r06/ab_spec_*)
 constexpr int kSpecChunks = ORT_PIXEL_SPEC_CHUNKS;
-inline int spec_chunk(int ns) { return (ns + kSpecChunks - 1) / kSpecChunks; }
+constexpr int kSpecMinChunk = 4;
+inline int spec_chunk(int ns) { return std::max(kSpecMinChunk, (ns + kSpecChunks - 1) / kSpecChunks); }
 inline int spec_nch(int ns) { return (ns + spec_chunk(ns) - 1) / spec_chunk(ns); }
 #ifndef ORT_PIXEL_SPEC_MOVED_MAX
 #define ORT_PIXEL_SPEC_MOVED_MAX 1000
 #endif
 constexpr long long kSpecMovedMax = ORT_PIXEL_SPEC_MOVED_MAX;
+constexpr float kSpecAutoGain = 1.0f;           // auto keeps speculating when it ran at most this x the whole-chain frame
+constexpr long long kSpecAutoPixels = 1 << 20;  // ... and without timing events, on frames of at most this many pixels
 inline size_t spec_bytes(size_t slots, int ns) { return slots * ((size_t)spec_nch(ns) * 16 + (size_t)ns * 12 + 28); }
 bool use_pixel_paths(const ort_ctx* ctx, int mode, int ns, int maxd);
 
@@ -2393,8 +2406,9 @@ int render_pixel_paths(ort_ctx* ctx, const ort_params* p, const ort_tile* t, int
     // runs the pixels' chains whole and records their samples' end states
     const int ns = p->num_samples;
     const size_t slots = (size_t)a.total;
-    const bool spec_on = ctx->pixel_spec != 0 && ns > 1 && spec_bytes(slots, ns) <= kSpecBudget;
     const int nch = spec_nch(ns);
+    const bool timed_now = !((ctx->debug_flags & 1) || !ctx->launch_times);
+    const bool spec_on = ctx->pixel_spec != 0 && nch > 1 && spec_bytes(slots, ns) <= kSpecBudget;
     if (!spec_on) ctx->sp_sig = 0;
     bool spec_frame = false;
     float2 *sp_prev = nullptr, *sp_cur = nullptr;
@@ -2415,13 +2429,32 @@ int render_pixel_paths(ort_ctx* ctx, const ort_params* p, const ort_tile* t, int
             ctx->sp_moved = ((volatile int*)ctx->sp_moved_host)[0];
             ctx->sp_pending = false;
         }
+        const long long pixels = (long long)t->width * t->rows;
         if (ctx->sp_sig != sig) {  // a fresh start: an empty fixup list, nothing measured
             HIPCHK(ctx, hipMemsetAsync(ctx->spfixn.p, 0, 64, s));
             ctx->sp_moved = 0;
             ctx->sp_pending = false;
+            ctx->sp_tune = 0;
+            // untimed contexts cannot compare: speculate on frames of at most kSpecAutoPixels
+            ctx->sp_use = ctx->pixel_spec > 0 || timed_now || pixels <= kSpecAutoPixels;
         }
-        const long long pixels = (long long)t->width * t->rows;
-        spec_frame = ctx->sp_sig == sig && ctx->sp_moved * kSpecMovedMax <= pixels;
+        if (ctx->sp_tune >= 3 && ctx->sp_tune < 5 && ctx->frames - ctx->sp_tframe >= ort_ctx::kRing - 2)
+            ctx->sp_tune = 2;  // the measured frames' timing slots are being reused: measure again
+        if (ctx->pixel_spec < 0 && ctx->sp_tune == 4) {  // auto: a measured whole-chain frame against a measured SPEC frame
+            float tw = 0.0f, tsp = 0.0f, x = 0.0f;
+            bool ok = hipEventQuery(ctx->tr1[ctx->sp_tslot[1]][2]) == hipSuccess;
+            for (int j = 0; ok && j < 3; ++j) {
+                ok = hipEventElapsedTime(&x, ctx->tr0[ctx->sp_tslot[1]][j], ctx->tr1[ctx->sp_tslot[1]][j]) == hipSuccess;
+                tsp += x;
+            }
+            if (ok) ok = hipEventElapsedTime(&tw, ctx->tr0[ctx->sp_tslot[0]][0], ctx->tr1[ctx->sp_tslot[0]][0]) == hipSuccess;
+            if (ok) {
+                ctx->sp_use = tsp < kSpecAutoGain * tw;
+                ctx->sp_tune = 5;
+            }
+        }
+        spec_frame = ctx->sp_sig == sig && ctx->sp_use && ctx->sp_moved * kSpecMovedMax <= pixels &&
+                     !(ctx->pixel_spec < 0 && timed_now && ctx->sp_tune == 2);  // auto: the measured whole-chain frame
         float2* st0 = (float2*)ctx->spst.p;
         sp_prev = ctx->sp_par ? st0 + (size_t)nch * slots : st0;
         sp_cur = ctx->sp_par ? st0 : st0 + (size_t)nch * slots;
@@ -2484,11 +2517,18 @@ int render_pixel_paths(ort_ctx* ctx, const ort_params* p, const ort_tile* t, int
     HIPCHK(ctx, hipEventRecord(ctx->ev0_last, s));
     if (!spec_frame) {  // every pixel's whole chain (recording its samples' end states when spec_on)
         a.sp_cur = sp_cur;
-        const hipError_t e = spec_on ? launch_pixel_paths<2>(ctx, mode, deep, lds_scene, lds, blocks, a, s)
-                                     : launch_pixel_paths<0>(ctx, mode, deep, lds_scene, lds, blocks, a, s);
+        const bool rec = spec_on && ctx->sp_use;  // (auto found speculation slower on this shape: no recording)
+        const hipError_t e = rec ? launch_pixel_paths<2>(ctx, mode, deep, lds_scene, lds, blocks, a, s)
+                                 : launch_pixel_paths<0>(ctx, mode, deep, lds_scene, lds, blocks, a, s);
         if (e != hipSuccess) return hip_fail(ctx, e, "ort_pixel_paths launch");
         if (timed) HIPCHK(ctx, hipEventRecord(ctx->tr1[fslot][0], s));
-        if (spec_on && ctx->sp_sig == sig) {  // how many pixels moved since last frame
+        if (rec && timed && ctx->sp_tune == 0) ctx->sp_tune = 1;  // auto: a shape's first frame (not measured)
+        if (rec && timed && ctx->sp_tune == 2) {  // auto: this frame's time is the whole-chain side
+            ctx->sp_tslot[0] = fslot;
+            ctx->sp_tframe = ctx->frames;
+            ctx->sp_tune = 3;
+        }
+        if (rec && ctx->sp_sig == sig) {  // how many pixels moved since last frame
             int* cnt = (int*)ctx->spfixn.p + 1;
             a.sp_prev = sp_prev;
             HIPCHK(ctx, hipMemsetAsync(cnt, 0, sizeof(int), s));
@@ -2526,6 +2566,11 @@ int render_pixel_paths(ort_ctx* ctx, const ort_params* p, const ort_tile* t, int
         e = launch_pixel_paths<2>(ctx, mode, deep, lds_scene, lds, blocks, a, s);  // the fixup list
         if (e != hipSuccess) return hip_fail(ctx, e, "ort_pixel_paths (fixup) launch");
         if (timed) HIPCHK(ctx, hipEventRecord(ctx->tr1[fslot][2], s));
+        if (timed && ctx->sp_tune == 1) ctx->sp_tune = 2;  // auto: the first speculating frame (not measured)
+        if (timed && ctx->sp_tune == 3) {  // auto: ... and this one's the speculating side
+            ctx->sp_tslot[1] = fslot;
+            ctx->sp_tune = 4;
+        }
     }
     if (spec_on) {  // this frame's end states are the next frame's
         ctx->sp_par ^= 1;

@@ -456,7 +456,7 @@ def test_pixel_paths_option_and_auto(ort, oracle, scene_c1, scene_c3):
     small tree's multi-bounce frame in ONE trace launch and the C3 tree's (10.9 M nodes) with
     the per-bounce pipeline; primary-ray frames (1 sample, 1 bounce) never take it."""
     s, t = scene_c1
-    p = ort.FrameParams.default_camera(128, 96, num_samples=4, max_depth=6)
+    p = ort.FrameParams.default_camera(128, 96, num_samples=8, max_depth=6)
     with ort.Renderer(0) as r:
         for bad in (-2, 2):
             with pytest.raises(ort.OrtError):
@@ -539,18 +539,18 @@ def test_pixel_speculate(ort, oracle, scene_c2, scene):
                                               use_octree=0 if bf else 1)
 
     W, H = (96, 64) if bf else (160, 120)
-    shots = [(cam(W, H, 8, 6), None)] * 3                                   # static (4 chunks of 2 samples)
+    shots = [(cam(W, H, 8, 6), None)] * 3                                   # static (2 chunks of 4 samples)
     shots += [(cam(W, H, 8, 6, 0.3 * j), None) for j in (1, 2, 3)]          # small turns
     shots += [(cam(W, H, 8, 6, 25.0), None), (cam(W, H, 8, 6, -40.0), None)]  # large jumps
-    shots += [(cam(W, H, 3, 4), None)] * 2                                  # another shape
-    shots += [(cam(320, 180, 2, 4), ort.Tile(0, 320, 150, 64, 16, 64))] * 2  # band padding
+    shots += [(cam(W, H, 12, 4), None)] * 2                                 # another shape: 3 chunks
+    shots += [(cam(320, 180, 9, 4), ort.Tile(0, 320, 150, 64, 16, 64))] * 2  # band padding, a 1-sample chunk
     with ort.Renderer(0) as r:
         for bad in (-2, 2):
             with pytest.raises(ort.OrtError):
                 r.set_pixel_speculate(bad)
         r.upload(s, t_up)
         with pixel_paths(r, 1):
-            for mode in (-1, 0):
+            for mode in (1, -1, 0):  # on, auto (timed per shape: either way), off
                 r.set_pixel_speculate(mode)
                 for i, (fp, tile) in enumerate(shots):
                     if tile is None:
@@ -567,7 +567,7 @@ def test_pixel_speculate(ort, oracle, scene_c2, scene):
                     n = r.frame_trace_times_ms(1)[0][1]
                     if mode == 0 or i in (0, 8, 10):
                         assert n == 1, (scene, mode, i, n)
-                    elif i in (1, 2, 3, 9, 11):
+                    elif mode == 1 and i in (1, 2, 3, 9, 11):
                         assert n == 3, (scene, mode, i, n)
                     else:
                         assert n in (1, 3), (scene, mode, i, n)
