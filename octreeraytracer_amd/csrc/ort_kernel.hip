@@ -1472,14 +1472,14 @@ ort_pixel_paths(PipeArgs A) {
     const int n_blocks = A.total >> 6;
     const int n_items = SPEC ? n_blocks * A.sp_nch : (fixup ? (*A.fx_n + 63) >> 6 : n_blocks);
     int cls_end = 0;
-    if (ORT_PIXEL_LPT && !SPEC && A.pl_r) {
+    if (ORT_PIXEL_LPT && A.pl_r) {
         cls_end = lane < kPixelClasses ? A.pl_rcnt[lane] : 0;
         for (int d = 1; d < kPixelClasses; d <<= 1) {
             const int v = __shfl_up(cls_end, d);
             if (lane >= d) cls_end += v;
         }
     }
-    const bool listed = ORT_PIXEL_LPT && !SPEC && !fixup && A.pl_r && __shfl(cls_end, kPixelClasses - 1) == n_blocks;
+    const bool listed = ORT_PIXEL_LPT && !fixup && A.pl_r && __shfl(cls_end, kPixelClasses - 1) == n_blocks;
     int k = -1;              // the lane's path slot (pixel), -1 idle
     int nb = 0;              // bounces traced for the lane's pixel so far (its cost class)
     int px = 0, py = 0, s = 0, b = 0;
@@ -1516,23 +1516,21 @@ ort_pixel_paths(PipeArgs A) {
                 j = __shfl(j, 0);
                 if (j >= n_items) {
                     drained = true;
-                } else if (SPEC) {  // block j / nch, its pixels' chunk j % nch
-                    next = (j / A.sp_nch) << 6;
-                    end = next + 64;
-                    item_s = j % A.sp_nch;
                 } else if (fixup) {
                     next = j << 6;
                     end = min(next + 64, *A.fx_n);
-                } else {
-                    int blk = j;
-                    if (listed) {  // item j of the class lists: class q = the first with j < its prefix end
-                        const unsigned long long in = __ballot(lane < kPixelClasses && j < cls_end);
+                } else {  // SPEC: block j / nch (its pixels' chunk j % nch), heavy blocks first as well
+                    const int jb = SPEC ? j / A.sp_nch : j;
+                    int blk = jb;
+                    if (listed) {  // item jb of the class lists: class q = the first with jb < its prefix end
+                        const unsigned long long in = __ballot(lane < kPixelClasses && jb < cls_end);
                         const int q = __builtin_ctzll(in);
                         const int before = q ? __shfl(cls_end, q - 1) : 0;
-                        blk = A.pl_r[(size_t)q * A.pl_stride + (j - before)];
+                        blk = A.pl_r[(size_t)q * A.pl_stride + (jb - before)];
                     }
                     next = blk << 6;
                     end = next + 64;
+                    if (SPEC) item_s = j - jb * A.sp_nch;
                 }
             }
             if (!drained) {
@@ -1667,7 +1665,7 @@ ort_pixel_paths(PipeArgs A) {
             atomicExch(A.sync + 2, 0);
             if (fixup) atomicExch(A.fx_n, 0);
             // the class counts read this frame become the next frame's write counts
-            if (ORT_PIXEL_LPT && A.pl_rcnt)
+            if (ORT_PIXEL_LPT && A.pl_rcnt && !SPEC)  // (SPEC frames read the lists, and keep them)
                 for (int q = 0; q < kPixelClasses; ++q) atomicExch(A.pl_rcnt + q, 0);
         }
     }
@@ -2549,8 +2547,15 @@ int render_pixel_paths(ort_ctx* ctx, const ort_params* p, const ort_tile* t, int
         a.fx_s0 = fx + slots;
         a.fx_st = (float2*)(fx + 2 * slots);
         a.fx_col = (float*)(fx + 4 * slots);
-        PipeArgs as = a;  // the samples: no fixup list
-        as.fx_slot = nullptr;
+        PipeArgs as = a;  // the samples: no fixup list; heavy blocks first by the lists the last
+        as.fx_slot = nullptr;  // whole-chain frame of this shape wrote (read only: SPEC frames keep them)
+        if (ORT_PIXEL_LPT && ctx->pp_sig == sig && ctx->pplist.p) {
+            const size_t nbk = (size_t)blocks * (kBlock / 64);
+            const int r = ctx->pp_par ^ 1;
+            as.pl_stride = (int)nbk;
+            as.pl_r = (int*)ctx->pplist.p + (size_t)r * kPixelClasses * nbk;
+            as.pl_rcnt = (int*)ctx->ppcnt.p + kPixelClasses * r;
+        }
         hipError_t e = launch_pixel_paths<1>(ctx, mode, deep, lds_scene, lds, blocks * nch, as, s);
         if (e != hipSuccess) return hip_fail(ctx, e, "ort_pixel_paths (samples) launch");
         if (timed) HIPCHK(ctx, hipEventRecord(ctx->tr1[fslot][0], s));
