@@ -2315,7 +2315,8 @@ inline int spec_nch(int ns) { return (ns + spec_chunk(ns) - 1) / spec_chunk(ns);
 #endif
 constexpr long long kSpecMovedMax = ORT_PIXEL_SPEC_MOVED_MAX;
 constexpr float kSpecAutoGain = 1.0f;           // auto keeps speculating when it ran at most this x the whole-chain frame
-constexpr long long kSpecAutoPixels = 1 << 20;  // ... and without timing events, on frames of at most this many pixels
+constexpr long long kSpecAutoPixels = 1 << 20;
+constexpr long long kSpecFixupQuietWgs = 32;  // ... and without timing events, on frames of at most this many pixels
 inline size_t spec_bytes(size_t slots, int ns) { return slots * ((size_t)spec_nch(ns) * 16 + (size_t)ns * 12 + 28); }
 bool use_pixel_paths(const ort_ctx* ctx, int mode, int ns, int maxd);
 
@@ -2568,7 +2569,9 @@ int render_pixel_paths(ort_ctx* ctx, const ort_params* p, const ort_tile* t, int
         HIPCHK(ctx, hipEventRecord(ctx->sp_ev, s));
         ctx->sp_pending = true;
         if (timed) HIPCHK(ctx, hipEventRecord(ctx->tr0[fslot][2], s));
-        e = launch_pixel_paths<2>(ctx, mode, deep, lds_scene, lds, blocks, a, s);  // the fixup list
+        // the fixup list: a few workgroups while the last measured frame moved no pixel (the list
+        // is then empty or short), else the whole persistent grid
+        e = launch_pixel_paths<2>(ctx, mode, deep, lds_scene, lds, ctx->sp_moved == 0 ? kSpecFixupQuietWgs : blocks, a, s);
         if (e != hipSuccess) return hip_fail(ctx, e, "ort_pixel_paths (fixup) launch");
         if (timed) HIPCHK(ctx, hipEventRecord(ctx->tr1[fslot][2], s));
         if (timed && ctx->sp_tune == 1) ctx->sp_tune = 2;  // auto: the first speculating frame (not measured)
