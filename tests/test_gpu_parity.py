@@ -601,3 +601,36 @@ def test_pixel_heavy_first(ort, oracle, scene_c2):
                     got = r.render(fp, tile) if tile else r.render(fp)
                     assert_same(got, refs[name], f"heavy_first={mode} {name}")
             r.set_pixel_heavy_first(-1)
+
+
+def test_pixel_speculate_stream_ordered_and_group(ort, oracle, scene_c2):
+    """Speculating frames queued back to back on a caller stream (device output, no host wait
+    between them: the moved-pixel counts and the auto mode's timings are read only once their
+    events completed), on two contexts alternating, and on a one-GPU render group's band
+    contexts -- every frame the synchronous whole-chain render's."""
+    torch = pytest.importorskip("torch")
+    from octreeraytracer_amd.group import RenderGroup
+    s, t = scene_c2
+    W, H = 200, 136
+    p = ort.FrameParams.default_camera(W, H, num_samples=8, max_depth=5)
+    ref = oracle.render(s, t, p)
+    rs = [ort.Renderer(0) for _ in range(2)]
+    try:
+        for x in rs:
+            x.upload(s, t)
+            x.set_pixel_paths(1)
+        st = torch.cuda.Stream()
+        outs = [torch.full((H, W, 3), -1.0, dtype=torch.float32, device="cuda:0") for _ in range(12)]
+        for k, o in enumerate(outs):
+            rs[k % 2].render(p, out=o, stream=st.cuda_stream)
+        st.synchronize()
+        for k, o in enumerate(outs):
+            assert_same(o.cpu().numpy(), ref, f"stream-ordered frame {k}")
+        assert any(n == 3 for _, n in rs[0].frame_trace_times_ms(6))  # some of them speculated
+    finally:
+        for x in rs:
+            x.close()
+    with RenderGroup([0, 0, 0], 1) as g:
+        g.upload(s, t)
+        for k in range(5):
+            assert_same(g.render(p), ref, f"group frame {k}")
