@@ -138,6 +138,10 @@ struct PipeArgs {
     float2* sp_cur;
     float* sp_col;
     int sp_chunk, sp_nch;  // samples per SPEC item (a chunk of a pixel's samples), chunks per pixel
+    // sp_ctl[0] the fixup list's length, [1] the pixels the last frame found moved, [2] this
+    // frame's mode (1 speculate, 0 fall back: every pixel's whole chain through the fixup list)
+    // -- decided on the device by ort_sample_decide, so frames queued ahead of the host follow it
+    int* sp_ctl;
     int* fx_n;
     int* fx_slot;
     int* fx_s0;
@@ -1447,6 +1451,21 @@ template <int MODE, bool DEEP, bool LDS, int PM = 0>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ORT_PIXEL_WAVES)))
 ort_pixel_paths(PipeArgs A) {
     constexpr bool SPEC = PM == 1;
+    // a SPEC launch in a fall-back frame, and the fixup launch's workgroups beyond what its list
+    // needs, only count themselves out (before any LDS set-up)
+    const bool idle_wg = (SPEC && A.sp_ctl[2] == 0) ||
+                         (PM == 2 && A.fx_slot && (long long)blockIdx.x * kBlock >= (long long)*A.fx_n + kBlock);
+    if (idle_wg) {
+        if (threadIdx.x == 0 && atomicAdd(A.sync + 2, 1) == (int)gridDim.x - 1) {
+            atomicExch(A.sync + 1, 0);
+            atomicExch(A.sync + 2, 0);
+            if (PM == 2 && A.fx_slot) {
+                if (A.sp_ctl[2]) atomicExch(A.sp_ctl + 1, *A.fx_n);  // speculated: the list = the moved pixels
+                atomicExch(A.fx_n, 0);
+            }
+        }
+        return;
+    }
     extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];  // plane tables: 1 KiB-aligned
     LdsView L{};
     ort::KScene S = A.S;
@@ -1663,7 +1682,10 @@ ort_pixel_paths(PipeArgs A) {
         if (atomicAdd(A.sync + 2, 1) == (int)gridDim.x - 1) {
             atomicExch(A.sync + 1, 0);
             atomicExch(A.sync + 2, 0);
-            if (fixup) atomicExch(A.fx_n, 0);
+            if (fixup) {
+                if (A.sp_ctl[2]) atomicExch(A.sp_ctl + 1, *A.fx_n);  // speculated: the list = the moved pixels
+                atomicExch(A.fx_n, 0);
+            }
             // the class counts read this frame become the next frame's write counts
             if (ORT_PIXEL_LPT && A.pl_rcnt && !SPEC)  // (SPEC frames read the lists, and keep them)
                 for (int q = 0; q < kPixelClasses; ++q) atomicExch(A.pl_rcnt + q, 0);
@@ -1686,6 +1708,18 @@ __global__ void __launch_bounds__(256) ort_sample_resolve(PipeArgs A) {
         return;
     }
     const int ns = A.pp.ns;
+    if (A.sp_ctl[2] == 0) {  // a fall-back frame: the whole chain from sample 0
+        ort_rng st;
+        ort::pixel_rng_init(A.pp, A.tm.x0 + cx, tile_row_to_y(A.tm, cy), st);
+        const int e = atomicAdd(A.fx_n, 1);
+        A.fx_slot[e] = k;
+        A.fx_s0[e] = 0;
+        A.fx_st[e] = make_float2(st.x, st.y);
+        A.fx_col[e] = 0.0f;
+        A.fx_col[(size_t)A.total + e] = 0.0f;
+        A.fx_col[2 * (size_t)A.total + e] = 0.0f;
+        return;
+    }
     int bad = A.sp_nch - 1;  // the first chunk whose end state moved (the last: none did)
     for (int c = 0; c < A.sp_nch - 1; ++c) {
         const size_t i = (size_t)c * A.total + k;
@@ -1716,10 +1750,21 @@ __global__ void __launch_bounds__(256) ort_sample_resolve(PipeArgs A) {
     A.fx_col[2 * (size_t)A.total + e] = col.z;
 }
 
+// The mode of a frame whose states last frame recorded: speculate while at most 1/kSpecMovedMax
+// of the pixels moved last frame (sp_ctl[1]), else fall back; a fall-back frame recounts them.
+__global__ void ort_sample_decide(int* ctl, long long pixels, long long moved_max) {
+    if (threadIdx.x == 0) {
+        const int spec = (long long)ctl[1] * moved_max <= pixels;
+        ctl[2] = spec;
+        if (!spec) ctl[1] = 0;
+    }
+}
+
 // A frame that ran the pixels' chains whole (recording their chunk end states): the pixels whose
 // chunk end states differ from last frame's -- the ones a SPEC frame would have re-traced -- into
 // *count (the camera or the scene moved: the next frame then does not speculate).
 __global__ void __launch_bounds__(256) ort_sample_moved(PipeArgs A, int* count) {
+    if (A.sp_ctl[2] != 0) return;  // a speculating frame: its fixup list counted them
     const int k = (int)(blockIdx.x * 256 + threadIdx.x);
     bool moved = false;
     int cx, cy;
@@ -1819,22 +1864,16 @@ struct ort_ctx {
     DevBuf spst, spcol, spfix, spfixn;
     int sp_par = 0;
     unsigned long long sp_sig = 0;
-    // the pixels the last measured frame found moved (re-traced by a SPEC frame, or counted by
-    // ort_sample_moved), copied to pinned memory behind sp_ev; the next frame speculates only
-    // while at most 1/kSpecMovedMax of the pixels moved (a moving camera: the re-traced pixels'
-    // chains would set the frame's length again)
-    int* sp_moved_host = nullptr;
-    // ORT_OPT_PIXEL_SPECULATE auto (-1): per shape, the first whole-chain frame's time (frame
-    // slot sp_tslot[0]) against the first speculating frame's (sp_tslot[1]) decides sp_use
+    // (the pixels a frame found moved, and whether the next one speculates: spfixn, PipeArgs::sp_ctl)
+    // ORT_OPT_PIXEL_SPECULATE auto (-1): per shape, a whole-chain frame's time (frame slot
+    // sp_tslot[0]) against a speculating frame's (sp_tslot[1]) decides sp_use
     // 0 fresh, 1 first frame done, 2 first speculating frame done (warm-up of both), 3 whole-chain
     // frame measured, 4 speculating frame measured, 5 decided
     int sp_tune = 0;
     int sp_tslot[2] = {0, 0};
     long long sp_tframe = 0;  // ctx->frames when the whole-chain side was measured
     bool sp_use = true;
-    hipEvent_t sp_ev = nullptr;
-    bool sp_pending = false;
-    long long sp_moved = 0;
+
     int pixel_spec = -1;  // ORT_OPT_PIXEL_SPECULATE: -1 auto, 0 off, 1 on
     int pp_par = 0;
     unsigned long long pp_sig = 0;
@@ -2315,8 +2354,7 @@ inline int spec_nch(int ns) { return (ns + spec_chunk(ns) - 1) / spec_chunk(ns);
 #endif
 constexpr long long kSpecMovedMax = ORT_PIXEL_SPEC_MOVED_MAX;
 constexpr float kSpecAutoGain = 1.0f;           // auto keeps speculating when it ran at most this x the whole-chain frame
-constexpr long long kSpecAutoPixels = 1 << 20;
-constexpr long long kSpecFixupQuietWgs = 32;  // ... and without timing events, on frames of at most this many pixels
+constexpr long long kSpecAutoPixels = 1 << 20;  // ... and without timing events, on frames of at most this many pixels
 inline size_t spec_bytes(size_t slots, int ns) { return slots * ((size_t)spec_nch(ns) * 16 + (size_t)ns * 12 + 28); }
 bool use_pixel_paths(const ort_ctx* ctx, int mode, int ns, int maxd);
 
@@ -2420,19 +2458,9 @@ int render_pixel_paths(ort_ctx* ctx, const ort_params* p, const ort_tile* t, int
             (rc = ensure(ctx, ctx->spfixn, 64)))
             return rc;
         if (ctx->spst.p != had) ctx->sp_sig = 0;  // reallocated: no recorded states
-        if (!ctx->sp_moved_host) {
-            HIPCHK(ctx, hipHostMalloc((void**)&ctx->sp_moved_host, 64, hipHostMallocDefault));
-            HIPCHK(ctx, hipEventCreateWithFlags(&ctx->sp_ev, hipEventDisableTiming));
-        }
-        if (ctx->sp_pending && hipEventQuery(ctx->sp_ev) == hipSuccess) {  // the last measurement, once it landed
-            ctx->sp_moved = ((volatile int*)ctx->sp_moved_host)[0];
-            ctx->sp_pending = false;
-        }
         const long long pixels = (long long)t->width * t->rows;
-        if (ctx->sp_sig != sig) {  // a fresh start: an empty fixup list, nothing measured
+        if (ctx->sp_sig != sig) {  // a fresh start: an empty fixup list, nothing moved
             HIPCHK(ctx, hipMemsetAsync(ctx->spfixn.p, 0, 64, s));
-            ctx->sp_moved = 0;
-            ctx->sp_pending = false;
             ctx->sp_tune = 0;
             // untimed contexts cannot compare: speculate on frames of at most kSpecAutoPixels
             ctx->sp_use = ctx->pixel_spec > 0 || timed_now || pixels <= kSpecAutoPixels;
@@ -2452,8 +2480,9 @@ int render_pixel_paths(ort_ctx* ctx, const ort_params* p, const ort_tile* t, int
                 ctx->sp_tune = 5;
             }
         }
-        spec_frame = ctx->sp_sig == sig && ctx->sp_use && ctx->sp_moved * kSpecMovedMax <= pixels &&
+        spec_frame = ctx->sp_sig == sig && ctx->sp_use &&
                      !(ctx->pixel_spec < 0 && timed_now && ctx->sp_tune == 2);  // auto: the measured whole-chain frame
+        a.sp_ctl = (int*)ctx->spfixn.p;
         float2* st0 = (float2*)ctx->spst.p;
         sp_prev = ctx->sp_par ? st0 + (size_t)nch * slots : st0;
         sp_cur = ctx->sp_par ? st0 : st0 + (size_t)nch * slots;
@@ -2527,16 +2556,13 @@ int render_pixel_paths(ort_ctx* ctx, const ort_params* p, const ort_tile* t, int
             ctx->sp_tframe = ctx->frames;
             ctx->sp_tune = 3;
         }
-        if (rec && ctx->sp_sig == sig) {  // how many pixels moved since last frame
+        if (rec && ctx->sp_sig == sig) {  // how many pixels moved since last frame (mode word 0: count)
             int* cnt = (int*)ctx->spfixn.p + 1;
             a.sp_prev = sp_prev;
-            HIPCHK(ctx, hipMemsetAsync(cnt, 0, sizeof(int), s));
+            HIPCHK(ctx, hipMemsetAsync(cnt, 0, 2 * sizeof(int), s));
             hipLaunchKernelGGL(ort_sample_moved, dim3((unsigned)((slots + 255) / 256)), dim3(256), 0, s, a, cnt);
             hipError_t e2;
             if ((e2 = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e2, "ort_sample_moved launch");
-            HIPCHK(ctx, hipMemcpyAsync(ctx->sp_moved_host, cnt, sizeof(int), hipMemcpyDeviceToHost, s));
-            HIPCHK(ctx, hipEventRecord(ctx->sp_ev, s));
-            ctx->sp_pending = true;
         }
     } else {
         int* fx = (int*)ctx->spfix.p;
@@ -2557,23 +2583,24 @@ int render_pixel_paths(ort_ctx* ctx, const ort_params* p, const ort_tile* t, int
             as.pl_r = (int*)ctx->pplist.p + (size_t)r * kPixelClasses * nbk;
             as.pl_rcnt = (int*)ctx->ppcnt.p + kPixelClasses * r;
         }
-        hipError_t e = launch_pixel_paths<1>(ctx, mode, deep, lds_scene, lds, blocks * nch, as, s);
+        hipLaunchKernelGGL(ort_sample_decide, dim3(1), dim3(64), 0, s, a.sp_ctl, (long long)t->width * t->rows, kSpecMovedMax);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return hip_fail(ctx, e, "ort_sample_decide launch");
+        e = launch_pixel_paths<1>(ctx, mode, deep, lds_scene, lds, blocks * nch, as, s);
         if (e != hipSuccess) return hip_fail(ctx, e, "ort_pixel_paths (samples) launch");
         if (timed) HIPCHK(ctx, hipEventRecord(ctx->tr1[fslot][0], s));
         if (timed) HIPCHK(ctx, hipEventRecord(ctx->tr0[fslot][1], s));
         hipLaunchKernelGGL(ort_sample_resolve, dim3((unsigned)((slots + 255) / 256)), dim3(256), 0, s, a);
         if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "ort_sample_resolve launch");
         if (timed) HIPCHK(ctx, hipEventRecord(ctx->tr1[fslot][1], s));
-        // the fixup list's length = the pixels that moved (before the fixup launch zeroes it)
-        HIPCHK(ctx, hipMemcpyAsync(ctx->sp_moved_host, a.fx_n, sizeof(int), hipMemcpyDeviceToHost, s));
-        HIPCHK(ctx, hipEventRecord(ctx->sp_ev, s));
-        ctx->sp_pending = true;
         if (timed) HIPCHK(ctx, hipEventRecord(ctx->tr0[fslot][2], s));
-        // the fixup list: a few workgroups while the last measured frame moved no pixel (the list
-        // is then empty or short), else the whole persistent grid
-        e = launch_pixel_paths<2>(ctx, mode, deep, lds_scene, lds, ctx->sp_moved == 0 ? kSpecFixupQuietWgs : blocks, a, s);
+        // the fixup list (the workgroups beyond what it needs leave at once); in a fall-back frame
+        // every pixel's chain, then the count of the pixels that moved
+        e = launch_pixel_paths<2>(ctx, mode, deep, lds_scene, lds, blocks, a, s);
         if (e != hipSuccess) return hip_fail(ctx, e, "ort_pixel_paths (fixup) launch");
         if (timed) HIPCHK(ctx, hipEventRecord(ctx->tr1[fslot][2], s));
+        hipLaunchKernelGGL(ort_sample_moved, dim3((unsigned)((slots + 255) / 256)), dim3(256), 0, s, a, a.sp_ctl + 1);
+        if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "ort_sample_moved launch");
         if (timed && ctx->sp_tune == 1) ctx->sp_tune = 2;  // auto: the first speculating frame (not measured)
         if (timed && ctx->sp_tune == 3) {  // auto: ... and this one's the speculating side
             ctx->sp_tslot[1] = fslot;
@@ -3133,8 +3160,6 @@ int ort_destroy(ort_ctx* ctx) {
         }
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->alive_host) (void)hipHostFree(ctx->alive_host);
-    if (ctx->sp_moved_host) (void)hipHostFree(ctx->sp_moved_host);
-    if (ctx->sp_ev) (void)hipEventDestroy(ctx->sp_ev);
     for (hipEvent_t ev : ctx->hint_ev)
         if (ev) (void)hipEventDestroy(ev);
     if (ctx->aux_stream) {
